@@ -1,0 +1,267 @@
+"""Functional fp32 CPU restatement of the reference's hot-path modules (oracle).
+
+Test infrastructure only (see oracle/__init__.py).  Parameters come from a flat
+`state_dict` using the reference's own keys; `p` is the key prefix of the module.
+All citations are relative to /root/reference/src.
+"""
+import math
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+__all__ = [
+    "crop_nd", "conv2d_ref", "conv_transpose_ref", "spectral_conv2d", "spectral_conv3d", "fno_layer", "fno",
+    "residual_block", "unet_modern", "dilated_resnet", "ufno", "enc_elementwise", "add_delta",
+    "dec_timeconvdense", "unet_structure",
+]
+
+
+def _j(p, s):
+    """Join a state_dict key prefix (no trailing dot; '' = root) with a child name."""
+    return f"{p}.{s}" if p else s
+
+
+def gelu(x):
+    return F.gelu(x)  # nn.GELU() default: erf form
+
+
+def crop_nd(enc_ftrs, shape, num_spatial_dims=2):
+    """common.py:20-34 — zero-pad (or crop) the trailing spatial dims to `shape`.
+
+    The ±0.001 tie-break rounds the first pad of each dim up and the second down
+    when the size difference is odd."""
+    s_des = tuple(shape)[-num_spatial_dims:]
+    s_cur = enc_ftrs.shape[-num_spatial_dims:]
+    pad_temp = np.repeat(np.subtract(s_des, s_cur) / 2, 2)
+    breaking = np.tile([1, -1], int(len(pad_temp) / 2)) / 1000
+    pad = tuple(reversed(tuple(map(lambda q: int(round(q)), pad_temp + breaking))))
+    return F.pad(enc_ftrs, pad)
+
+
+def conv2d_ref(x, sd, p, stride=1, padding=0, dilation=1, padding_mode="zeros"):
+    """nn.Conv2d as constructed by get_conv_with_right_spatial_dim (common.py:37-47).
+
+    padding='same' with circular mode pads d*(k-1) total, left = total//2
+    (torch.nn.modules.conv._ConvNd semantics)."""
+    w = sd[_j(p, "weight")]
+    b = sd.get(_j(p, "bias"))
+    if padding_mode != "zeros":
+        k = w.shape[-1]
+        if padding == "same":
+            total = dilation * (k - 1)
+            lo = total // 2
+            pads = (lo, total - lo, lo, total - lo)
+        else:
+            pads = (padding,) * 4
+        if any(pads):
+            x = F.pad(x, pads, mode="circular")
+        return F.conv2d(x, w, b, stride=stride, padding=0, dilation=dilation)
+    return F.conv2d(x, w, b, stride=stride, padding=padding, dilation=dilation)
+
+
+def conv_transpose_ref(x, sd, p, stride, padding=0, circ_pre_pad=0):
+    """common.py:61-120: ConvTranspose2d, optionally after circular_pad_2d (ConvTranspose2d_padded)."""
+    if circ_pre_pad:
+        c = circ_pre_pad
+        x = torch.cat([x[..., -c:], x, x[..., :c]], dim=-1)    # common.py:81-83
+        x = torch.cat([x[..., -c:, :], x, x[..., :c, :]], dim=-2)  # common.py:86-88
+    return F.conv_transpose2d(x, sd[_j(p, "weight")], sd.get(_j(p, "bias")), stride=stride, padding=padding)
+
+
+# ---------------------------------------------------------------- spectral ----
+def spectral_conv2d(x, w1, w2):
+    """SpectralConv2d.forward, proc_fno.py:257-288 (FiLM branch unused)."""
+    m1, m2 = w1.shape[-2], w1.shape[-1]
+    B = x.shape[0]
+    x_ft = torch.fft.rfft2(x)
+    out_ft = torch.zeros(B, w1.shape[1], x.size(-2), x.size(-1) // 2 + 1, dtype=torch.cfloat)
+    out_ft[:, :, :m1, :m2] = torch.einsum("bixy,ioxy->boxy", x_ft[:, :, :m1, :m2], w1)
+    out_ft[:, :, -m1:, :m2] = torch.einsum("bixy,ioxy->boxy", x_ft[:, :, -m1:, :m2], w2)
+    return torch.fft.irfft2(out_ft, s=(x.size(-2), x.size(-1)))
+
+
+def spectral_conv3d(x, w1, w2, w3, w4):
+    """SpectralConv3d.forward, proc_fno.py:334-376 (FiLM branch unused)."""
+    m1, m2, m3 = w1.shape[-3:]
+    B = x.shape[0]
+    x_ft = torch.fft.rfftn(x, dim=[-3, -2, -1])
+    out_ft = torch.zeros(B, w1.shape[1], x.size(-3), x.size(-2), x.size(-1) // 2 + 1, dtype=torch.cfloat)
+    mul = lambda a, w: torch.einsum("bixyz,ioxyz->boxyz", a, w)
+    out_ft[:, :, :m1, :m2, :m3] = mul(x_ft[:, :, :m1, :m2, :m3], w1)
+    out_ft[:, :, -m1:, :m2, :m3] = mul(x_ft[:, :, -m1:, :m2, :m3], w2)
+    out_ft[:, :, :m1, -m2:, :m3] = mul(x_ft[:, :, :m1, -m2:, :m3], w3)
+    out_ft[:, :, -m1:, -m2:, :m3] = mul(x_ft[:, :, -m1:, -m2:, :m3], w4)
+    return torch.fft.irfftn(out_ft, s=(x.size(-3), x.size(-2), x.size(-1)))
+
+
+def fno_layer(sd, p, x, activation=True, padding_mode="circular", conv_mode="single"):
+    """FNO_Layer.forward, proc_fno.py:133-155: spectral(x) + w(x) [+ w2(x)], then GELU if activation."""
+    x1 = spectral_conv2d(x, sd[_j(p, "conv.weights1")], sd[_j(p, "conv.weights2")])
+    x2 = conv2d_ref(x, sd, _j(p, "w"), padding="same", padding_mode=padding_mode)
+    y = x1 + x2
+    if conv_mode == "double":
+        y = y + conv2d_ref(x, sd, _j(p, "w2"), padding="same", padding_mode=padding_mode)
+    return gelu(y) if activation else y
+
+
+def fno(sd, p, cfg, h, vb):
+    """FNO.forward, proc_fno.py:73-83 (cond_mode='concat')."""
+    pm = cfg.get("padding_mode", "circular")
+    pm = pm if pm != "ones" else "zeros"
+    for i in range(cfg.get("hidden_blocks", 4)):
+        h_in = torch.cat([h, vb], dim=1) if vb is not None else h
+        h = fno_layer(sd, _j(p, f"fno_layers.{i}"), h_in, activation=True, padding_mode=pm,
+                      conv_mode=cfg.get("fno_conv_mode", "single"))
+    return h
+
+
+# ------------------------------------------------------------------ U-Net -----
+def residual_block(sd, p, x, norm, pad_kw):
+    """ResidualBlock.forward, proc_unet_modern.py:243-250 (GroupNorm(1, C), GELU)."""
+    h = x
+    if norm:
+        h = F.group_norm(h, 1, sd[_j(p, "norm1.weight")], sd[_j(p, "norm1.bias")], 1e-5)
+    h = conv2d_ref(gelu(h), sd, _j(p, "conv1"), **pad_kw)
+    if norm:
+        h = F.group_norm(h, 1, sd[_j(p, "norm2.weight")], sd[_j(p, "norm2.bias")], 1e-5)
+    h = conv2d_ref(gelu(h), sd, _j(p, "conv2"), **pad_kw)
+    sc = conv2d_ref(x, sd, _j(p, "shortcut")) if _j(p, "shortcut.weight") in sd else x
+    return crop_nd(h, sc.shape) + sc
+
+
+def unet_structure(hidden_features, ch_mults, n_blocks, n_cond):
+    """Module list of UNetModern.__init__, proc_unet_modern.py:91-152.
+
+    Returns (down, middle, up) where entries are ('down', cin, cout), ('downsample', c),
+    ('up', cin, cout) [cin excludes the skip channels], ('upsample', c)."""
+    n_res = len(ch_mults)
+    down = []
+    out_c = in_c = hidden_features
+    for i in range(n_res):
+        out_c = in_c * ch_mults[i]
+        for _ in range(n_blocks):
+            down.append(("down", in_c + n_cond, out_c))
+            in_c = out_c
+        if i < n_res - 1:
+            down.append(("downsample", in_c))
+    middle = ("middle", out_c + n_cond, out_c)
+    up = []
+    in_c = out_c
+    for i in reversed(range(n_res)):
+        out_c = in_c
+        for _ in range(n_blocks):
+            up.append(("up", in_c + n_cond, out_c))
+        out_c = in_c // ch_mults[i]
+        up.append(("up", in_c + n_cond, out_c))
+        in_c = out_c
+        if i > 0:
+            up.append(("upsample", in_c))
+    return down, middle, up
+
+
+def unet_modern(sd, p, cfg, h, vb):
+    """UNetModern.forward, proc_unet_modern.py:169-196 (cond_mode='concat', no attention)."""
+    pmode = cfg.get("padding_mode", "ones")
+    pad_kw = dict(padding=1) if pmode == "ones" else dict(padding_mode="circular")
+    norm = cfg.get("norm", False)
+    n_cond = cfg.get("n_cond", 0) if cfg.get("cond_mode", "concat") is not None else 0
+    down, _, up = unet_structure(cfg.get("hidden_features", 128), cfg.get("ch_mults", (1, 2, 2, 4)),
+                                 cfg.get("n_blocks", 2), n_cond)
+    h_shape = h.shape
+    feats, vbs = [h], [vb]
+    for i, m in enumerate(down):
+        q = _j(p, f"down.{i}")
+        if m[0] == "down":  # DownBlock, :349-354
+            x = torch.cat([h, vb], dim=1) if vb is not None else h
+            h = residual_block(sd, _j(q, "res"), x, norm, pad_kw)
+        else:  # Downsample, :451-455 (3x3, stride 2)
+            h = conv2d_ref(h, sd, _j(q, "conv"), stride=2, **pad_kw)
+            if vb is not None:
+                vb = conv2d_ref(vb, sd, _j(q, "conv_variables_broadcast"), stride=2, **pad_kw)
+        feats.append(h)
+        vbs.append(vb)
+    x = torch.cat([h, vb], dim=1) if vb is not None else h  # MiddleBlock, :416-422
+    h = residual_block(sd, _j(p, "middle.res1"), x, norm, pad_kw)
+    h = residual_block(sd, _j(p, "middle.res2"), h, norm, pad_kw)
+    for i, m in enumerate(up):
+        q = _j(p, f"up.{i}")
+        if m[0] == "upsample":  # Upsample → get_upconv_with_right_spatial_dim, common.py:103-120
+            if pmode == "circular":
+                h = conv_transpose_ref(h, sd, _j(q, "conv"), stride=2, padding=0, circ_pre_pad=1)
+            else:
+                h = conv_transpose_ref(h, sd, _j(q, "conv"), stride=2, padding=1)
+        else:
+            s = crop_nd(feats.pop(), h.shape)
+            v = crop_nd(vbs.pop(), h.shape) if vbs[-1] is not None else vbs.pop()
+            x = torch.cat((h, s, v), dim=1) if v is not None else torch.cat((h, s), dim=1)
+            h = residual_block(sd, _j(q, "res"), x, norm, pad_kw)
+    if norm:
+        h = F.group_norm(h, 8, sd[_j(p, "norm.weight")], sd[_j(p, "norm.bias")], 1e-5)
+    h = gelu(h)
+    if cfg.get("use1x1", False):
+        h = conv2d_ref(h, sd, _j(p, "final"))
+    else:
+        h = conv2d_ref(h, sd, _j(p, "final"), **pad_kw)
+    return crop_nd(h, h_shape)
+
+
+# ------------------------------------------------------------ dilated ResNet --
+def dilated_resnet(sd, p, cfg, h, vb):
+    """DilatedResnet.forward + DilatedResnetBlock, proc_dilatedresnet.py:43-50, 53-84."""
+    dil = (1, 2, 4, 8, 4, 2, 1)
+    pm = cfg.get("padding_mode", "zeros")
+    for blk in range(cfg.get("hidden_blocks", 4)):
+        x = torch.cat([h, vb], dim=1) if vb is not None else h
+        for li, d in enumerate(dil):
+            x = gelu(conv2d_ref(x, sd, _j(p, f"processor.{blk}.layers.{2 * li}"), padding="same", dilation=d,
+                                padding_mode=pm))
+        h = h + x
+    return h
+
+
+# ----------------------------------------------------------------- U-FNO ------
+def ufno(sd, p, cfg, h, vb):
+    """UFNO.forward, proc_ufno.py:105-118 (cond_mode='concat')."""
+    pm = cfg.get("padding_mode", "circular")
+    ucfg = dict(cfg)
+    ucfg.setdefault("ch_mults", (1, 1, 1))
+    ucfg.setdefault("n_blocks", 1)
+    ucfg.setdefault("use1x1", True)
+    ucfg["padding_mode"] = pm
+    for i in range(cfg.get("hidden_blocks", 4)):
+        h_in = torch.cat([h, vb], dim=1) if vb is not None else h
+        h_fno = fno_layer(sd, _j(p, f"fno_layers.{i}"), h_in, activation=False,
+                          padding_mode=pm if pm != "ones" else "zeros", conv_mode=cfg.get("fno_conv_mode", "single"))
+        h_unet = unet_modern(sd, _j(p, f"unet_layers.{i}"), ucfg, h, vb)
+        h = gelu(h_fno + h_unet)
+    return h
+
+
+# ------------------------------------------------------- encoder / decoder ----
+def enc_elementwise(sd, p, u, pos, vb):
+    """enc_grid.ElementWise.forward, enc_grid.py:41-50 (activation = GELU from the cfg)."""
+    h = torch.flatten(u, 1, 2)
+    pos = torch.movedim(pos, -1, 1)
+    h = torch.cat([h, pos, vb], dim=1) if vb is not None else torch.cat([h, pos], dim=1)
+    h = gelu(conv2d_ref(h, sd, _j(p, "encoder.0")))
+    return gelu(conv2d_ref(h, sd, _j(p, "encoder.2")))
+
+
+def add_delta(delta, u, dt, tw):
+    """dec_grid.add_delta 'per_step', dec_grid.py:8-31."""
+    dts = torch.cumsum(torch.ones(1, 1, tw) * dt, dim=2)[..., None, None]
+    u_last = u[:, :, [-1], ...].repeat(1, 1, tw, 1, 1)
+    return u_last + dts * delta
+
+
+def dec_timeconvdense(sd, p, h, u, dt, num_c, tw):
+    """dec_grid.TimeConvDense.forward, dec_grid.py:126-146."""
+    h = conv2d_ref(h, sd, _j(p, "pre_decoder"))
+    B, _, H, W = h.shape
+    h = h.permute(0, 2, 3, 1).reshape(B * H * W, num_c, tw * 3)
+    d = F.conv1d(h, sd[_j(p, "decoder.0.weight")], sd[_j(p, "decoder.0.bias")], stride=2)
+    d = gelu(d)
+    d = F.conv1d(d, sd[_j(p, "decoder.2.weight")], sd[_j(p, "decoder.2.bias")])
+    d = d.view(B, H, W, num_c, tw).permute(0, 3, 4, 1, 2)
+    return add_delta(d, u, dt, tw)
