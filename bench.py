@@ -1,0 +1,205 @@
+"""Rollout throughput bench: U-FNO twophase cfg, 256x256, 3 fields, obstacle (BASELINE.json config C3).
+
+python bench.py [--gpus N --steps K --warmup W]
+  * one step = one autoregressive model call (advances tw=25 timesteps for every sample) plus the
+    per-window MSE_sum loss, i.e. one iteration of AutoregressivePushforwardTrainer.simulate
+    (reference trainers/autoregressivepushforwardtrainer.py:354-432), trajectory resident in HBM;
+  * strong scaling: a fixed global batch (16) is sharded over the ranks (one process per GPU,
+    torchrun); no collective inside the rollout, one barrier + max-reduction of the timings;
+  * value = global samples x tw x K / max-over-ranks wall time  [sample-timesteps/s];
+  * roofline: the implicit-GEMM conv kernel (nps_conv2d_fwd = conv2d_fwd_kernel<*>), >99% of the
+    model's flops, timed live with HIP events on its stream during one extra model call after the
+    timed region: achieved = sum(algorithmic conv flops) / sum(kernel durations) vs the 157.3 TF/s
+    fp32 MFMA peak (MI355X_MICROARCH.md);
+  * cpu_baseline: the CPU oracle (oracle/, the reference restated in fp32 PyTorch-CPU) on a bounded
+    sample (2 model calls at B=2) on rank 0 only, with the GPU-vs-CPU rel-L2 of that sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "neural-pde-surrogates_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+from torch import nn  # noqa: E402
+
+FP32_MFMA_PEAK_TFLOPS = 157.3
+ORACLE_PDE = dict(tmin=0.0, tmax=1.0, nt=501, n_cond_static=3, n_cond_spatial=1)
+
+# cfg_twophase_*.py model dicts (reference src/configs/train/), wrapper args included
+_WRAP = dict(activation_final=nn.Tanh(), enforce_spatial_cond=True, spatial_cond_channel=0,
+             approx_volume_preserve=True, approx_volume_preserve_mode="individual_static", max_pct_dif=1 / 25,
+             model_class="EncProcDec", num_spatial_dims=2, time_window=25, data_structure="grid",
+             processor_residual=False, encoder="enc_grid.ElementWise", decoder="dec_grid.TimeConvDense",
+             dec_delta_mode="per_step")
+CFGS = {
+    "ufno": dict(processor="UFNO", fno_modes=10, hidden_blocks=3, hidden_features=192, fno_kernel_size=1,
+                 fno_conv_mode="single", padding_mode="circular", ch_mults=[1, 1], is_attn=[False, False],
+                 mid_attn=False, norm=True, use1x1=True),
+    "unet": dict(processor="UNetModern", ch_mults=[2, 2, 1, 2], is_attn=[False] * 4, mid_attn=False,
+                 hidden_features=32, norm=True, use1x1=True, cond_mode="concat", padding_mode="circular",
+                 dec_kernel_size=5, dec_padding_mode="circular"),
+    "drn": dict(processor="DilatedResnet", kernel_size=5, hidden_blocks=2, hidden_features=128,
+                padding_mode="circular", dec_kernel_size=5, dec_padding_mode="circular"),
+}
+
+
+def build_model(kind, res, num_c, device, fno_modes=None, seed=42):
+    """Random-init (seed 42, configs/train/defaults/base.py:4) twophase model of the given cfg."""
+    import models
+    from pdes import PDE2D
+    cfg = dict(_WRAP, activation=nn.GELU(), num_c=num_c, **CFGS[kind])
+    if fno_modes is not None:
+        cfg["fno_modes"] = fno_modes
+    pde = PDE2D(tmin=ORACLE_PDE["tmin"], tmax=ORACLE_PDE["tmax"], nt=ORACLE_PDE["nt"], L1=1.0, L2=1.0, nx1=res,
+                nx2=res, x=None, name="twophase", n_cond_static=3, n_cond_spatial=1)
+    torch.manual_seed(seed)
+    m = models.activation_wrapper(**cfg, pde=pde).to(device).eval()
+    ocfg = {k: v for k, v in cfg.items() if k not in ("activation", "activation_final")}
+    return m, ocfg, dict(ORACLE_PDE, nx1=res, nx2=res)
+
+
+def conv_roofline(model, x, cond, pos, sc):
+    """One model call with every conv launch bracketed by HIP events on its stream."""
+    from nps_hip import ops
+    ops.conv_probe = []
+    with torch.no_grad():
+        model(x, cond=cond, bc=None, pos=pos, t_cond=None, spatial_cond=sc)
+    torch.cuda.synchronize()
+    probe, ops.conv_probe = ops.conv_probe, None
+    ms = sum(e0.elapsed_time(e1) for e0, e1, _ in probe)
+    flops = sum(f for _, _, f in probe)
+    achieved = flops / (ms * 1e-3) / 1e12
+    return dict(bound="mfma", achieved=round(achieved, 3), peak=FP32_MFMA_PEAK_TFLOPS, unit="TFLOP/s",
+                frac=round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), traffic=None,
+                kernel="conv2d_fwd_kernel (nps_conv2d_fwd)", launches=len(probe),
+                avg_launch_ms=round(ms / max(1, len(probe)), 4), flops_per_call=flops)
+
+
+def cpu_baseline(model, ocfg, opde, res, num_c, calls=2, B=2):
+    import oracle
+    from trainers.synthetic import twophase_batch
+    threads = int(os.environ.get("OMP_NUM_THREADS", len(os.sched_getaffinity(0))))
+    torch.set_num_threads(threads)
+    om = oracle.build_oracle_model(ocfg, opde, {k: v.detach().cpu() for k, v in model.state_dict().items()})
+    u, cond, pos, sc = twophase_batch(B, num_c, 25 * (calls + 1), res, res, seed=99, obstacle="disc")
+    tw = 25
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        losses, preds = oracle.simulate(om, u, cond, pos, sc, tw, 25 * (calls + 1))
+    dt = time.perf_counter() - t0
+    # parity of the same sample on the GPU path
+    dev = next(model.parameters()).device
+    pred = u[:, :, :tw].to(dev)
+    err = 0.0
+    with torch.no_grad():
+        for k in range(calls):
+            pred = model(pred, cond=cond.to(dev), bc=None, pos=pos.to(dev), t_cond=None, spatial_cond=sc.to(dev))
+            ref = preds[k + 1].double()
+            e = (torch.linalg.vector_norm(pred.cpu().double() - ref) / torch.linalg.vector_norm(ref)).item()
+            err = max(err, e)
+    return dict(value=round(B * tw * calls / dt, 3), unit="sample-timesteps/s", cores=threads, kind="port",
+                sample=f"oracle (fp32 PyTorch-CPU restatement of the reference) simulate: {calls} model calls, "
+                       f"B={B}, {res}x{res}, {num_c} fields, {dt:.1f} s",
+                rel_l2_gpu_vs_cpu=err)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--model", default="ufno", choices=list(CFGS))
+    ap.add_argument("--res", type=int, default=256)
+    ap.add_argument("--num-c", type=int, default=3)
+    ap.add_argument("--global-batch", type=int, default=16)
+    ap.add_argument("--fno-modes", type=int, default=None)
+    ap.add_argument("--cpu-calls", type=int, default=2, help="CPU-baseline sample size (model calls, 0 = skip)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+    if args.global_batch % world != 0:
+        raise SystemExit(f"global batch {args.global_batch} not divisible by {world} ranks")
+    B = args.global_batch // world
+    tw = 25
+
+    import argparse as _ap
+    import types
+    from common.interfaces import D
+    from trainers.autoregressivepushforwardtrainer import AutoregressivePushforwardTrainer
+    from trainers.synthetic import twophase_batch
+
+    model, ocfg, opde = build_model(args.model, args.res, args.num_c, dev, fno_modes=args.fno_modes)
+    # this rank's shard of the global synthetic batch: samples [rank*B, (rank+1)*B)
+    T = tw * (max(args.steps, args.warmup) + 1)
+    u, cond, pos, sc = twophase_batch(args.global_batch, args.num_c, 1, args.res, args.res, seed=1234,
+                                      obstacle="disc")
+    u_all, _, _, _ = twophase_batch(B, args.num_c, T, args.res, args.res, seed=1234 + rank, obstacle="disc",
+                                    device=dev)
+    cond = cond[rank * B:(rank + 1) * B].to(dev)
+    pos = pos[rank * B:(rank + 1) * B].to(dev)
+    sc = sc[rank * B:(rank + 1) * B].to(dev)
+    cfg = _ap.Namespace(time_window=tw, base_resolution=(T, args.res, args.res), device=dev, nr_gt_steps=1)
+    tr = AutoregressivePushforwardTrainer(model=model, data=types.SimpleNamespace(pde=model.pde, data_interface=D.sim2d),
+                                          criterion=nn.MSELoss(reduction="sum"), config=cfg)
+
+    def rollout(nsteps):
+        with torch.no_grad():
+            return tr.simulate(u_all, cond, pos, compute_loss=True, include_data=False, nr_gt_steps=1,
+                               t_res=tw * (nsteps + 1), spatial_conditioning=sc)
+
+    if args.warmup > 0:
+        rollout(args.warmup)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    losses = rollout(args.steps)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = t.item()
+    value = args.global_batch * tw * args.steps / elapsed
+
+    if rank == 0:
+        roof = conv_roofline(model, u_all[:, :, :tw], cond, pos, sc)
+        cpu = cpu_baseline(model, ocfg, opde, args.res, args.num_c, calls=args.cpu_calls) if (
+            args.cpu_calls > 0 and world == 1) else None
+        line = {
+            "metric": "rollout timesteps/sec on 256x256 two-phase grid (sample-timesteps/s); rel-L2 vs CPU reference",
+            "value": round(value, 3), "unit": "sample-timesteps/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": f"{args.model.upper()} twophase cfg rollout (simulate), {args.res}x{args.res}, "
+                                   f"{args.num_c} fields, obstacle mask, tw=25", "model": args.model,
+                       "global_batch": args.global_batch, "per_gpu_batch": B, "res": args.res,
+                       "num_c": args.num_c, "parallelism": f"dp{world} (batch-sharded rollout, no collective)"},
+            "roofline": roof, "cpu_baseline": cpu,
+            "rel_l2_vs_cpu": None if cpu is None else cpu["rel_l2_gpu_vs_cpu"],
+            "loss_last_window": float(losses[-1].item()),
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

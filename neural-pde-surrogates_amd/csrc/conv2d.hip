@@ -1,0 +1,476 @@
+// Implicit-GEMM 2-D convolution on fp32 MFMA for gfx950 (MI355X), NHWC activations.
+//
+// Replaces every nn.Conv2d / nn.ConvTranspose2d forward on the reference's grid
+// path (models/common.py:37-47, 93-120; proc_unet_modern.py, proc_dilatedresnet.py,
+// proc_fno.py:114-117, enc_grid.py:234-243, dec_grid.py:365-368), see include/nps.h.
+//
+// GEMM view: D[co][px] = sum_k A[co][k] * B[k][px], k = (chunk of 16 input
+// channels, tap).  One workgroup = WAVES wavefronts = 64 output channels x
+// 64*WAVES output pixels (a TH x TW pixel tile of one sample); each wave owns
+// 64 co x 64 px = 2 x 2 tiles of v_mfma_f32_32x32x2_f32 (exact f32, the only
+// f32 matrix path on gfx950).
+//   * B (input patch of the tile incl. halo, 16 channels) is staged global ->
+//     registers -> LDS once per channel chunk and read by every tap: 9x fewer
+//     global reads than im2col for a 3x3 conv.  The prologue (crop_Nd zero
+//     fill, channel concat, circular wrap, GroupNorm affine, GELU) is applied
+//     while staging, so none of those ever round-trips through HBM.
+//   * A (weights) is pre-packed in MFMA-fragment order so every wave load is
+//     one contiguous 1 KiB dwordx4 burst straight into VGPRs (L2 resident),
+//     prefetched one tap ahead.
+//   * Dilated convs tile the output on the dilation lattice ("lattice" mode),
+//     so the LDS patch is (TH+KH-1) x (TW+KW-1) instead of growing with d.
+//   * Patch double-buffered in LDS; one barrier per 16-channel chunk.
+#include "nps_common.hpp"
+
+namespace {
+
+constexpr int CK = 16;          // input channels per K chunk
+constexpr int PIXS = CK + 4;    // LDS floats per patch pixel (+4 pad: conflict-free ds_read_b128)
+constexpr int MAXL = 12;        // max float4 patch loads per thread per chunk
+
+struct Geo {
+    int T, ri, rk, rstep, PH, PW, tiles_x, tiles_y;
+};
+
+__host__ __device__ inline Geo make_geo(const nps_conv2d_t& a) {
+    Geo g;
+    g.T = a.lattice ? a.dil : 1;
+    g.ri = a.lattice ? 1 : a.stride;
+    g.rk = a.lattice ? 1 : a.dil;
+    g.rstep = a.lattice ? a.dil : 1;
+    g.PH = (a.TH - 1) * g.ri + (a.KH - 1) * g.rk + 1;
+    g.PW = (a.TW - 1) * g.ri + (a.KW - 1) * g.rk + 1;
+    const int ny = (a.Hout + g.T - 1) / g.T, nx = (a.Wout + g.T - 1) / g.T;
+    g.tiles_y = g.T * ((ny + a.TH - 1) / a.TH);
+    g.tiles_x = g.T * ((nx + a.TW - 1) / a.TW);
+    return g;
+}
+
+// Fetch 4 consecutive virtual channels [c, c+4) at virtual-frame position (y, x) of sample b.
+__device__ __forceinline__ f32x4 fetch4(const nps_conv2d_t& a, int b, int y, int x, int c) {
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    int c0 = 0;
+#pragma unroll
+    for (int s = 0; s < NPS_MAX_SRC; ++s) {
+        if (s < a.nsrc) {
+            const nps_src_t& S = a.src[s];
+            const int lo = c0, hi = c0 + S.C;
+            // fast path: all 4 channels inside this source and 16-B aligned
+            if (c >= lo && c + 4 <= hi && ((c - lo) & 3) == 0 && (S.C & 3) == 0) {
+                const int yy = y - S.off_y, xx = x - S.off_x;
+                if (yy >= 0 && yy < S.H && xx >= 0 && xx < S.W)
+                    v = *reinterpret_cast<const f32x4*>(S.ptr + ((size_t)(b * S.H + yy) * S.W + xx) * S.C + (c - lo));
+                return v;
+            }
+            c0 = hi;
+        }
+    }
+    // general path: per-channel gather (sources with C % 4 != 0, straddling chunks)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int ce = c + e;
+        int base = 0;
+        float r = 0.f;
+#pragma unroll
+        for (int s = 0; s < NPS_MAX_SRC; ++s) {
+            if (s < a.nsrc) {
+                const nps_src_t& S = a.src[s];
+                if (ce >= base && ce < base + S.C) {
+                    const int yy = y - S.off_y, xx = x - S.off_x;
+                    if (yy >= 0 && yy < S.H && xx >= 0 && xx < S.W)
+                        r = S.ptr[((size_t)(b * S.H + yy) * S.W + xx) * S.C + (ce - base)];
+                }
+                base += S.C;
+            }
+        }
+        v[e] = r;
+    }
+    return v;
+}
+
+template <int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void conv2d_fwd_kernel(const nps_conv2d_t a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    constexpr int NT = WAVES * 64;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int b = blockIdx.z, cob = blockIdx.y;
+    const Geo g = make_geo(a);
+    const int ty = blockIdx.x / g.tiles_x, tx = blockIdx.x % g.tiles_x;
+    const int oy0 = (ty % g.T) + (ty / g.T) * a.TH * g.T;
+    const int ox0 = (tx % g.T) + (tx / g.T) * a.TW * g.T;
+    const int ybase = oy0 * a.stride - a.pad_y, xbase = ox0 * a.stride - a.pad_x;
+    const int Hext = a.Hin + 2 * a.circ, Wext = a.Win + 2 * a.circ;
+    const int npix = g.PH * g.PW;
+    const int NG = npix * (CK / 4);
+    const int bufsz = ((npix * PIXS + 3) & ~3);
+    float2* gn_tab = reinterpret_cast<float2*>(smem);          // [gn_groups <= 16] (mean, rstd)
+    float* pbuf = smem + 32;                                   // 2 patch buffers (128 B header keeps 16-B alignment)
+    const int nchunks = (a.Cin + CK - 1) / CK;
+    const int ntaps = a.KH * a.KW;
+    const int ncb = 2 * ((a.Cout + 63) / 64);
+
+    if (a.gn_stats != nullptr && tid < a.gn_groups) {
+        const double cnt = (double)(a.Cin / a.gn_groups) * a.Hin * a.Win;
+        const double s = a.gn_stats[(b * a.gn_groups + tid) * 2], ss = a.gn_stats[(b * a.gn_groups + tid) * 2 + 1];
+        const double mean = s / cnt;
+        double var = ss / cnt - mean * mean;
+        var = var < 0.0 ? 0.0 : var;
+        gn_tab[tid] = make_float2((float)mean, (float)(1.0 / sqrt(var + (double)a.gn_eps)));
+    }
+    __syncthreads();
+    const int cpg = a.gn_stats ? a.Cin / a.gn_groups : 1;
+
+    f32x4 pre[MAXL];
+    auto load_patch = [&](int ch) {
+#pragma unroll
+        for (int k = 0; k < MAXL; ++k) {
+            const int idx = tid + k * NT;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if (idx < NG) {
+                const int p = idx >> 2, gq = idx & 3;
+                const int pr = p / g.PW, pc = p - pr * g.PW;
+                const int ye = ybase + pr * g.rstep, xe = xbase + pc * g.rstep;
+                const int c = ch * CK + gq * 4;
+                if (ye >= 0 && ye < Hext && xe >= 0 && xe < Wext && c < a.Cin) {
+                    const int yv = a.circ ? nps::wrap_mod(ye - a.circ, a.Hin) : ye;
+                    const int xv = a.circ ? nps::wrap_mod(xe - a.circ, a.Win) : xe;
+                    v = fetch4(a, b, yv, xv, c);
+                    if (a.gn_stats != nullptr || a.pre_act) {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            if (c + e < a.Cin) {
+                                float t = v[e];
+                                if (a.gn_stats != nullptr) {
+                                    const float2 mr = gn_tab[(c + e) / cpg];
+                                    t = (t - mr.x) * mr.y * a.gn_gamma[c + e] + a.gn_beta[c + e];
+                                }
+                                if (a.pre_act == 1) t = nps::gelu_erf(t);
+                                v[e] = t;
+                            }
+                        }
+                    }
+                }
+            }
+            pre[k] = v;
+        }
+    };
+    auto store_patch = [&](int buf) {
+        float* dst = pbuf + buf * bufsz;
+#pragma unroll
+        for (int k = 0; k < MAXL; ++k) {
+            const int idx = tid + k * NT;
+            if (idx < NG) {
+                const int p = idx >> 2, gq = idx & 3;
+                *reinterpret_cast<f32x4*>(dst + p * PIXS + gq * 4) = pre[k];
+            }
+        }
+    };
+
+    // per-lane B (patch) base offsets for this wave's two 32-pixel blocks
+    int boff[2];
+#pragma unroll
+    for (int pb = 0; pb < 2; ++pb) {
+        const int P = wave * 64 + pb * 32 + (lane & 31);
+        const int ti = P / a.TW, tj = P - (P / a.TW) * a.TW;
+        boff[pb] = ((ti * g.ri) * g.PW + tj * g.ri) * PIXS + (lane >> 5) * 8;
+    }
+
+    const f32x4* wp = reinterpret_cast<const f32x4*>(a.wpack);
+    auto load_A = [&](f32x4 (&dst)[2][2], int ch, int tap) {
+        const size_t base = ((size_t)(ch * ntaps + tap) * ncb + cob * 2) * 2;
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+            for (int q = 0; q < 2; ++q) dst[cb][q] = wp[(base + cb * 2 + q) * 64 + lane];
+    };
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    f32x4 a_cur[2][2], a_nxt[2][2];
+    load_A(a_cur, 0, 0);
+    load_patch(0);
+    store_patch(0);
+    __syncthreads();
+
+    for (int ch = 0; ch < nchunks; ++ch) {
+        const bool more = ch + 1 < nchunks;
+        if (more) load_patch(ch + 1);
+        const float* buf = pbuf + (ch & 1) * bufsz;
+        for (int tap = 0; tap < ntaps; ++tap) {
+            int nch = ch, ntap = tap + 1;
+            if (ntap == ntaps) { ntap = 0; nch = ch + 1; }
+            if (nch < nchunks) load_A(a_nxt, nch, ntap);
+            const int ky = tap / a.KW, kx = tap - (tap / a.KW) * a.KW;
+            const int toff = (ky * g.rk * g.PW + kx * g.rk) * PIXS;
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                f32x4 bv[2];
+#pragma unroll
+                for (int pb = 0; pb < 2; ++pb) bv[pb] = *reinterpret_cast<const f32x4*>(buf + boff[pb] + toff + q * 4);
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+#pragma unroll
+                    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+                        for (int pb = 0; pb < 2; ++pb)
+                            acc[cb][pb] = __builtin_amdgcn_mfma_f32_32x32x2f32(a_cur[cb][q][e], bv[pb][e], acc[cb][pb], 0, 0, 0);
+            }
+#pragma unroll
+            for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+                for (int q = 0; q < 2; ++q) a_cur[cb][q] = a_nxt[cb][q];
+        }
+        if (more) store_patch((ch + 1) & 1);
+        __syncthreads();
+    }
+
+    // ---------------- epilogue ----------------
+    const int h = lane >> 5;
+#pragma unroll
+    for (int pb = 0; pb < 2; ++pb) {
+        const int P = wave * 64 + pb * 32 + (lane & 31);
+        const int ti = P / a.TW, tj = P - (P / a.TW) * a.TW;
+        const int oy = oy0 + ti * g.T, ox = ox0 + tj * g.T;
+        if (ti >= a.TH || oy >= a.Hout || ox >= a.Wout) continue;
+        const int dy = oy * a.out_os + a.out_off_y, dx = ox * a.out_os + a.out_off_x;
+        if (dy < 0 || dy >= a.out_H || dx < 0 || dx >= a.out_W) continue;
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const int co0 = cob * 64 + cb * 32 + 8 * m + 4 * h;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int co = co0 + e;
+                    if (co >= a.Cout) continue;
+                    const size_t di = a.out_nchw ? (((size_t)b * a.out_C + co) * a.out_H + dy) * a.out_W + dx
+                                                 : (((size_t)b * a.out_H + dy) * a.out_W + dx) * a.out_C + co;
+                    float v = acc[cb][pb][4 * m + e];
+                    if (a.bias) v += a.bias[co];
+                    if (!a.add_after_act) {
+                        if (a.addend0) v += a.addend0[di];
+                        if (a.addend1) v += a.addend1[di];
+                    }
+                    if (a.act == 1) v = nps::gelu_erf(v);
+                    if (a.add_after_act) {
+                        if (a.addend0) v += a.addend0[di];
+                        if (a.addend1) v += a.addend1[di];
+                    }
+                    if (a.accumulate) v += a.out[di];
+                    a.out[di] = v;
+                }
+            }
+        }
+    }
+}
+
+// Packed layout: [chunk][tap][cb (32-co block, padded to a multiple of 2)][q (2)][lane (64)][4]
+// element = w[co = cb*32 + (lane&31)][ci = chunk*16 + (lane>>5)*8 + q*4 + e][tap]
+__global__ void pack_weights_kernel(const float* __restrict__ w, float* __restrict__ wp, int Cout, int Cin, int KH,
+                                    int KW, int tphase, size_t total) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int ntaps = KH * KW;
+    const int ncb = 2 * ((Cout + 63) / 64);
+    const int e = i & 3;
+    size_t r = i >> 2;
+    const int lane = r & 63; r >>= 6;
+    const int q = r & 1; r >>= 1;
+    const int cb = r % ncb; r /= ncb;
+    const int tap = r % ntaps; r /= ntaps;
+    const int chunk = (int)r;
+    const int co = cb * 32 + (lane & 31);
+    const int ci = chunk * CK + (lane >> 5) * 8 + q * 4 + e;
+    float v = 0.f;
+    if (co < Cout && ci < Cin) {
+        const int ky = tap / KW, kx = tap % KW;
+        if (tphase < 0) {
+            v = w[(((size_t)co * Cin + ci) * KH + ky) * KW + kx];
+        } else {
+            // 4x4 / stride-2 transposed conv, output phase (py, px): tap (ty, tx) uses
+            // kernel element (py + 2(1-ty), px + 2(1-tx)) of w[Cin][Cout][4][4]
+            const int py = tphase >> 1, px = tphase & 1;
+            const int kyy = py + 2 * (1 - ky), kxx = px + 2 * (1 - kx);
+            v = w[(((size_t)ci * Cout + co) * 4 + kyy) * 4 + kxx];
+        }
+    }
+    wp[i] = v;
+}
+
+size_t packed_size(int Cout, int Cin, int ntaps) {
+    const size_t nchunks = (Cin + CK - 1) / CK, ncb = 2 * ((Cout + 63) / 64);
+    return nchunks * ntaps * ncb * 2 * 64 * 4;
+}
+
+int lds_bytes(const nps_conv2d_t& a) {
+    const Geo g = make_geo(a);
+    const int bufsz = ((g.PH * g.PW * PIXS + 3) & ~3);
+    return (32 + 2 * bufsz) * 4;
+}
+
+}  // namespace
+
+extern "C" size_t nps_conv2d_packed_size(int Cout, int Cin, int ntaps) { return packed_size(Cout, Cin, ntaps); }
+
+extern "C" int nps_conv2d_pack_weights(const float* w, float* wpack, int Cout, int Cin, int KH, int KW,
+                                       int transposed_phase, void* stream) {
+    NPS_CHECK_ARG(w && wpack && Cout > 0 && Cin > 0 && KH > 0 && KW > 0, "conv2d_pack_weights: bad args");
+    NPS_CHECK_ARG(transposed_phase < 0 || (KH == 2 && KW == 2 && transposed_phase < 4),
+                  "conv2d_pack_weights: transposed phase packing needs KH=KW=2");
+    const size_t total = packed_size(Cout, Cin, KH * KW);
+    const int bs = 256;
+    pack_weights_kernel<<<(unsigned)((total + bs - 1) / bs), bs, 0, (hipStream_t)stream>>>(w, wpack, Cout, Cin, KH, KW,
+                                                                                        transposed_phase, total);
+    NPS_CHECK_LAUNCH("conv2d_pack_weights");
+    return 0;
+}
+
+extern "C" int nps_conv2d_plan(nps_conv2d_t* a) {
+    NPS_CHECK_ARG(a != nullptr, "conv2d_plan: null");
+    // dilated stride-1 convs tile on the dilation lattice (patch independent of d)
+    a->lattice = (a->dil > 1 && a->stride == 1) ? 1 : 0;
+    const long units_co = (a->Cout + 63) / 64;
+    // candidate tiles (waves, TH, TW), largest first: take the first one whose grid
+    // puts >= 8 waves on each of the 256 CUs, else the one with the most waves.
+    const int cand[5][3] = {{4, 16, 16}, {4, 8, 32}, {2, 8, 16}, {1, 8, 8}, {1, 4, 16}};
+    int best = -1;
+    long best_waves = -1;
+    for (int i = 0; i < 5; ++i) {
+        nps_conv2d_t t = *a;
+        t.waves = cand[i][0];
+        t.TH = cand[i][1];
+        t.TW = cand[i][2];
+        if (t.stride > 1 && t.TH * t.TW > 128) continue;  // stride-2 patches grow 4x
+        if (lds_bytes(t) > 160 * 1024) continue;
+        const Geo g = make_geo(t);
+        if (g.PH * g.PW * (CK / 4) > MAXL * 64 * t.waves) continue;
+        const long waves = (long)g.tiles_x * g.tiles_y * a->B * units_co * t.waves;
+        if (waves > best_waves) {
+            best_waves = waves;
+            best = i;
+        }
+        if (waves >= 256 * 8) break;
+    }
+    NPS_CHECK_ARG(best >= 0, "conv2d_plan: no tile fits (KH=%d KW=%d stride=%d dil=%d)", a->KH, a->KW, a->stride,
+                  a->dil);
+    a->waves = cand[best][0];
+    a->TH = cand[best][1];
+    a->TW = cand[best][2];
+    return lds_bytes(*a);
+}
+
+extern "C" int nps_conv2d_fwd(const nps_conv2d_t* ap, void* stream) {
+    NPS_CHECK_ARG(ap != nullptr, "conv2d_fwd: null args");
+    const nps_conv2d_t& a = *ap;
+    NPS_CHECK_ARG(a.nsrc >= 1 && a.nsrc <= NPS_MAX_SRC, "conv2d_fwd: nsrc=%d", a.nsrc);
+    int csum = 0;
+    for (int s = 0; s < a.nsrc; ++s) {
+        NPS_CHECK_ARG(a.src[s].ptr && a.src[s].C > 0 && a.src[s].H > 0 && a.src[s].W > 0, "conv2d_fwd: bad src %d", s);
+        csum += a.src[s].C;
+    }
+    NPS_CHECK_ARG(csum == a.Cin, "conv2d_fwd: Cin=%d != sum of source channels %d", a.Cin, csum);
+    NPS_CHECK_ARG(a.B > 0 && a.Hout > 0 && a.Wout > 0 && a.Cout > 0 && a.wpack && a.out, "conv2d_fwd: bad shape");
+    NPS_CHECK_ARG(a.KH > 0 && a.KW > 0 && a.stride > 0 && a.dil > 0, "conv2d_fwd: bad kernel geometry");
+    NPS_CHECK_ARG(!a.gn_stats || (a.gn_groups > 0 && a.gn_groups <= 16 && a.Cin % a.gn_groups == 0 && a.gn_gamma &&
+                                  a.gn_beta),
+                  "conv2d_fwd: bad GroupNorm prologue");
+    NPS_CHECK_ARG(a.circ == 0 || (a.Hin > 0 && a.Win > 0), "conv2d_fwd: circular padding of empty frame");
+    NPS_CHECK_ARG(a.waves == 1 || a.waves == 2 || a.waves == 4, "conv2d_fwd: call nps_conv2d_plan first");
+    NPS_CHECK_ARG(a.TH * a.TW == 64 * a.waves, "conv2d_fwd: tile %dx%d != 64*waves", a.TH, a.TW);
+    const Geo g = make_geo(a);
+    NPS_CHECK_ARG(g.PH * g.PW * (CK / 4) <= MAXL * 64 * a.waves, "conv2d_fwd: patch too large for tile");
+    const int lds = lds_bytes(a);
+    NPS_CHECK_ARG(lds <= 160 * 1024, "conv2d_fwd: LDS %d B too large", lds);
+    dim3 grid((unsigned)(g.tiles_x * g.tiles_y), (unsigned)((a.Cout + 63) / 64), (unsigned)a.B);
+    hipStream_t s = (hipStream_t)stream;
+    static bool attr_set = false;  // allow > 64 KiB dynamic LDS (gfx950 has 160 KiB per CU)
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)conv2d_fwd_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)conv2d_fwd_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)conv2d_fwd_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr_set = true;
+    }
+    switch (a.waves) {
+        case 4: conv2d_fwd_kernel<4><<<grid, 256, lds, s>>>(a); break;
+        case 2: conv2d_fwd_kernel<2><<<grid, 128, lds, s>>>(a); break;
+        default: conv2d_fwd_kernel<1><<<grid, 64, lds, s>>>(a); break;
+    }
+    NPS_CHECK_LAUNCH("conv2d_fwd");
+    return 0;
+}
+
+// ------------------------------------------------------------------ GroupNorm statistics
+namespace {
+__global__ void gn_stats_kernel(nps_conv2d_t a, int G, double* __restrict__ stats) {
+    // a.src / a.nsrc / frame fields only
+    __shared__ double red[16];
+    const int b = blockIdx.z, gidx = blockIdx.y;
+    const int cpg = a.Cin / G;
+    const int g0 = gidx * cpg, g1 = g0 + cpg;
+    double s = 0.0, ss = 0.0;
+    int c0 = 0;
+    for (int si = 0; si < a.nsrc; ++si) {
+        const nps_src_t S = a.src[si];
+        const int lo = max(c0, g0), hi = min(c0 + S.C, g1);
+        c0 += S.C;
+        if (lo >= hi) continue;
+        const int nc = hi - lo, lc0 = lo - (c0 - S.C);
+        const int y0 = max(0, S.off_y), y1 = min(a.Hin, S.off_y + S.H);
+        const int x0 = max(0, S.off_x), x1 = min(a.Win, S.off_x + S.W);
+        if (y0 >= y1 || x0 >= x1) continue;
+        const int wi = x1 - x0;
+        const long n = (long)(y1 - y0) * wi * nc;
+        for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+            const long pix = i / nc;
+            const int cc = (int)(i - pix * nc);
+            const int y = (int)(pix / wi) + y0, x = (int)(pix % wi) + x0;
+            const float v = S.ptr[((size_t)(b * S.H + (y - S.off_y)) * S.W + (x - S.off_x)) * S.C + lc0 + cc];
+            s += v;
+            ss += (double)v * v;
+        }
+    }
+    s = nps::block_sum(s, red);
+    ss = nps::block_sum(ss, red);
+    if (threadIdx.x == 0) {
+        atomicAdd(&stats[(b * G + gidx) * 2], s);
+        atomicAdd(&stats[(b * G + gidx) * 2 + 1], ss);
+    }
+}
+}  // namespace
+
+extern "C" int nps_group_norm_stats(const nps_src_t* src, int nsrc, int B, int Hin, int Win, int Cin, int G,
+                                    double* stats, int zero_first, void* stream) {
+    NPS_CHECK_ARG(src && nsrc >= 1 && nsrc <= NPS_MAX_SRC && stats && B > 0 && G > 0 && Cin % G == 0,
+                  "group_norm_stats: bad args");
+    nps_conv2d_t a = {};
+    a.nsrc = nsrc;
+    int csum = 0;
+    for (int i = 0; i < nsrc; ++i) {
+        a.src[i] = src[i];
+        csum += src[i].C;
+    }
+    NPS_CHECK_ARG(csum == Cin, "group_norm_stats: Cin mismatch");
+    a.B = B;
+    a.Hin = Hin;
+    a.Win = Win;
+    a.Cin = Cin;
+    hipStream_t s = (hipStream_t)stream;
+    if (zero_first) {
+        if (hipMemsetAsync(stats, 0, sizeof(double) * 2 * B * G, s) != hipSuccess) {
+            nps::set_error("group_norm_stats: memset failed");
+            return -2;
+        }
+    }
+    const long per = (long)Hin * Win * (Cin / G);
+    int nblk = (int)((per + 256 * 16 - 1) / (256 * 16));
+    nblk = nblk < 1 ? 1 : (nblk > 512 ? 512 : nblk);
+    gn_stats_kernel<<<dim3(nblk, G, B), 256, 0, s>>>(a, G, stats);
+    NPS_CHECK_LAUNCH("group_norm_stats");
+    return 0;
+}

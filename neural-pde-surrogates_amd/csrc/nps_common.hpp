@@ -1,0 +1,67 @@
+// Shared helpers for the gfx950 kernels of libnps_hip.so (see include/nps.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdarg>
+#include <cmath>
+
+#include "../../include/nps.h"
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+namespace nps {
+
+void set_error(const char* fmt, ...);
+
+#define NPS_CHECK_ARG(cond, ...)            \
+    do {                                    \
+        if (!(cond)) {                      \
+            ::nps::set_error(__VA_ARGS__);  \
+            return -1;                      \
+        }                                   \
+    } while (0)
+
+#define NPS_CHECK_LAUNCH(what)                                                          \
+    do {                                                                                \
+        hipError_t e_ = hipGetLastError();                                              \
+        if (e_ != hipSuccess) {                                                         \
+            ::nps::set_error("%s: HIP launch failed: %s", what, hipGetErrorString(e_)); \
+            return -2;                                                                  \
+        }                                                                               \
+    } while (0)
+
+// nn.GELU() default (approximate='none'): 0.5 x (1 + erf(x / sqrt 2))
+__device__ __forceinline__ float gelu_erf(float x) {
+    return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
+}
+
+__device__ __forceinline__ int wrap_mod(int v, int n) {
+    int r = v % n;
+    return r < 0 ? r + n : r;
+}
+
+// wave64 sum of a double
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Block-wide sum of a double into lane 0 of wave 0 (blockDim.x multiple of 64, <= 1024).
+__device__ __forceinline__ double block_sum(double v, double* scratch) {
+    v = wave_sum(v);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) scratch[wid] = v;
+    __syncthreads();
+    double r = 0.0;
+    if (threadIdx.x < 64) {
+        const int nw = blockDim.x >> 6;
+        r = (lane < nw) ? scratch[lane] : 0.0;
+        r = wave_sum(r);
+    }
+    __syncthreads();
+    return r;
+}
+
+}  // namespace nps

@@ -1,0 +1,270 @@
+// Grid encoder input packing, TimeConvDense decoder, activation_wrapper
+// post-processing, reductions and layout transforms for gfx950 (see include/nps.h).
+#include "nps_common.hpp"
+
+#include <cstring>
+
+namespace nps {
+static thread_local char g_err[512] = "";
+void set_error(const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+}  // namespace nps
+
+extern "C" const char* nps_last_error(void) { return nps::g_err; }
+extern "C" const char* nps_version(void) { return "nps_hip 0.1 gfx950"; }
+
+namespace {
+
+// ---------------------------------------------------------------- encoder input
+// One block = 64 pixels of one sample; channels staged through LDS so both the
+// planar reads of u and the NHWC writes are coalesced.
+__global__ void pack_grid_kernel(const float* __restrict__ u, const float* __restrict__ pos,
+                                 const float* __restrict__ cond, const float* __restrict__ sc, float* __restrict__ xin,
+                                 float* __restrict__ vb, int CT, int HW, int K, int S, int Cp) {
+    extern __shared__ float tile[];  // [Cp][65]
+    const int b = blockIdx.y;
+    const int p0 = blockIdx.x * 64;
+    const int np = min(64, HW - p0);
+    const int KS = K + S;
+    for (int i = threadIdx.x; i < Cp * 64; i += blockDim.x) {
+        const int ch = i / 64, p = i % 64;
+        float v = 0.f;
+        if (p < np) {
+            const int pix = p0 + p;
+            if (ch < CT)
+                v = u[((size_t)b * CT + ch) * HW + pix];
+            else if (ch < CT + 2)
+                v = pos[((size_t)b * HW + pix) * 2 + (ch - CT)];
+            else if (ch < CT + 2 + K)
+                v = cond[b * K + (ch - CT - 2)];
+            else if (ch < CT + 2 + KS)
+                v = sc[((size_t)b * S + (ch - CT - 2 - K)) * HW + pix];
+        }
+        tile[ch * 65 + p] = v;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < np * Cp; i += blockDim.x) {
+        const int p = i / Cp, ch = i % Cp;
+        xin[((size_t)b * HW + p0 + p) * Cp + ch] = tile[ch * 65 + p];
+    }
+    if (vb != nullptr) {
+        for (int i = threadIdx.x; i < np * KS; i += blockDim.x) {
+            const int p = i / KS, ch = i % KS;
+            vb[((size_t)b * HW + p0 + p) * KS + ch] = tile[(CT + 2 + ch) * 65 + p];
+        }
+    }
+}
+
+// ---------------------------------------------------------------- TimeConvDense
+// One block = 64 pixels x 4 slots.  Phase 1: d1[o][t1] = GELU(conv1d_k1,s2(pre)) into
+// LDS; phase 2: d2 = conv1d_k2(d1), then add_delta, tanh, spatial-cond mask.
+__global__ void timeconv_kernel(const float* __restrict__ pre, const float* __restrict__ u,
+                                const float* __restrict__ w1, const float* __restrict__ b1,
+                                const float* __restrict__ w2, const float* __restrict__ b2,
+                                const float* __restrict__ dtcum, const float* __restrict__ mask, int mask_S,
+                                int mask_ch, float* __restrict__ out, int nc, int tw, int HW, int ka, int kb, int L1,
+                                int act_tanh) {
+    extern __shared__ float d1s[];  // [2nc][L1][64]
+    const int b = blockIdx.y;
+    const int p = threadIdx.x & 63, slot = threadIdx.x >> 6;
+    const int pix = blockIdx.x * 64 + p;
+    const bool valid = pix < HW;
+    const int L = 3 * tw;
+    const int c2 = 2 * nc;
+    const float* pb = pre + (size_t)b * nc * L * HW + pix;
+    for (int o = slot; o < c2; o += 4) {
+        for (int t1 = 0; t1 < L1; ++t1) {
+            float acc = b1[o];
+            if (valid) {
+                for (int ci = 0; ci < nc; ++ci) {
+                    const float* src = pb + (size_t)(ci * L + 2 * t1) * HW;
+                    const float* wr = w1 + (o * nc + ci) * ka;
+                    for (int k = 0; k < ka; ++k) acc = fmaf(wr[k], src[(size_t)k * HW], acc);
+                }
+            }
+            d1s[(o * L1 + t1) * 64 + p] = nps::gelu_erf(acc);
+        }
+    }
+    __syncthreads();
+    if (!valid) return;
+    const float* mrow = mask ? mask + ((size_t)b * mask_S + mask_ch) * HW + pix : nullptr;
+    const float m = mrow ? *mrow : 0.f;
+    for (int o2 = slot; o2 < nc; o2 += 4) {
+        const float ulast = u[(((size_t)b * nc + o2) * tw + (tw - 1)) * HW + pix];
+        for (int t2 = 0; t2 < tw; ++t2) {
+            float acc = b2[o2];
+            for (int o = 0; o < c2; ++o) {
+                const float* wr = w2 + (o2 * c2 + o) * kb;
+                for (int k = 0; k < kb; ++k) acc = fmaf(wr[k], d1s[(o * L1 + t2 + k) * 64 + p], acc);
+            }
+            float v = ulast + dtcum[t2] * acc;
+            if (act_tanh) v = tanhf(v);
+            if (mrow) v = v - m * v;
+            out[(((size_t)b * nc + o2) * tw + t2) * HW + pix] = v;
+        }
+    }
+}
+
+// sums[p] = sum of plane p (fp64)
+__global__ void plane_sums_kernel(const float* __restrict__ base, long plane_stride, int plane_size,
+                                  double* __restrict__ sums) {
+    __shared__ double red[16];
+    const float* pl = base + (size_t)blockIdx.y * plane_stride;
+    double s = 0.0;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < plane_size; i += gridDim.x * blockDim.x) s += pl[i];
+    s = nps::block_sum(s, red);
+    if (threadIdx.x == 0) atomicAdd(&sums[blockIdx.y], s);
+}
+
+// activation_wrapper.py:80-105 'individual_static', element-wise in place
+__global__ void volume_rescale_kernel(float* __restrict__ u, const double* __restrict__ new_tot,
+                                      const double* __restrict__ prev_tot, const float* __restrict__ mpdcum,
+                                      const float* __restrict__ mask, int mask_S, int mask_ch, int nc, int tw, int HW) {
+    const int plane = blockIdx.y;  // (b, c, t)
+    const int t = plane % tw;
+    const int bc = plane / tw;
+    const int b = bc / nc;
+    const float newt = (float)new_tot[plane];
+    const float prev = (float)prev_tot[bc];
+    const float mpd = mpdcum[t];
+    float dif = (1.f - newt / prev) * 100.f;
+    dif = tanhf(dif / mpd) / 100.f * mpd;
+    const float resc = 1.f - dif;
+    const float f = resc * prev;
+    float* pl = u + (size_t)plane * HW;
+    const float* mk = mask ? mask + ((size_t)b * mask_S + mask_ch) * HW : nullptr;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < HW; i += gridDim.x * blockDim.x) {
+        float v = (pl[i] / newt) * f;
+        if (mk) v = v - mk[i] * v;
+        pl[i] = v;
+    }
+}
+
+__global__ void sq_err_kernel(const float* __restrict__ a, const float* __restrict__ b, long n,
+                              double* __restrict__ out) {
+    __shared__ double red[16];
+    double s = 0.0;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+        const float d = a[i] - b[i];
+        s += (double)d * d;
+    }
+    s = nps::block_sum(s, red);
+    if (threadIdx.x == 0) atomicAdd(out, s);
+}
+
+// [B][R][Cc] -> [B][Cc][R] tile transpose (R = H*W pixels, Cc channels)
+__global__ void transpose_kernel(const float* __restrict__ in, float* __restrict__ out, int R, int Cc) {
+    __shared__ float t[32][33];
+    const int b = blockIdx.z;
+    const int r0 = blockIdx.x * 32, c0 = blockIdx.y * 32;
+    const float* ib = in + (size_t)b * R * Cc;
+    float* ob = out + (size_t)b * R * Cc;
+    for (int i = threadIdx.y; i < 32; i += blockDim.y) {
+        const int r = r0 + i, c = c0 + threadIdx.x;
+        if (r < R && c < Cc) t[i][threadIdx.x] = ib[(size_t)r * Cc + c];
+    }
+    __syncthreads();
+    for (int i = threadIdx.y; i < 32; i += blockDim.y) {
+        const int c = c0 + i, r = r0 + threadIdx.x;
+        if (r < R && c < Cc) ob[(size_t)c * R + r] = t[threadIdx.x][i];
+    }
+}
+
+}  // namespace
+
+extern "C" int nps_pack_grid_input(const float* u, const float* pos, const float* cond, const float* sc, float* xin,
+                                   float* vb, int B, int CT, int H, int W, int K, int S, int Cp, void* stream) {
+    NPS_CHECK_ARG(u && pos && xin && B > 0 && CT > 0 && H > 0 && W > 0 && K >= 0 && S >= 0 && Cp >= CT + 2 + K + S,
+                  "pack_grid_input: bad args");
+    NPS_CHECK_ARG((K == 0 || cond) && (S == 0 || sc), "pack_grid_input: missing cond/spatial cond");
+    const size_t lds = sizeof(float) * Cp * 65;
+    NPS_CHECK_ARG(lds <= 64 * 1024, "pack_grid_input: Cp=%d too large", Cp);
+    const int HW = H * W;
+    pack_grid_kernel<<<dim3((HW + 63) / 64, B), 256, lds, (hipStream_t)stream>>>(u, pos, cond, sc, xin,
+                                                                                 (K + S) ? vb : nullptr, CT, HW, K, S,
+                                                                                 Cp);
+    NPS_CHECK_LAUNCH("pack_grid_input");
+    return 0;
+}
+
+extern "C" int nps_timeconv_decode(const float* pre, const float* u, const float* w1, const float* b1, const float* w2,
+                                   const float* b2, const float* dtcum, const float* mask, int mask_S, int mask_ch,
+                                   float* out, int B, int num_c, int tw, int H, int W, int act_tanh, void* stream) {
+    NPS_CHECK_ARG(pre && u && w1 && b1 && w2 && b2 && dtcum && out && B > 0 && num_c > 0 && tw > 0 && H > 0 && W > 0,
+                  "timeconv_decode: bad args");
+    // dec_grid.py:117-124 kernel sizes
+    const int ka = (tw + 1) / 2;
+    const int kb = (tw + 3) / 4 + 1 + (tw % 4 == 0 ? 1 : 0);
+    const int L1 = (3 * tw - ka) / 2 + 1;
+    NPS_CHECK_ARG(L1 - kb + 1 == tw, "timeconv_decode: kernel sizes do not reproduce tw=%d", tw);
+    const size_t lds = sizeof(float) * 2 * num_c * L1 * 64;
+    NPS_CHECK_ARG(lds <= 96 * 1024, "timeconv_decode: num_c=%d too large", num_c);
+    const int HW = H * W;
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)timeconv_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+        attr_set = true;
+    }
+    timeconv_kernel<<<dim3((HW + 63) / 64, B), 256, lds, (hipStream_t)stream>>>(
+        pre, u, w1, b1, w2, b2, dtcum, mask, mask_S, mask_ch, out, num_c, tw, HW, ka, kb, L1, act_tanh);
+    NPS_CHECK_LAUNCH("timeconv_decode");
+    return 0;
+}
+
+extern "C" int nps_plane_sums(const float* base, long plane_stride, int plane_size, int nplanes, double* sums,
+                              void* stream) {
+    NPS_CHECK_ARG(base && sums && plane_size > 0 && nplanes > 0, "plane_sums: bad args");
+    hipStream_t s = (hipStream_t)stream;
+    if (hipMemsetAsync(sums, 0, sizeof(double) * nplanes, s) != hipSuccess) {
+        nps::set_error("plane_sums: memset failed");
+        return -2;
+    }
+    int nb = (plane_size + 256 * 8 - 1) / (256 * 8);
+    nb = nb < 1 ? 1 : (nb > 64 ? 64 : nb);
+    plane_sums_kernel<<<dim3(nb, nplanes), 256, 0, s>>>(base, plane_stride, plane_size, sums);
+    NPS_CHECK_LAUNCH("plane_sums");
+    return 0;
+}
+
+extern "C" int nps_volume_rescale(float* u, const double* new_tot, const double* prev_tot, const float* mpdcum,
+                                  const float* mask, int mask_S, int mask_ch, int B, int num_c, int tw, int H, int W,
+                                  void* stream) {
+    NPS_CHECK_ARG(u && new_tot && prev_tot && mpdcum && B > 0 && num_c > 0 && tw > 0, "volume_rescale: bad args");
+    const int HW = H * W;
+    int nb = (HW + 256 * 4 - 1) / (256 * 4);
+    nb = nb < 1 ? 1 : (nb > 64 ? 64 : nb);
+    volume_rescale_kernel<<<dim3(nb, B * num_c * tw), 256, 0, (hipStream_t)stream>>>(u, new_tot, prev_tot, mpdcum, mask,
+                                                                                     mask_S, mask_ch, num_c, tw, HW);
+    NPS_CHECK_LAUNCH("volume_rescale");
+    return 0;
+}
+
+extern "C" int nps_sq_err_sum(const float* a, const float* b, long n, double* out, void* stream) {
+    NPS_CHECK_ARG(a && b && out && n > 0, "sq_err_sum: bad args");
+    long nb = (n + 256 * 16 - 1) / (256 * 16);
+    nb = nb < 1 ? 1 : (nb > 1024 ? 1024 : nb);
+    sq_err_kernel<<<(unsigned)nb, 256, 0, (hipStream_t)stream>>>(a, b, n, out);
+    NPS_CHECK_LAUNCH("sq_err_sum");
+    return 0;
+}
+
+extern "C" int nps_nchw_to_nhwc(const float* in, float* out, int B, int C, int H, int W, void* stream) {
+    NPS_CHECK_ARG(in && out && B > 0 && C > 0 && H > 0 && W > 0, "nchw_to_nhwc: bad args");
+    // in: [B][C][HW] = [B][R=C][Cc=HW] -> out [B][HW][C]
+    const int R = C, Cc = H * W;
+    transpose_kernel<<<dim3((R + 31) / 32, (Cc + 31) / 32, B), dim3(32, 8), 0, (hipStream_t)stream>>>(in, out, R, Cc);
+    NPS_CHECK_LAUNCH("nchw_to_nhwc");
+    return 0;
+}
+
+extern "C" int nps_nhwc_to_nchw(const float* in, float* out, int B, int C, int H, int W, void* stream) {
+    NPS_CHECK_ARG(in && out && B > 0 && C > 0 && H > 0 && W > 0, "nhwc_to_nchw: bad args");
+    const int R = H * W, Cc = C;
+    transpose_kernel<<<dim3((R + 31) / 32, (Cc + 31) / 32, B), dim3(32, 8), 0, (hipStream_t)stream>>>(in, out, R, Cc);
+    NPS_CHECK_LAUNCH("nhwc_to_nchw");
+    return 0;
+}

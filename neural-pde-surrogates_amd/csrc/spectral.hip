@@ -1,0 +1,341 @@
+// SpectralConv2d forward for gfx950 (proc_fno.py:257-288): truncated DFT analysis,
+// per-mode complex channel mixing, truncated inverse DFT + c2r synthesis.
+//
+// Only the retained 2*m1 x m2 modes exist on device: the forward W-transform
+// keeps m2 of W/2+1 bins, the H-transform keeps R = min(H, 2*m1) rows, so the
+// input is read exactly once and nothing of size B*C*H*(W/2+1) is formed.
+// Every stage streams NHWC activations with C on consecutive lanes (coalesced)
+// and reads twiddles from LDS tables built in-kernel from sincospif of the exact
+// integer phase (k*n mod N)/N.
+#include "nps_common.hpp"
+
+namespace {
+
+constexpr int KW_CHUNK = 16;   // W-bins per pass in the W-transforms
+constexpr int R_CHUNK = 8;     // retained rows per pass in dft_h
+constexpr int MAXR = 32;       // max retained rows in idft_h (m1 <= 16)
+constexpr int MAXB = 8;        // batch rows held in registers by the mixer per pass
+
+// retained row r -> frequency k1 (proc_fno.py:266-269: rows [:m1] and [-m1:])
+__device__ __forceinline__ int row_k1(int r, int H, int R, int m1) { return r < m1 ? r : H - R + r; }
+
+// e^{-2 pi i k n / N} = (cos, -sin)
+__device__ __forceinline__ float2 twiddle(int k, int n, int N) {
+    const int ph = (int)(((long)k * n) % N);
+    float s, c;
+    sincospif(2.0f * (float)ph / (float)N, &s, &c);
+    return make_float2(c, s);  // (cos theta, sin theta), theta = 2 pi k n / N
+}
+
+// X1[b][h][k2][c] = sum_w x[b][h][w][c] e^{-2 pi i k2 w / W}
+__global__ void dft_w_kernel(nps_conv2d_t a, int m2, float2* __restrict__ X1) {
+    extern __shared__ float2 tw[];  // [KW_CHUNK][W]
+    const int h = blockIdx.x, b = blockIdx.y;
+    const int W = a.Win, H = a.Hin, C = a.Cin;
+    for (int kb = 0; kb < m2; kb += KW_CHUNK) {
+        const int nk = min(KW_CHUNK, m2 - kb);
+        __syncthreads();
+        for (int i = threadIdx.x; i < nk * W; i += blockDim.x) tw[i] = twiddle(kb + i / W, i % W, W);
+        __syncthreads();
+        for (int c = threadIdx.x; c < C; c += blockDim.x) {
+            // locate the source of channel c
+            const float* base = nullptr;
+            int sc = 0, sC = 1;
+            int c0 = 0;
+            for (int s = 0; s < a.nsrc; ++s) {
+                if (c >= c0 && c < c0 + a.src[s].C) {
+                    base = a.src[s].ptr;
+                    sc = c - c0;
+                    sC = a.src[s].C;
+                }
+                c0 += a.src[s].C;
+            }
+            const float* row = base + ((size_t)(b * H + h) * W) * sC + sc;
+            float re[KW_CHUNK], im[KW_CHUNK];
+#pragma unroll
+            for (int k = 0; k < KW_CHUNK; ++k) re[k] = im[k] = 0.f;
+            for (int w = 0; w < W; ++w) {
+                const float v = row[(size_t)w * sC];
+#pragma unroll
+                for (int k = 0; k < KW_CHUNK; ++k) {
+                    if (k < nk) {
+                        const float2 t = tw[k * W + w];
+                        re[k] = fmaf(v, t.x, re[k]);
+                        im[k] = fmaf(-v, t.y, im[k]);
+                    }
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < KW_CHUNK; ++k)
+                if (k < nk) X1[((size_t)(b * H + h) * m2 + kb + k) * C + c] = make_float2(re[k], im[k]);
+        }
+    }
+}
+
+// X2[b][r][k2][c] = sum_h X1[b][h][k2][c] e^{-2 pi i k1(r) h / H}
+__global__ void dft_h_kernel(const float2* __restrict__ X1, float2* __restrict__ X2, int H, int R, int m1, int m2,
+                             int C) {
+    extern __shared__ float2 tw[];  // [R_CHUNK][H]
+    const int b = blockIdx.z, r0 = blockIdx.y * R_CHUNK;
+    const int nr = min(R_CHUNK, R - r0);
+    for (int i = threadIdx.x; i < nr * H; i += blockDim.x) tw[i] = twiddle(row_k1(r0 + i / H, H, R, m1), i % H, H);
+    __syncthreads();
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;  // (k2, c)
+    if (idx >= m2 * C) return;
+    float2 acc[R_CHUNK];
+#pragma unroll
+    for (int r = 0; r < R_CHUNK; ++r) acc[r] = make_float2(0.f, 0.f);
+    const float2* src = X1 + (size_t)b * H * m2 * C + idx;
+    for (int hh = 0; hh < H; ++hh) {
+        const float2 v = src[(size_t)hh * m2 * C];
+#pragma unroll
+        for (int r = 0; r < R_CHUNK; ++r) {
+            if (r < nr) {
+                const float2 t = tw[r * H + hh];  // e^{-i th} = (c, -s)
+                acc[r].x = fmaf(v.x, t.x, fmaf(v.y, t.y, acc[r].x));
+                acc[r].y = fmaf(v.y, t.x, fmaf(-v.x, t.y, acc[r].y));
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R_CHUNK; ++r)
+        if (r < nr) X2[((size_t)(b * R + r0 + r) * m2) * C + idx] = acc[r];
+}
+
+// wpack[r][k2][i][o] from weights1/weights2 [Cin][Cout][m1][m2] (complex64)
+__global__ void spec_pack_kernel(const float2* __restrict__ w1, const float2* __restrict__ w2, float2* __restrict__ wp,
+                                 int Cin, int Cout, int H, int R, int m1, int m2) {
+    const size_t n = (size_t)R * m2 * Cin * Cout;
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int o = i % Cout;
+    size_t t = i / Cout;
+    const int ci = t % Cin;
+    t /= Cin;
+    const int k2 = t % m2;
+    const int r = (int)(t / m2);
+    const int k1 = row_k1(r, H, R, m1);
+    // the [-m1:] write happens second and wins where the corners overlap
+    if (k1 >= H - m1)
+        wp[i] = w2[(((size_t)ci * Cout + o) * m1 + (k1 - (H - m1))) * m2 + k2];
+    else
+        wp[i] = w1[(((size_t)ci * Cout + o) * m1 + k1) * m2 + k2];
+}
+
+// Y[b][mode][o] = sum_i X2[b][mode][i] * wp[mode][i][o]   (complex; mode = (r, k2))
+__global__ void mix_kernel(const float2* __restrict__ X2, const float2* __restrict__ wp, float2* __restrict__ Y, int B,
+                           int nmodes, int Cin, int Cout) {
+    extern __shared__ float2 xs[];  // [MAXB][Cin]
+    const int mode = blockIdx.x;
+    const int o = blockIdx.y * blockDim.x + threadIdx.x;
+    for (int b0 = 0; b0 < B; b0 += MAXB) {
+        const int nb = min(MAXB, B - b0);
+        __syncthreads();
+        for (int i = threadIdx.x; i < nb * Cin; i += blockDim.x)
+            xs[i] = X2[((size_t)(b0 + i / Cin) * nmodes + mode) * Cin + i % Cin];
+        __syncthreads();
+        if (o < Cout) {
+            float2 acc[MAXB];
+#pragma unroll
+            for (int bb = 0; bb < MAXB; ++bb) acc[bb] = make_float2(0.f, 0.f);
+            const float2* w = wp + (size_t)mode * Cin * Cout + o;
+            for (int i = 0; i < Cin; ++i) {
+                const float2 wv = w[(size_t)i * Cout];
+#pragma unroll
+                for (int bb = 0; bb < MAXB; ++bb) {
+                    if (bb < nb) {
+                        const float2 xv = xs[bb * Cin + i];
+                        acc[bb].x = fmaf(xv.x, wv.x, fmaf(-xv.y, wv.y, acc[bb].x));
+                        acc[bb].y = fmaf(xv.x, wv.y, fmaf(xv.y, wv.x, acc[bb].y));
+                    }
+                }
+            }
+#pragma unroll
+            for (int bb = 0; bb < MAXB; ++bb)
+                if (bb < nb) Y[((size_t)(b0 + bb) * nmodes + mode) * Cout + o] = acc[bb];
+        }
+    }
+}
+
+// Z[b][h][k2][o] = sum_r Y[b][r][k2][o] e^{+2 pi i k1(r) h / H}
+__global__ void idft_h_kernel(const float2* __restrict__ Y, float2* __restrict__ Z, int H, int R, int m1, int m2,
+                              int Cout) {
+    extern __shared__ float2 tw[];  // [R][H]
+    const int b = blockIdx.z;
+    for (int i = threadIdx.x; i < R * H; i += blockDim.x) tw[i] = twiddle(row_k1(i / H, H, R, m1), i % H, H);
+    __syncthreads();
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;  // (k2, o)
+    if (idx >= m2 * Cout) return;
+    float2 y[MAXR];
+#pragma unroll
+    for (int r = 0; r < MAXR; ++r) y[r] = (r < R) ? Y[((size_t)(b * R + r) * m2) * Cout + idx] : make_float2(0.f, 0.f);
+    for (int hh = 0; hh < H; ++hh) {
+        float re = 0.f, im = 0.f;
+#pragma unroll
+        for (int r = 0; r < MAXR; ++r) {
+            if (r < R) {
+                const float2 t = tw[r * H + hh];  // e^{+i th} = (c, s)
+                re = fmaf(y[r].x, t.x, fmaf(-y[r].y, t.y, re));
+                im = fmaf(y[r].x, t.y, fmaf(y[r].y, t.x, im));
+            }
+        }
+        Z[((size_t)(b * H + hh) * m2) * Cout + idx] = make_float2(re, im);
+    }
+}
+
+// out[b][h][w][o] (=|+=) act( sum_k c_k Re(Z[b][h][k][o] e^{2 pi i k w / W}) / (H W) [+ addend] )
+__global__ void idft_w_kernel(const float2* __restrict__ Z, float* __restrict__ out, int H, int W, int m2, int Cout,
+                              int accumulate, const float* __restrict__ addend, int act) {
+    extern __shared__ float2 tw[];  // [m2][W]
+    const int h = blockIdx.x, b = blockIdx.y;
+    for (int i = threadIdx.x; i < m2 * W; i += blockDim.x) tw[i] = twiddle(i / W, i % W, W);
+    __syncthreads();
+    const float scale = 1.0f / ((float)H * (float)W);
+    for (int o = threadIdx.x; o < Cout; o += blockDim.x) {
+        float zr[KW_CHUNK], zi[KW_CHUNK];
+        for (int kb = 0; kb < m2; kb += KW_CHUNK) {
+            const int nk = min(KW_CHUNK, m2 - kb);
+#pragma unroll
+            for (int k = 0; k < KW_CHUNK; ++k) {
+                float2 z = make_float2(0.f, 0.f);
+                if (k < nk) {
+                    const int kk = kb + k;
+                    z = Z[((size_t)(b * H + h) * m2 + kk) * Cout + o];
+                    // one-sided c2r: DC and (even W) Nyquist count once, with Im discarded
+                    const bool self_conj = (kk == 0) || (2 * kk == W);
+                    const float cm = self_conj ? 1.f : 2.f;
+                    z.x *= cm;
+                    z.y = self_conj ? 0.f : z.y * cm;
+                }
+                zr[k] = z.x;
+                zi[k] = z.y;
+            }
+            for (int w = 0; w < W; ++w) {
+                float v = 0.f;
+#pragma unroll
+                for (int k = 0; k < KW_CHUNK; ++k) {
+                    if (k < nk) {
+                        const float2 t = tw[(kb + k) * W + w];
+                        v = fmaf(zr[k], t.x, fmaf(-zi[k], t.y, v));
+                    }
+                }
+                const size_t di = ((size_t)(b * H + h) * W + w) * Cout + o;
+                if (kb == 0) {
+                    v *= scale;
+                    if (accumulate) v += out[di];
+                } else {
+                    v = out[di] + v * scale;
+                }
+                if (kb + KW_CHUNK >= m2) {
+                    if (addend) v += addend[di];
+                    if (act == 1) v = nps::gelu_erf(v);
+                }
+                out[di] = v;
+            }
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" int nps_spectral_dft_w(const nps_src_t* src, int nsrc, int B, int H, int W, int C, int m2, float* X1,
+                                  void* stream) {
+    NPS_CHECK_ARG(src && nsrc >= 1 && nsrc <= NPS_MAX_SRC && X1 && B > 0 && H > 0 && W > 0 && m2 > 0 &&
+                      m2 <= W / 2 + 1,
+                  "spectral_dft_w: bad args (m2=%d W=%d)", m2, W);
+    nps_conv2d_t a = {};
+    a.nsrc = nsrc;
+    int cs = 0;
+    for (int i = 0; i < nsrc; ++i) {
+        NPS_CHECK_ARG(src[i].H == H && src[i].W == W && src[i].off_y == 0 && src[i].off_x == 0,
+                      "spectral_dft_w: sources must cover the frame");
+        a.src[i] = src[i];
+        cs += src[i].C;
+    }
+    NPS_CHECK_ARG(cs == C, "spectral_dft_w: channel mismatch");
+    a.Hin = H;
+    a.Win = W;
+    a.Cin = C;
+    const size_t lds = sizeof(float2) * KW_CHUNK * W;
+    NPS_CHECK_ARG(lds <= 64 * 1024, "spectral_dft_w: W=%d too large", W);
+    const int bs = C >= 256 ? 256 : ((C + 63) / 64) * 64;
+    dft_w_kernel<<<dim3(H, B), bs, lds, (hipStream_t)stream>>>(a, m2, reinterpret_cast<float2*>(X1));
+    NPS_CHECK_LAUNCH("spectral_dft_w");
+    return 0;
+}
+
+extern "C" int nps_spectral_dft_h(const float* X1, float* X2, int B, int H, int m1, int m2, int C, void* stream) {
+    NPS_CHECK_ARG(X1 && X2 && B > 0 && H > 0 && m1 > 0 && m1 <= H && m2 > 0 && C > 0, "spectral_dft_h: bad args");
+    const int R = H < 2 * m1 ? H : 2 * m1;
+    const size_t lds = sizeof(float2) * R_CHUNK * H;
+    NPS_CHECK_ARG(lds <= 64 * 1024, "spectral_dft_h: H=%d too large", H);
+    dim3 grid((m2 * C + 255) / 256, (R + R_CHUNK - 1) / R_CHUNK, B);
+    dft_h_kernel<<<grid, 256, lds, (hipStream_t)stream>>>(reinterpret_cast<const float2*>(X1),
+                                                          reinterpret_cast<float2*>(X2), H, R, m1, m2, C);
+    NPS_CHECK_LAUNCH("spectral_dft_h");
+    return 0;
+}
+
+extern "C" int nps_spectral_pack_weights(const float* w1, const float* w2, float* wpack, int Cin, int Cout, int H,
+                                         int m1, int m2, void* stream) {
+    NPS_CHECK_ARG(w1 && w2 && wpack && Cin > 0 && Cout > 0 && m1 > 0 && m1 <= H && m2 > 0,
+                  "spectral_pack_weights: bad args");
+    const int R = H < 2 * m1 ? H : 2 * m1;
+    const size_t n = (size_t)R * m2 * Cin * Cout;
+    spec_pack_kernel<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+        reinterpret_cast<const float2*>(w1), reinterpret_cast<const float2*>(w2), reinterpret_cast<float2*>(wpack),
+        Cin, Cout, H, R, m1, m2);
+    NPS_CHECK_LAUNCH("spectral_pack_weights");
+    return 0;
+}
+
+extern "C" int nps_spectral_mix(const float* X2, const float* wpack, float* Y, int B, int R, int m2, int Cin, int Cout,
+                                void* stream) {
+    NPS_CHECK_ARG(X2 && wpack && Y && B > 0 && R > 0 && m2 > 0 && Cin > 0 && Cout > 0, "spectral_mix: bad args");
+    const size_t lds = sizeof(float2) * MAXB * Cin;
+    NPS_CHECK_ARG(lds <= 64 * 1024, "spectral_mix: Cin=%d too large", Cin);
+    const int bs = Cout >= 256 ? 256 : ((Cout + 63) / 64) * 64;
+    dim3 grid(R * m2, (Cout + bs - 1) / bs);
+    mix_kernel<<<grid, bs, lds, (hipStream_t)stream>>>(reinterpret_cast<const float2*>(X2),
+                                                       reinterpret_cast<const float2*>(wpack),
+                                                       reinterpret_cast<float2*>(Y), B, R * m2, Cin, Cout);
+    NPS_CHECK_LAUNCH("spectral_mix");
+    return 0;
+}
+
+extern "C" int nps_spectral_idft_h(const float* Y, float* Z, int B, int H, int m1, int m2, int Cout, void* stream) {
+    NPS_CHECK_ARG(Y && Z && B > 0 && H > 0 && m1 > 0 && m1 <= H && m2 > 0 && Cout > 0, "spectral_idft_h: bad args");
+    const int R = H < 2 * m1 ? H : 2 * m1;
+    NPS_CHECK_ARG(R <= MAXR, "spectral_idft_h: %d retained rows > %d", R, MAXR);
+    const size_t lds = sizeof(float2) * R * H;
+    NPS_CHECK_ARG(lds <= 96 * 1024, "spectral_idft_h: H=%d too large", H);
+    dim3 grid((m2 * Cout + 255) / 256, 1, B);
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)idft_h_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+        (void)hipFuncSetAttribute((const void*)idft_w_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+        attr_set = true;
+    }
+    idft_h_kernel<<<grid, 256, lds, (hipStream_t)stream>>>(reinterpret_cast<const float2*>(Y),
+                                                           reinterpret_cast<float2*>(Z), H, R, m1, m2, Cout);
+    NPS_CHECK_LAUNCH("spectral_idft_h");
+    return 0;
+}
+
+extern "C" int nps_spectral_idft_w(const float* Z, float* out, int B, int H, int W, int m2, int Cout, int accumulate,
+                                   const float* addend, int act, void* stream) {
+    NPS_CHECK_ARG(Z && out && B > 0 && H > 0 && W > 0 && m2 > 0 && m2 <= W / 2 + 1 && Cout > 0,
+                  "spectral_idft_w: bad args");
+    const size_t lds = sizeof(float2) * m2 * W;
+    NPS_CHECK_ARG(lds <= 96 * 1024, "spectral_idft_w: m2*W too large");
+    const int bs = Cout >= 256 ? 256 : ((Cout + 63) / 64) * 64;
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)idft_w_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+        attr_set = true;
+    }
+    idft_w_kernel<<<dim3(H, B), bs, lds, (hipStream_t)stream>>>(reinterpret_cast<const float2*>(Z), out, H, W, m2,
+                                                                Cout, accumulate, addend, act);
+    NPS_CHECK_LAUNCH("spectral_idft_w");
+    return 0;
+}

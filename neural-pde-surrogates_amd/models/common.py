@@ -1,0 +1,168 @@
+"""Conv building blocks of the grid models (reference models/common.py).
+
+The parameter-holding classes subclass torch.nn's Conv2d / ConvTranspose2d /
+GroupNorm so construction, initialisation and `state_dict` keys are identical
+to the reference; their forward never calls aten convolution: it runs the
+gfx950 implicit-GEMM kernel through nps_hip (fails loudly off-GPU).
+"""
+import copy
+
+import torch
+from torch import nn
+
+from nps_hip import ops
+
+
+class Swish(nn.Module):
+    """common.py:7-17 (unused by the twophase cfgs, which pass GELU)."""
+
+    def __init__(self, beta=1):
+        super().__init__()
+        self.beta = beta
+
+    def forward(self, x):
+        raise NotImplementedError("Swish is not on the MI355X hot path (twophase cfgs use GELU)")
+
+
+def activation_code(act):
+    """Map an activation module to the fused-epilogue code of the HIP kernels."""
+    if act is None or isinstance(act, nn.Identity):
+        return 0
+    if isinstance(act, nn.GELU) and getattr(act, "approximate", "none") == "none":
+        return ops.GELU
+    raise NotImplementedError(f"activation {act!r} is not fused on the MI355X path (GELU only)")
+
+
+def crop_offsets(cur_hw, des_hw):
+    """(top, left) placement of a cur-sized map inside a des-sized frame, crop_Nd semantics (common.py:20-34)."""
+    return ops.crop_offset(cur_hw[0], des_hw[0]), ops.crop_offset(cur_hw[1], des_hw[1])
+
+
+def crop_Nd(num_spatial_dims, enc_ftrs, shape):
+    """common.py:20-34 on NCHW device tensors (module-boundary helper; the fused paths never call it)."""
+    if num_spatial_dims != 2:
+        raise NotImplementedError("crop_Nd: 2-D only on the MI355X path")
+    if isinstance(shape, torch.Tensor):
+        shape = shape.shape
+    H, W = shape[-2], shape[-1]
+    B, C, h, w = enc_ftrs.shape
+    oy, ox = crop_offsets((h, w), (H, W))
+    x = ops.nchw_to_nhwc(enc_ftrs)
+    out = torch.zeros((B, H, W, C), dtype=torch.float32, device=x.device)
+    y0, y1 = max(0, oy), min(H, oy + h)
+    x0, x1 = max(0, ox), min(W, ox + w)
+    out[:, y0:y1, x0:x1] = x[:, y0 - oy:y1 - oy, x0 - ox:x1 - ox]
+    return ops.nhwc_to_nchw(out)
+
+
+class _PackedMixin:
+    """Caches the MFMA-packed copy of `weight`, re-packed when the parameter changes."""
+
+    def _packed(self, fn):
+        w = self.weight
+        key = (w.data_ptr(), w._version, str(w.device))
+        if getattr(self, "_pk_key", None) != key:
+            self._pk = fn(w)
+            self._pk_key = key
+        return self._pk
+
+
+class Conv2d(_PackedMixin, nn.Conv2d):
+    """nn.Conv2d parameters; forward = fused HIP implicit-GEMM conv (NHWC internally)."""
+
+    def geometry(self):
+        """(KH, KW, stride, dil, pad_top_left, pad_bottom_right, circ) of this conv."""
+        KH, KW = self.kernel_size
+        if self.stride[0] != self.stride[1] or self.dilation[0] != self.dilation[1]:
+            raise NotImplementedError("anisotropic stride/dilation")
+        s, d = self.stride[0], self.dilation[0]
+        if self.padding == "same":
+            tot = (d * (KH - 1), d * (KW - 1))
+            lo = (tot[0] // 2, tot[1] // 2)
+            hi = (tot[0] - lo[0], tot[1] - lo[1])
+        elif self.padding == "valid":
+            lo = hi = (0, 0)
+        else:
+            lo = hi = tuple(self.padding)
+        if self.padding_mode == "circular":
+            if lo != hi or lo[0] != lo[1]:
+                raise NotImplementedError("asymmetric circular padding")
+            return KH, KW, s, d, (0, 0), (0, 0), lo[0]
+        if self.padding_mode != "zeros":
+            raise NotImplementedError(f"padding_mode {self.padding_mode}")
+        return KH, KW, s, d, lo, hi, 0
+
+    def run(self, srcs, frame_hw, **kw):
+        KH, KW, s, d, lo, hi, circ = self.geometry()
+        return ops.conv2d(srcs, frame_hw, self._packed(ops.pack_conv_weight), self.bias, self.out_channels, KH, KW,
+                          stride=s, dil=d, pad=lo, pad_bottom=hi, circ=circ, **kw)
+
+    def forward(self, x):
+        x = ops.nchw_to_nhwc(x)
+        y = self.run([ops.Src(x)], x.shape[1:3])
+        return ops.nhwc_to_nchw(y)
+
+
+class ConvTranspose2d(_PackedMixin, nn.ConvTranspose2d):
+    """nn.ConvTranspose2d(k=4, s=2) parameters; forward = 4 phase convs on the HIP conv kernel.
+
+    Output phase (py, px) of a stride-2 4x4 transposed conv is a 2x2 conv of the
+    input with taps (py + 2(1-ty), px + 2(1-tx)), written to rows 2*qy+py."""
+    pre_pad = 0  # circular pre-padding (ConvTranspose2d_padded)
+
+    def run(self, x, act=0):
+        if tuple(self.kernel_size) != (4, 4) or tuple(self.stride) != (2, 2) or tuple(self.dilation) != (1, 1) \
+                or tuple(self.output_padding) != (0, 0) or self.groups != 1:
+            raise NotImplementedError("only the U-Net Upsample transposed conv (k=4, s=2) runs on the MI355X path")
+        p = self.padding[0]
+        if self.padding[1] != p or p not in (0, 1):
+            raise NotImplementedError("transposed conv padding must be 0 or 1")
+        B, H, W, C = x.shape
+        c = self.pre_pad
+        Hp, Wp = H + 2 * c, W + 2 * c
+        Ho, Wo = 2 * Hp + 2 - 2 * p, 2 * Wp + 2 - 2 * p
+        out = ops.empty_nhwc(B, Ho, Wo, self.out_channels, x)
+        phases = self._packed(ops.pack_convT_phases)
+        for ph in range(4):
+            py, px = ph >> 1, ph & 1
+            ops.conv2d([ops.Src(x)], (H, W), phases[ph], self.bias, self.out_channels, 2, 2, pad=(1, 1), circ=c,
+                       out_hw=(Hp + 1, Wp + 1), out=out, out_os=2, out_off=(py - p, px - p), act=act)
+        return out
+
+    def forward(self, x):
+        return ops.nhwc_to_nchw(self.run(ops.nchw_to_nhwc(x)))
+
+
+class ConvTranspose2d_padded(ConvTranspose2d):
+    """common.py:93-100: circular_pad_2d(x, pad) then the transposed conv (fused as circular frame extension)."""
+
+    def __init__(self, pad, *args, **kwargs):
+        super().__init__(*args, **kwargs)
+        self.pad = pad
+        self.pre_pad = pad
+
+
+def get_conv_with_right_spatial_dim(spatial_dim, **kwargs):
+    """common.py:37-47."""
+    if spatial_dim == 1:
+        return nn.Conv1d(**kwargs)
+    if spatial_dim == 2:
+        return Conv2d(**kwargs)
+    if spatial_dim == 3:
+        return nn.Conv3d(**kwargs)
+    raise NotImplementedError(f"only 0<x<=3d convs implemented so far, but found spatial dim {spatial_dim}!")
+
+
+def get_upconv_with_right_spatial_dim(spatial_dim, in_channels, out_channels, **kwargs):
+    """common.py:103-120."""
+    if spatial_dim == 1:
+        return nn.ConvTranspose1d(in_channels, out_channels, **kwargs)
+    if spatial_dim == 2:
+        if kwargs.get("padding_mode") == "circular":
+            kernel_size = kwargs["kernel_size"]
+            slice_size = (kernel_size - 1) // 2
+            kw = copy.deepcopy(kwargs)
+            del kw["padding_mode"]
+            return ConvTranspose2d_padded(slice_size, in_channels, out_channels, **kw)
+        return ConvTranspose2d(in_channels, out_channels, **kwargs)
+    raise NotImplementedError(f"only 0<x<=2d convs implemented so far, but found spatial dim {spatial_dim}!")

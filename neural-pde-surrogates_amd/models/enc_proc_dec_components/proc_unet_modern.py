@@ -1,0 +1,321 @@
+"""Modern U-Net (reference models/enc_proc_dec_components/proc_unet_modern.py).
+
+Same module tree / kwargs / state_dict as the reference.  The forward is a
+chain of fused HIP launches on NHWC tensors:
+  * a ResidualBlock = GN-stats(x) -> conv1 [GN+GELU prologue] -> GN-stats ->
+    conv2 [GN+GELU prologue] accumulated at the crop_Nd offset into the
+    shortcut (1x1 conv or x);
+  * torch.cat((h, crop_Nd(skip), crop_Nd(vb))) never exists: the three tensors
+    are sources of one virtual conv input frame with their crop offsets;
+  * the final GN(8)+GELU+conv+crop is one conv launch whose epilogue can also
+    fuse the U-FNO `GELU(h_fno + h_unet)` (proc_ufno.py:118).
+"""
+from typing import List, Tuple, Union
+
+import torch
+from torch import nn
+
+from common.interfaces import D, M
+from models.common import (get_conv_with_right_spatial_dim, get_upconv_with_right_spatial_dim, crop_offsets,
+                           activation_code)
+from nps_hip import ops
+from pdes import PDE
+
+
+def _gn_args(norm_mod, stats):
+    return ops.GN(stats, norm_mod.weight, norm_mod.bias, norm_mod.num_groups, float(norm_mod.eps))
+
+
+class UNetModern(nn.Module):
+    """proc_unet_modern.py:24-196."""
+    model_interface = M.AR_TB
+    data_interface = [D.sim1d, D.sim2d, D.sim1d_var_t]
+
+    def __init__(self, pde: PDE, num_spatial_dims: int = 1, n_cond: int = 0, hidden_features: int = 128,
+                 cond_mode: str = "concat", activation: nn.Module = nn.GELU(), norm: bool = False,
+                 ch_mults: Union[Tuple[int, ...], List[int]] = (1, 2, 2, 4),
+                 is_attn: Union[Tuple[bool, ...], List[bool]] = (False, False, False, False), mid_attn: bool = False,
+                 n_blocks: int = 2, use1x1: bool = False, padding_mode: str = "ones", **kwargs) -> None:
+        super().__init__()
+        self.hidden_features = hidden_features
+        self.num_spatial_dims = num_spatial_dims
+        assert cond_mode in ["concat", None], "Incorrect conditioning mode supplied"
+        self.cond_mode = cond_mode
+        self.n_cond = 0 if self.cond_mode is None else n_cond
+        assert padding_mode in ["ones", "circular"]
+        self.padding_mode = padding_mode
+        padding_kwargs = dict(padding=1) if padding_mode == "ones" else dict(padding_mode="circular")
+        self.activation: nn.Module = activation
+        n_resolutions = len(ch_mults)
+        n_channels = hidden_features
+        down = []
+        out_channels = in_channels = n_channels
+        for i in range(n_resolutions):
+            out_channels = in_channels * ch_mults[i]
+            for _ in range(n_blocks):
+                down.append(DownBlock(in_channels + n_cond, out_channels, has_attn=is_attn[i], activation=activation,
+                                      norm=norm, num_spatial_dims=num_spatial_dims, padding_kwargs=padding_kwargs))
+                in_channels = out_channels
+            if i < n_resolutions - 1:
+                down.append(Downsample(in_channels, num_spatial_dims=num_spatial_dims, n_cond=n_cond,
+                                       padding_kwargs=padding_kwargs))
+        self.down = nn.ModuleList(down)
+        self.middle = MiddleBlock(in_channels=out_channels + n_cond, out_channels=out_channels, has_attn=mid_attn,
+                                  activation=activation, norm=norm, num_spatial_dims=num_spatial_dims,
+                                  padding_kwargs=padding_kwargs)
+        up = []
+        in_channels = out_channels
+        for i in reversed(range(n_resolutions)):
+            out_channels = in_channels
+            for _ in range(n_blocks):
+                up.append(UpBlock(in_channels + n_cond, out_channels, has_attn=is_attn[i], activation=activation,
+                                  norm=norm, num_spatial_dims=num_spatial_dims, padding_kwargs=padding_kwargs))
+            out_channels = in_channels // ch_mults[i]
+            up.append(UpBlock(in_channels + n_cond, out_channels, has_attn=is_attn[i], activation=activation,
+                              norm=norm, num_spatial_dims=num_spatial_dims, padding_kwargs=padding_kwargs))
+            in_channels = out_channels
+            if i > 0:
+                up.append(Upsample(in_channels, num_spatial_dims=num_spatial_dims, padding_kwargs=padding_kwargs))
+        self.up = nn.ModuleList(up)
+        self.norm = nn.GroupNorm(8, n_channels) if norm else nn.Identity()
+        if use1x1:
+            self.final = get_conv_with_right_spatial_dim(num_spatial_dims, in_channels=hidden_features,
+                                                         out_channels=hidden_features, kernel_size=1)
+        else:
+            self.final = get_conv_with_right_spatial_dim(num_spatial_dims, in_channels=hidden_features,
+                                                         out_channels=hidden_features, kernel_size=3, **padding_kwargs)
+
+    def run(self, h, vb, addend=None, act_after=0):
+        """NHWC forward (proc_unet_modern.py:169-196).  Optional fused epilogue on the final conv:
+        out = act_after(final(...) + addend) — the U-FNO block combination."""
+        if self.num_spatial_dims != 2:
+            raise NotImplementedError("UNetModern: 2-D only on the MI355X path")
+        if self.n_cond > 0 and vb is None:
+            # reference Downsample.forward returns a bare tensor here (proc_unet_modern.py:451-455) which
+            # :175 then unpacks along the batch dimension; refuse instead of reproducing that bug
+            raise ValueError("UNetModern with n_cond > 0 needs variables_broadcast")
+        if self.n_cond == 0:
+            vb = None
+        h_shape = h.shape
+        feats, vbs = [h], [vb]
+        for m in self.down:
+            if isinstance(m, Downsample):
+                h, vb = m.run(h, vb)
+            else:
+                h = m.run(h, vb)
+            feats.append(h)
+            vbs.append(vb)
+        h = self.middle.run(h, vb)
+        for m in self.up:
+            if isinstance(m, Upsample):
+                h = m.conv.run(h)
+            else:
+                s = feats.pop()
+                v = vbs.pop()
+                H, W = h.shape[1:3]
+                srcs = [ops.Src(h), ops.Src(s, *crop_offsets(s.shape[1:3], (H, W)))]
+                if v is not None:
+                    srcs.append(ops.Src(v, *crop_offsets(v.shape[1:3], (H, W))))
+                h = m.res.run(srcs, (H, W))
+        # final: conv(act(norm(h))) then crop_Nd to the input size, as one launch
+        H, W = h.shape[1:3]
+        gn = None
+        if isinstance(self.norm, nn.GroupNorm):
+            gn = _gn_args(self.norm, ops.group_norm_stats([ops.Src(h)], (H, W), self.norm.num_groups))
+        oy, ox = crop_offsets(self.final_out_hw(H, W), h_shape[1:3])
+        B, Ht, Wt = h_shape[0], h_shape[1], h_shape[2]
+        out = ops.empty_nhwc(B, Ht, Wt, self.final.out_channels, h)
+        if oy > 0 or ox > 0:
+            out.zero_()  # crop_Nd zero-pads when the output is smaller than the input
+        self.final.run([ops.Src(h)], (H, W), gn=gn, pre_act=activation_code(self.activation), out=out,
+                       out_off=(oy, ox), addends=[addend] if addend is not None else [], act=act_after)
+        return out
+
+    def final_out_hw(self, H, W):
+        KH, KW, s, d, lo, hi, circ = self.final.geometry()
+        return ((H + 2 * circ + lo[0] + hi[0] - d * (KH - 1) - 1) // s + 1,
+                (W + 2 * circ + lo[1] + hi[1] - d * (KW - 1) - 1) // s + 1)
+
+    def forward(self, h: torch.Tensor, variables_broadcast: torch.Tensor = None, pos=None):
+        assert h.dim() == 2 + self.num_spatial_dims
+        vb = ops.nchw_to_nhwc(variables_broadcast) if variables_broadcast is not None else None
+        return ops.nhwc_to_nchw(self.run(ops.nchw_to_nhwc(h), vb))
+
+
+class ResidualBlock(nn.Module):
+    """proc_unet_modern.py:199-250."""
+
+    def __init__(self, in_channels: int, out_channels: int, activation: nn.Module = torch.nn.GELU(),
+                 norm: bool = False, n_groups: int = 1, num_spatial_dims: int = 1, padding_kwargs: dict = None):
+        super().__init__()
+        self.activation: nn.Module = activation
+        padding_kwargs = padding_kwargs or dict()
+        self.conv1 = get_conv_with_right_spatial_dim(num_spatial_dims, in_channels=in_channels,
+                                                     out_channels=out_channels, kernel_size=3, **padding_kwargs)
+        self.conv2 = get_conv_with_right_spatial_dim(num_spatial_dims, in_channels=out_channels,
+                                                     out_channels=out_channels, kernel_size=3, **padding_kwargs)
+        if in_channels != out_channels:
+            self.shortcut = get_conv_with_right_spatial_dim(num_spatial_dims, in_channels=in_channels,
+                                                            out_channels=out_channels, kernel_size=1)
+        else:
+            self.shortcut = nn.Identity()
+        if norm:
+            self.norm1 = nn.GroupNorm(n_groups, in_channels)
+            self.norm2 = nn.GroupNorm(n_groups, out_channels)
+        else:
+            self.norm1 = nn.Identity()
+            self.norm2 = nn.Identity()
+        self.num_spatial_dims = num_spatial_dims
+
+    def run(self, srcs, frame_hw):
+        """srcs: the virtual NHWC input x (concat of slices).  Returns crop_Nd(h, sc) + sc."""
+        act = activation_code(self.activation)
+        H, W = frame_hw
+        gn1 = gn2 = None
+        if isinstance(self.norm1, nn.GroupNorm):
+            gn1 = _gn_args(self.norm1, ops.group_norm_stats(srcs, (H, W), self.norm1.num_groups))
+        h1 = self.conv1.run(srcs, (H, W), gn=gn1, pre_act=act)
+        if isinstance(self.shortcut, nn.Identity):
+            if len(srcs) != 1 or srcs[0].off_y or srcs[0].off_x or tuple(srcs[0].t.shape[1:3]) != (H, W):
+                raise RuntimeError("identity shortcut on a concatenated input")
+            out = srcs[0].t.clone()
+        else:
+            out = self.shortcut.run(srcs, (H, W))
+        H1, W1 = h1.shape[1:3]
+        if isinstance(self.norm2, nn.GroupNorm):
+            gn2 = _gn_args(self.norm2, ops.group_norm_stats([ops.Src(h1)], (H1, W1), self.norm2.num_groups))
+        KH, KW, s, d, lo, hi, circ = self.conv2.geometry()
+        H2 = (H1 + 2 * circ + lo[0] + hi[0] - d * (KH - 1) - 1) // s + 1
+        W2 = (W1 + 2 * circ + lo[1] + hi[1] - d * (KW - 1) - 1) // s + 1
+        oy, ox = crop_offsets((H2, W2), out.shape[1:3])
+        self.conv2.run([ops.Src(h1)], (H1, W1), gn=gn2, pre_act=act, out=out, out_off=(oy, ox), accumulate=True)
+        return out
+
+    def forward(self, x: torch.Tensor):
+        x = ops.nchw_to_nhwc(x)
+        return ops.nhwc_to_nchw(self.run([ops.Src(x)], x.shape[1:3]))
+
+
+class AttentionBlock(nn.Module):
+    """proc_unet_modern.py:253-317 — parameters only (is_attn / mid_attn are False in every cfg)."""
+
+    def __init__(self, in_channels: int, out_channels: int = None, n_heads: int = 1, d_k=None, n_groups: int = 1,
+                 num_spatial_dims: int = 1):
+        super().__init__()
+        out_channels = in_channels if out_channels is None else out_channels
+        d_k = in_channels if d_k is None else d_k
+        self.in_channels, self.out_channels = in_channels, out_channels
+        self.norm = nn.GroupNorm(n_groups, in_channels)
+        self.projection = nn.Linear(in_channels, n_heads * d_k * 3)
+        self.output = nn.Linear(n_heads * d_k, out_channels)
+        self.scale = d_k ** -0.5
+        self.n_heads, self.d_k = n_heads, d_k
+        if in_channels != out_channels:
+            self.shortcut = get_conv_with_right_spatial_dim(num_spatial_dims, in_channels=in_channels,
+                                                            out_channels=out_channels, kernel_size=1)
+        else:
+            self.shortcut = nn.Identity()
+
+    def forward(self, x):
+        raise NotImplementedError("U-Net attention is not on the MI355X path (is_attn=False in all cfgs)")
+
+
+def _check_no_attn(m):
+    if not isinstance(m.attn, nn.Identity):
+        raise NotImplementedError("U-Net attention is not on the MI355X path (is_attn=False in all cfgs)")
+
+
+class DownBlock(nn.Module):
+    """proc_unet_modern.py:320-354."""
+
+    def __init__(self, in_channels: int, out_channels: int, has_attn: bool = False, activation: nn.Module = nn.GELU(),
+                 norm: bool = False, num_spatial_dims: int = 1, padding_kwargs: dict = None):
+        super().__init__()
+        self.res = ResidualBlock(in_channels, out_channels, activation=activation, norm=norm,
+                                 num_spatial_dims=num_spatial_dims, padding_kwargs=padding_kwargs)
+        self.attn = AttentionBlock(out_channels, num_spatial_dims=num_spatial_dims) if has_attn else nn.Identity()
+
+    def run(self, x, vb):
+        _check_no_attn(self)
+        srcs = [ops.Src(x)] + ([ops.Src(vb)] if vb is not None else [])
+        return self.res.run(srcs, x.shape[1:3])
+
+    def forward(self, x: torch.Tensor, variables_broadcast: torch.Tensor = None):
+        vb = ops.nchw_to_nhwc(variables_broadcast) if variables_broadcast is not None else None
+        return ops.nhwc_to_nchw(self.run(ops.nchw_to_nhwc(x), vb)), variables_broadcast
+
+
+class UpBlock(nn.Module):
+    """proc_unet_modern.py:357-391."""
+
+    def __init__(self, in_channels: int, out_channels: int, has_attn: bool = False, activation: nn.Module = nn.GELU(),
+                 norm: bool = False, num_spatial_dims: int = 1, padding_kwargs: dict = None):
+        super().__init__()
+        self.res = ResidualBlock(in_channels + out_channels, out_channels, activation=activation, norm=norm,
+                                 num_spatial_dims=num_spatial_dims, padding_kwargs=padding_kwargs)
+        self.attn = AttentionBlock(out_channels, num_spatial_dims=num_spatial_dims) if has_attn else nn.Identity()
+
+    def forward(self, x: torch.Tensor):
+        _check_no_attn(self)
+        x = ops.nchw_to_nhwc(x)
+        return ops.nhwc_to_nchw(self.res.run([ops.Src(x)], x.shape[1:3]))
+
+
+class MiddleBlock(nn.Module):
+    """proc_unet_modern.py:394-422."""
+
+    def __init__(self, in_channels, out_channels: int, has_attn: bool = False, activation: nn.Module = nn.GELU(),
+                 norm: bool = False, num_spatial_dims: int = 1, padding_kwargs: dict = None):
+        super().__init__()
+        self.res1 = ResidualBlock(in_channels, out_channels, activation=activation, norm=norm,
+                                  num_spatial_dims=num_spatial_dims, padding_kwargs=padding_kwargs)
+        self.attn = AttentionBlock(out_channels, num_spatial_dims=num_spatial_dims) if has_attn else nn.Identity()
+        self.res2 = ResidualBlock(out_channels, out_channels, activation=activation, norm=norm,
+                                  num_spatial_dims=num_spatial_dims, padding_kwargs=padding_kwargs)
+
+    def run(self, x, vb):
+        _check_no_attn(self)
+        srcs = [ops.Src(x)] + ([ops.Src(vb)] if vb is not None else [])
+        h = self.res1.run(srcs, x.shape[1:3])
+        return self.res2.run([ops.Src(h)], h.shape[1:3])
+
+    def forward(self, x: torch.Tensor, variables_broadcast: torch.Tensor = None):
+        vb = ops.nchw_to_nhwc(variables_broadcast) if variables_broadcast is not None else None
+        return ops.nhwc_to_nchw(self.run(ops.nchw_to_nhwc(x), vb)), variables_broadcast
+
+
+class Upsample(nn.Module):
+    """proc_unet_modern.py:425-436 (ConvTranspose2d k=4 s=2, circularly pre-padded in 'circular' mode)."""
+
+    def __init__(self, n_channels: int, num_spatial_dims: int, padding_kwargs: dict):
+        super().__init__()
+        self.conv = get_upconv_with_right_spatial_dim(num_spatial_dims, in_channels=n_channels,
+                                                      out_channels=n_channels, kernel_size=4, stride=2,
+                                                      **padding_kwargs)
+
+    def forward(self, x: torch.Tensor):
+        return self.conv(x)
+
+
+class Downsample(nn.Module):
+    """proc_unet_modern.py:439-455 (3x3 stride-2 conv on h and on the conditioning channels)."""
+
+    def __init__(self, n_channels: int, num_spatial_dims: int, n_cond: int, padding_kwargs: dict):
+        super().__init__()
+        self.conv = get_conv_with_right_spatial_dim(num_spatial_dims, in_channels=n_channels, out_channels=n_channels,
+                                                    kernel_size=3, stride=2, **padding_kwargs)
+        if n_cond > 0:
+            self.conv_variables_broadcast = get_conv_with_right_spatial_dim(
+                num_spatial_dims, in_channels=n_cond, out_channels=n_cond, kernel_size=3, stride=2, **padding_kwargs)
+
+    def run(self, x, vb):
+        h = self.conv.run([ops.Src(x)], x.shape[1:3])
+        if vb is not None:
+            vb = self.conv_variables_broadcast.run([ops.Src(vb)], vb.shape[1:3])
+        return h, vb
+
+    def forward(self, x: torch.Tensor, variables_broadcast: torch.Tensor = None):
+        if variables_broadcast is not None:
+            h, v = self.run(ops.nchw_to_nhwc(x), ops.nchw_to_nhwc(variables_broadcast))
+            return ops.nhwc_to_nchw(h), ops.nhwc_to_nchw(v)
+        return self.conv(x)

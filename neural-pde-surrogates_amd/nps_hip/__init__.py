@@ -1,0 +1,99 @@
+"""ctypes binding of libnps_hip.so — the C ABI declared in include/nps.h.
+
+This is the product's only compute path: every function here launches a
+hand-written gfx950 HIP kernel on the caller's current torch stream.  There is
+no CPU or torch fallback; importing this module raises if the library is
+missing, and every op raises unless its tensors are fp32 on a ROCm device.
+
+Tensors are passed as raw device pointers; PyTorch provides the memory
+(caching allocator), streams and graph capture only.
+"""
+import ctypes
+import os
+
+import torch
+
+__all__ = ["lib", "Src", "Conv2dArgs", "check", "stream_ptr", "ptr", "LIB_PATH"]
+
+LIB_PATH = os.environ.get("NPS_HIP_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "libnps_hip.so"))
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"nps_hip: {LIB_PATH} not found. Build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+        "or `make -C neural-pde-surrogates_amd/csrc` (hipcc --offload-arch=gfx950).")
+lib = ctypes.CDLL(LIB_PATH)
+
+MAX_SRC = 3
+
+
+class Src(ctypes.Structure):
+    _fields_ = [("ptr", ctypes.c_void_p), ("C", ctypes.c_int), ("H", ctypes.c_int), ("W", ctypes.c_int),
+                ("off_y", ctypes.c_int), ("off_x", ctypes.c_int)]
+
+
+class Conv2dArgs(ctypes.Structure):
+    _fields_ = [
+        ("nsrc", ctypes.c_int), ("src", Src * MAX_SRC),
+        ("B", ctypes.c_int), ("Hin", ctypes.c_int), ("Win", ctypes.c_int), ("Cin", ctypes.c_int),
+        ("gn_stats", ctypes.c_void_p), ("gn_gamma", ctypes.c_void_p), ("gn_beta", ctypes.c_void_p),
+        ("gn_groups", ctypes.c_int), ("gn_eps", ctypes.c_float), ("pre_act", ctypes.c_int),
+        ("KH", ctypes.c_int), ("KW", ctypes.c_int), ("stride", ctypes.c_int), ("dil", ctypes.c_int),
+        ("pad_y", ctypes.c_int), ("pad_x", ctypes.c_int), ("circ", ctypes.c_int),
+        ("Hout", ctypes.c_int), ("Wout", ctypes.c_int),
+        ("wpack", ctypes.c_void_p), ("bias", ctypes.c_void_p), ("Cout", ctypes.c_int),
+        ("out", ctypes.c_void_p), ("out_C", ctypes.c_int), ("out_H", ctypes.c_int), ("out_W", ctypes.c_int),
+        ("out_os", ctypes.c_int), ("out_off_y", ctypes.c_int), ("out_off_x", ctypes.c_int),
+        ("out_nchw", ctypes.c_int), ("accumulate", ctypes.c_int),
+        ("addend0", ctypes.c_void_p), ("addend1", ctypes.c_void_p),
+        ("act", ctypes.c_int), ("add_after_act", ctypes.c_int),
+        ("TH", ctypes.c_int), ("TW", ctypes.c_int), ("lattice", ctypes.c_int), ("waves", ctypes.c_int),
+    ]
+
+
+_vp, _i, _l, _sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_size_t
+_SIGS = {
+    "nps_conv2d_packed_size": (_sz, [_i, _i, _i]),
+    "nps_conv2d_pack_weights": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp]),
+    "nps_conv2d_plan": (_i, [ctypes.POINTER(Conv2dArgs)]),
+    "nps_conv2d_fwd": (_i, [ctypes.POINTER(Conv2dArgs), _vp]),
+    "nps_group_norm_stats": (_i, [ctypes.POINTER(Src), _i, _i, _i, _i, _i, _i, _vp, _i, _vp]),
+    "nps_spectral_dft_w": (_i, [ctypes.POINTER(Src), _i, _i, _i, _i, _i, _i, _vp, _vp]),
+    "nps_spectral_dft_h": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp]),
+    "nps_spectral_pack_weights": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _vp]),
+    "nps_spectral_mix": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _vp]),
+    "nps_spectral_idft_h": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp]),
+    "nps_spectral_idft_w": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _i, _vp]),
+    "nps_pack_grid_input": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp]),
+    "nps_timeconv_decode": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _vp, _i, _i, _i, _i, _i, _i,
+                                 _vp]),
+    "nps_plane_sums": (_i, [_vp, _l, _i, _i, _vp, _vp]),
+    "nps_volume_rescale": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp]),
+    "nps_sq_err_sum": (_i, [_vp, _vp, _l, _vp, _vp]),
+    "nps_nchw_to_nhwc": (_i, [_vp, _vp, _i, _i, _i, _i, _vp]),
+    "nps_nhwc_to_nchw": (_i, [_vp, _vp, _i, _i, _i, _i, _vp]),
+    "nps_last_error": (ctypes.c_char_p, []),
+    "nps_version": (ctypes.c_char_p, []),
+}
+for _name, (_res, _args) in _SIGS.items():
+    _f = getattr(lib, _name)  # AttributeError here = the .so does not export what include/nps.h declares
+    _f.restype = _res
+    _f.argtypes = _args
+
+EXPORTED = tuple(_SIGS)
+
+
+def check(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed ({rc}): {lib.nps_last_error().decode()}")
+
+
+def ptr(t):
+    """Device pointer of an fp32/fp64/complex64 ROCm tensor (None -> NULL)."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise RuntimeError("nps_hip ops run on the MI355X only: tensor is on " + str(t.device))
+    return t.data_ptr()
+
+
+def stream_ptr():
+    return torch.cuda.current_stream().cuda_stream

@@ -1,0 +1,256 @@
+"""Torch-tensor front end of the HIP kernels (include/nps.h).
+
+Activations are NHWC fp32 tensors of shape (B, H, W, C).  A conv input is a
+*virtual frame*: a list of `Src(tensor, off_y, off_x)` slices concatenated
+along channels, each placed at an offset of the frame (crop_Nd, cat), so no
+cat / pad / crop is ever materialised.
+"""
+import math
+from typing import List, NamedTuple, Optional, Sequence
+
+import torch
+
+from . import Conv2dArgs, Src as _CSrc, check, lib, ptr, stream_ptr
+
+GELU = 1
+
+# Optional live probe of the conv kernel (bench.py): when a list, every conv2d launch appends
+# (start_event, end_event, algorithmic_flops) recorded on the launching stream.
+conv_probe = None
+
+
+class Src(NamedTuple):
+    t: torch.Tensor          # (B, H, W, C) NHWC contiguous
+    off_y: int = 0
+    off_x: int = 0
+
+
+def _c_src(srcs: Sequence[Src]):
+    arr = (_CSrc * 3)()
+    for i, s in enumerate(srcs):
+        t = s.t
+        if t.dtype != torch.float32 or not t.is_contiguous() or t.dim() != 4:
+            raise RuntimeError(f"nps_hip: sources must be contiguous fp32 NHWC, got {t.dtype} {tuple(t.shape)}")
+        arr[i].ptr = ptr(t)
+        arr[i].H, arr[i].W, arr[i].C = t.shape[1], t.shape[2], t.shape[3]
+        arr[i].off_y, arr[i].off_x = int(s.off_y), int(s.off_x)
+    return arr
+
+
+def crop_offset(cur: int, des: int) -> int:
+    """Top/left zero-pad (negative = crop) that crop_Nd applies when resizing cur -> des
+    (models/common.py:20-34: the ±0.001 tie-break pads the trailing side one more)."""
+    return int(round((des - cur) / 2 - 0.001))
+
+
+def empty_nhwc(B, H, W, C, like: torch.Tensor):
+    return torch.empty((B, H, W, C), dtype=torch.float32, device=like.device)
+
+
+# ----------------------------------------------------------------- weights ----
+def pack_conv_weight(w: torch.Tensor) -> torch.Tensor:
+    """nn.Conv2d weight (Cout, Cin, KH, KW) -> MFMA-fragment-packed buffer."""
+    w = w.detach().contiguous()
+    Cout, Cin, KH, KW = w.shape
+    n = lib.nps_conv2d_packed_size(Cout, Cin, KH * KW)
+    out = torch.empty(n, dtype=torch.float32, device=w.device)
+    check(lib.nps_conv2d_pack_weights(ptr(w), ptr(out), Cout, Cin, KH, KW, -1, stream_ptr()), "conv2d_pack_weights")
+    return out
+
+
+def pack_convT_phases(w: torch.Tensor) -> List[torch.Tensor]:
+    """nn.ConvTranspose2d(k=4, s=2) weight (Cin, Cout, 4, 4) -> 4 packed 2x2 phase convs."""
+    w = w.detach().contiguous()
+    Cin, Cout = w.shape[0], w.shape[1]
+    n = lib.nps_conv2d_packed_size(Cout, Cin, 4)
+    outs = []
+    for ph in range(4):
+        out = torch.empty(n, dtype=torch.float32, device=w.device)
+        check(lib.nps_conv2d_pack_weights(ptr(w), ptr(out), Cout, Cin, 2, 2, ph, stream_ptr()), "pack convT")
+        outs.append(out)
+    return outs
+
+
+def pack_spectral_weight(w1: torch.Tensor, w2: torch.Tensor, H: int) -> torch.Tensor:
+    """weights1/weights2 (Cin, Cout, m1, m2) complex64 -> [R][m2][Cin][Cout] complex for frame height H."""
+    w1 = w1.detach().contiguous()
+    w2 = w2.detach().contiguous()
+    Cin, Cout, m1, m2 = w1.shape
+    R = min(H, 2 * m1)
+    out = torch.empty((R, m2, Cin, Cout), dtype=torch.complex64, device=w1.device)
+    check(lib.nps_spectral_pack_weights(ptr(w1), ptr(w2), ptr(out), Cin, Cout, H, m1, m2, stream_ptr()),
+          "spectral_pack_weights")
+    return out
+
+
+# ------------------------------------------------------------------- conv -----
+class GN(NamedTuple):
+    stats: torch.Tensor      # (B, G, 2) float64
+    gamma: torch.Tensor
+    beta: torch.Tensor
+    groups: int
+    eps: float
+
+
+def group_norm_stats(srcs: Sequence[Src], frame_hw, groups: int) -> torch.Tensor:
+    t0 = srcs[0].t
+    B = t0.shape[0]
+    Cin = sum(s.t.shape[3] for s in srcs)
+    stats = torch.empty((B, groups, 2), dtype=torch.float64, device=t0.device)
+    check(lib.nps_group_norm_stats(_c_src(srcs), len(srcs), B, frame_hw[0], frame_hw[1], Cin, groups, ptr(stats), 1,
+                                   stream_ptr()), "group_norm_stats")
+    return stats
+
+
+def conv2d(srcs: Sequence[Src], frame_hw, wpack: torch.Tensor, bias: Optional[torch.Tensor], Cout: int, KH: int,
+           KW: int, stride=1, dil=1, pad=(0, 0), circ=0, out_hw=None, gn: Optional[GN] = None, pre_act=0,
+           out: Optional[torch.Tensor] = None, out_nchw=False, out_os=1, out_off=(0, 0), accumulate=False,
+           addends: Sequence[torch.Tensor] = (), act=0, add_after_act=False, pad_bottom=None):
+    """One fused conv launch.  `pad` = top/left zero padding (in the circularly
+    extended frame), `pad_bottom` defaults to `pad`.  Returns `out`."""
+    t0 = srcs[0].t
+    B = t0.shape[0]
+    Hin, Win = int(frame_hw[0]), int(frame_hw[1])
+    Cin = sum(s.t.shape[3] for s in srcs)
+    pb = pad if pad_bottom is None else pad_bottom
+    if out_hw is None:
+        Hout = (Hin + 2 * circ + pad[0] + pb[0] - dil * (KH - 1) - 1) // stride + 1
+        Wout = (Win + 2 * circ + pad[1] + pb[1] - dil * (KW - 1) - 1) // stride + 1
+    else:
+        Hout, Wout = out_hw
+    if Hout <= 0 or Wout <= 0:
+        raise RuntimeError(f"nps_hip conv2d: empty output {Hout}x{Wout} for input {Hin}x{Win} k={KH}")
+    if out is None:
+        out = (torch.empty((B, Cout, Hout, Wout), dtype=torch.float32, device=t0.device) if out_nchw
+               else empty_nhwc(B, Hout, Wout, Cout, t0))
+    if out_nchw:
+        oC, oH, oW = out.shape[1], out.shape[2], out.shape[3]
+    else:
+        oH, oW, oC = out.shape[1], out.shape[2], out.shape[3]
+    a = Conv2dArgs()
+    a.nsrc = len(srcs)
+    a.src = _c_src(srcs)
+    a.B, a.Hin, a.Win, a.Cin = B, Hin, Win, Cin
+    if gn is not None:
+        a.gn_stats, a.gn_gamma, a.gn_beta = ptr(gn.stats), ptr(gn.gamma), ptr(gn.beta)
+        a.gn_groups, a.gn_eps = gn.groups, gn.eps
+    a.pre_act = pre_act
+    a.KH, a.KW, a.stride, a.dil = KH, KW, stride, dil
+    a.pad_y, a.pad_x, a.circ = pad[0], pad[1], circ
+    a.Hout, a.Wout = Hout, Wout
+    a.wpack, a.bias, a.Cout = ptr(wpack), ptr(bias), Cout
+    a.out, a.out_C, a.out_H, a.out_W = ptr(out), oC, oH, oW
+    a.out_os, a.out_off_y, a.out_off_x = out_os, out_off[0], out_off[1]
+    a.out_nchw = 1 if out_nchw else 0
+    a.accumulate = 1 if accumulate else 0
+    ads = list(addends)
+    a.addend0 = ptr(ads[0]) if len(ads) > 0 else None
+    a.addend1 = ptr(ads[1]) if len(ads) > 1 else None
+    a.act, a.add_after_act = act, (1 if add_after_act else 0)
+    if lib.nps_conv2d_plan(ctypes_byref(a)) < 0:
+        raise RuntimeError("conv2d_plan failed: " + lib.nps_last_error().decode())
+    if conv_probe is not None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        check(lib.nps_conv2d_fwd(ctypes_byref(a), stream_ptr()), "conv2d_fwd")
+        e1.record()
+        conv_probe.append((e0, e1, 2.0 * B * Hout * Wout * Cout * Cin * KH * KW))
+    else:
+        check(lib.nps_conv2d_fwd(ctypes_byref(a), stream_ptr()), "conv2d_fwd")
+    return out
+
+
+def ctypes_byref(x):
+    import ctypes
+    return ctypes.byref(x)
+
+
+# --------------------------------------------------------------- spectral -----
+def spectral_conv2d(srcs: Sequence[Src], wpack: torch.Tensor, m1: int, m2: int, Cout: int,
+                    out: Optional[torch.Tensor] = None, accumulate=False, addend=None, act=0):
+    """y = irfft2(P(rfft2(x))) on the retained modes (proc_fno.py:257-288), NHWC in/out."""
+    t0 = srcs[0].t
+    B, H, W = t0.shape[0], t0.shape[1], t0.shape[2]
+    Cin = sum(s.t.shape[3] for s in srcs)
+    if not (m1 <= H and m2 <= W // 2 + 1):
+        raise AssertionError("modes should be at most the spatial dim (// 2 + 1 for the last spatial dimension)")
+    R = min(H, 2 * m1)
+    dev = t0.device
+    X1 = torch.empty((B, H, m2, Cin), dtype=torch.complex64, device=dev)
+    X2 = torch.empty((B, R, m2, Cin), dtype=torch.complex64, device=dev)
+    Y = torch.empty((B, R, m2, Cout), dtype=torch.complex64, device=dev)
+    Z = torch.empty((B, H, m2, Cout), dtype=torch.complex64, device=dev)
+    if out is None:
+        out = empty_nhwc(B, H, W, Cout, t0)
+        accumulate = False
+    s = stream_ptr()
+    check(lib.nps_spectral_dft_w(_c_src(srcs), len(srcs), B, H, W, Cin, m2, ptr(X1), s), "spectral_dft_w")
+    check(lib.nps_spectral_dft_h(ptr(X1), ptr(X2), B, H, m1, m2, Cin, s), "spectral_dft_h")
+    check(lib.nps_spectral_mix(ptr(X2), ptr(wpack), ptr(Y), B, R, m2, Cin, Cout, s), "spectral_mix")
+    check(lib.nps_spectral_idft_h(ptr(Y), ptr(Z), B, H, m1, m2, Cout, s), "spectral_idft_h")
+    check(lib.nps_spectral_idft_w(ptr(Z), ptr(out), B, H, W, m2, Cout, 1 if accumulate else 0, ptr(addend), act, s),
+          "spectral_idft_w")
+    return out
+
+
+# ----------------------------------------------------------- misc kernels -----
+def nchw_to_nhwc(x: torch.Tensor) -> torch.Tensor:
+    x = x.contiguous()
+    B, C, H, W = x.shape
+    out = torch.empty((B, H, W, C), dtype=torch.float32, device=x.device)
+    check(lib.nps_nchw_to_nhwc(ptr(x), ptr(out), B, C, H, W, stream_ptr()), "nchw_to_nhwc")
+    return out
+
+
+def nhwc_to_nchw(x: torch.Tensor) -> torch.Tensor:
+    B, H, W, C = x.shape
+    out = torch.empty((B, C, H, W), dtype=torch.float32, device=x.device)
+    check(lib.nps_nhwc_to_nchw(ptr(x), ptr(out), B, C, H, W, stream_ptr()), "nhwc_to_nchw")
+    return out
+
+
+def pack_grid_input(u, pos, cond, sc, Cp):
+    """-> (xin (B,H,W,Cp), vb (B,H,W,K+S) or None)."""
+    B, c, tw, H, W = u.shape
+    K = 0 if cond is None else cond.shape[1]
+    S = 0 if sc is None else sc.shape[1]
+    xin = torch.empty((B, H, W, Cp), dtype=torch.float32, device=u.device)
+    vb = torch.empty((B, H, W, K + S), dtype=torch.float32, device=u.device) if K + S > 0 else None
+    check(lib.nps_pack_grid_input(ptr(u), ptr(pos), ptr(cond), ptr(sc), ptr(xin), ptr(vb), B, c * tw, H, W, K, S, Cp,
+                                  stream_ptr()), "pack_grid_input")
+    return xin, vb
+
+
+def timeconv_decode(pre, u, w1, b1, w2, b2, dtcum, mask, mask_ch, act_tanh, num_c, tw):
+    B, _, _, H, W = u.shape
+    out = torch.empty((B, num_c, tw, H, W), dtype=torch.float32, device=u.device)
+    S = 0 if mask is None else mask.shape[1]
+    check(lib.nps_timeconv_decode(ptr(pre), ptr(u), ptr(w1), ptr(b1), ptr(w2), ptr(b2), ptr(dtcum), ptr(mask), S,
+                                  mask_ch, ptr(out), B, num_c, tw, H, W, 1 if act_tanh else 0, stream_ptr()),
+          "timeconv_decode")
+    return out
+
+
+def plane_sums(base: torch.Tensor, offset: int, plane_stride: int, plane_size: int, nplanes: int) -> torch.Tensor:
+    sums = torch.empty(nplanes, dtype=torch.float64, device=base.device)
+    check(lib.nps_plane_sums(ptr(base) + 4 * offset, plane_stride, plane_size, nplanes, ptr(sums), stream_ptr()),
+          "plane_sums")
+    return sums
+
+
+def volume_rescale(u, new_tot, prev_tot, mpdcum, mask, mask_ch):
+    B, c, tw, H, W = u.shape
+    S = 0 if mask is None else mask.shape[1]
+    check(lib.nps_volume_rescale(ptr(u), ptr(new_tot), ptr(prev_tot), ptr(mpdcum), ptr(mask), S, mask_ch, B, c, tw,
+                                 H, W, stream_ptr()), "volume_rescale")
+    return u
+
+
+def sq_err_sum(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    a = a.contiguous()
+    b = b.contiguous()
+    if a.shape != b.shape:
+        raise RuntimeError(f"sq_err_sum: shape mismatch {tuple(a.shape)} vs {tuple(b.shape)}")
+    out = torch.zeros(1, dtype=torch.float64, device=a.device)
+    check(lib.nps_sq_err_sum(ptr(a), ptr(b), a.numel(), ptr(out), stream_ptr()), "sq_err_sum")
+    return out[0]

@@ -1,0 +1,139 @@
+"""Autoregressive rollout driver (reference trainers/autoregressivepushforwardtrainer.py).
+
+`simulate` keeps the reference's signature, loop bounds (:354-358), loss
+normalisation (:422, :433-434) and return conventions, with the trajectory
+resident on the device (windows are views, no per-step host copies) and the
+MSE_sum criterion computed by a HIP fp64 reduction.  Grid models only.
+"""
+import argparse
+import math
+from typing import Tuple
+
+import torch
+from torch import nn
+
+from common.interfaces import D, M
+from nps_hip import ops
+
+
+class DataCreator:
+    """common/data_creator.py:48-78 (windowing only; the GNN graph builders are not built)."""
+
+    def __init__(self, pde=None, neighbors: int = 2, time_window: int = 5, t_resolution: int = 250,
+                 x_resolution=100):
+        self.pde = pde
+        self.n = neighbors
+        self.tw = time_window
+        self.t_res = t_resolution
+        self.x_res = x_resolution
+        assert isinstance(self.n, int)
+        assert isinstance(self.tw, int)
+
+    def to(self, device):
+        return self
+
+    def create_data(self, datapoints: torch.Tensor, steps: list, mode="both"):
+        assert mode in ["data", "labels", "both"]
+        T = datapoints.shape[2]
+        for step in steps:
+            assert step - self.tw >= 0 and step + self.tw <= T, 'this step - time window combination is not valid'
+        if len(set(steps)) == 1:  # the rollout case: one slice of the whole batch, no per-sample cat
+            s = steps[0]
+            data = datapoints[:, :, s - self.tw:s]
+            labels = datapoints[:, :, s:s + self.tw]
+        else:
+            data = torch.stack([dp[:, s - self.tw:s] for dp, s in zip(datapoints, steps)])
+            labels = torch.stack([dp[:, s:s + self.tw] for dp, s in zip(datapoints, steps)])
+        if mode == "data":
+            return data
+        if mode == "labels":
+            return labels
+        return data, labels
+
+
+class AutoregressivePushforwardTrainer:
+    data_interface = [D.sim1d, D.sim2d, D.sim1d_var_t]
+    model_interface = [M.AR_TB, M.AR_TB_GNN]
+
+    def __init__(self, model, data, criterion, optimizer=None, lr_scheduler=None, config: argparse.Namespace = None,
+                 save_path: str = "models/model.pt", **kwargs):
+        self.model = model
+        self.data = data
+        self.config = config if config is not None else argparse.Namespace(**kwargs)
+        self.config.save_path = save_path
+        self.criterion = criterion
+        self.optimizer = optimizer
+        self.lr_scheduler = lr_scheduler
+        if not hasattr(self.config, "process_settings"):
+            self.config.process_settings = {}
+        self.data_creator = DataCreator(pde=self.data.pde, neighbors=getattr(self.config, "neighbors", 3),
+                                        time_window=self.config.time_window,
+                                        t_resolution=self.config.base_resolution[0],
+                                        x_resolution=self.config.base_resolution[1])
+
+    def _loss(self, pred, labels):
+        c = self.criterion
+        if isinstance(c, nn.MSELoss) and c.reduction == "sum":
+            return ops.sq_err_sum(pred, labels)
+        return c(pred, labels)
+
+    def simulate(self, u, conditioning, x, compute_loss, include_data, nr_gt_steps, t_res,
+                 t_conditioning=torch.empty(0), spatial_conditioning=torch.empty(0), clip_min=True, use_bc=True,
+                 u_bc=None, u_mask=None, divide_by_t=True):
+        """autoregressivepushforwardtrainer.py:288-440 (grid models; process_step is a no-op for twophase)."""
+        use_mask = u_mask is not None
+        if compute_loss is False and use_mask:
+            raise ValueError("Mask supplied for computing the loss, but 'compute_loss'=False!")
+        if compute_loss is True and u.shape[2] < t_res:
+            raise ValueError("Cannot compute loss if no ground-truth simulation is provided for the full rollout")
+        if u_bc is None:
+            u_bc = u
+        if use_bc and u_bc.shape[2] < t_res:
+            raise ValueError("Cannot set BCs if the provided BC information is <= the unrolling time")
+        if u.shape[2] < nr_gt_steps * self.data_creator.tw:
+            raise ValueError("The training data is shorter than the specified number of unrolling steps")
+        if self.model.model_interface != M.AR_TB:
+            raise NotImplementedError("graph (GNN) models are not on the MI355X path")
+        if str(getattr(self.data.pde, "name", "")) == "DIV1D":
+            raise NotImplementedError("DIV1D boundary processing is not on the grid path")
+        use_t_conditioning = torch.numel(t_conditioning) != 0
+        use_spatial_conditioning = torch.numel(spatial_conditioning) != 0
+        batch_size = u.shape[0]
+        device = self.config.device
+        tw = self.data_creator.tw
+        pred = self.data_creator.create_data(u, [tw * nr_gt_steps] * batch_size, mode="data").to(device)
+        if include_data:
+            data_gt = [pred] if compute_loss else None
+            data_pred = [pred]
+        losses = []
+        n_t = 0
+        for step in range(tw * nr_gt_steps, t_res - tw + 1, tw):
+            same_steps = [step] * batch_size
+            if compute_loss:
+                labels = self.data_creator.create_data(u, same_steps, mode="labels").to(device)
+            if use_mask:
+                labels_mask = self.data_creator.create_data(u_mask, same_steps, mode="labels").to(device)
+            t_cond = self.data_creator.create_data(t_conditioning, same_steps, mode="labels") \
+                if use_t_conditioning else None
+            spatial_cond = spatial_conditioning if use_spatial_conditioning else None
+            pred = self.model(pred, cond=conditioning, bc=None, pos=x, t_cond=t_cond, spatial_cond=spatial_cond)
+            if compute_loss and use_mask:
+                pred = pred * labels_mask
+                labels = labels * labels_mask
+            if compute_loss:
+                loss = self._loss(pred, labels) / math.prod(self.config.base_resolution[1:])
+                losses.append(loss / batch_size)
+            if include_data:
+                if compute_loss:
+                    data_gt.append(labels)
+                data_pred.append(pred)
+            n_t += tw
+        if divide_by_t:
+            losses = [v / n_t for v in losses]
+        losses = [v.float() for v in losses]
+        if compute_loss and not include_data:
+            return losses
+        elif not compute_loss and include_data:
+            return data_pred
+        else:
+            return losses, (data_gt, data_pred)

@@ -1,0 +1,202 @@
+"""GPU parity: the HIP path (through the C ABI) vs the pinned CPU oracle / reference goldens.
+
+Tolerance: fp32 rel-L2 < 1e-5 (BASELINE.json north star; fp32 noise floor ~1e-7).
+"""
+import pytest
+import torch
+from torch import nn
+
+import oracle
+from oracle import functional as Fo
+from conftest import load_golden, rel_l2
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+DEV = "cuda"
+
+
+def _gelu():
+    return nn.GELU()
+
+
+# ------------------------------------------------------------------ conv unit tests
+CONV_CASES = [
+    # (Cin, Cout, k, stride, dil, padding, padding_mode, H, W)
+    (16, 64, 3, 1, 1, 0, "zeros", 20, 20),          # valid 3x3
+    (196, 192, 3, 1, 1, 0, "zeros", 33, 35),        # U-FNO shape, chunk tail (196 = 12*16 + 4)
+    (7, 5, 3, 1, 1, 1, "zeros", 17, 13),            # zero pad, odd channels (scalar gather path)
+    (12, 12, 3, 2, 1, 0, "zeros", 31, 29),          # downsample s2 valid
+    (12, 40, 3, 2, 1, 1, "zeros", 16, 16),          # downsample s2 pad 1
+    (8, 8, 5, 1, 2, "same", "circular", 24, 24),    # DRN dilated circular
+    (8, 8, 5, 1, 8, "same", "circular", 20, 20),    # dilation 8 > tile lattice
+    (132, 128, 5, 1, 4, "same", "circular", 40, 36),
+    (81, 192, 1, 1, 1, 0, "zeros", 19, 23),         # encoder 1x1, Cin % 4 != 0
+    (192, 75, 1, 1, 1, 0, "zeros", 16, 16),         # pre-decoder 1x1, Cout % 32 != 0
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv2d_vs_torch(case):
+    from models.common import Conv2d
+    Cin, Cout, k, s, d, p, pm, H, W = case
+    torch.manual_seed(0)
+    m = Conv2d(Cin, Cout, k, stride=s, dilation=d, padding=p, padding_mode=pm)
+    x = torch.randn(2, Cin, H, W)
+    ref = Fo.conv2d_ref(x, {"weight": m.weight.detach(), "bias": m.bias.detach()}, "", stride=s, padding=p,
+                        dilation=d, padding_mode=pm)
+    y = m.to(DEV)(x.to(DEV)).cpu()
+    assert y.shape == ref.shape
+    assert rel_l2(y, ref) < TOL
+
+
+@pytest.mark.parametrize("circ", [True, False])
+def test_conv_transpose_vs_torch(circ):
+    from models.common import ConvTranspose2d, ConvTranspose2d_padded
+    torch.manual_seed(0)
+    if circ:
+        m = ConvTranspose2d_padded(1, 24, 20, kernel_size=4, stride=2)
+    else:
+        m = ConvTranspose2d(24, 20, kernel_size=4, stride=2, padding=1)
+    x = torch.randn(2, 24, 13, 11)
+    sd = {"weight": m.weight.detach(), "bias": m.bias.detach()}
+    ref = Fo.conv_transpose_ref(x, sd, "", stride=2, padding=0 if circ else 1, circ_pre_pad=1 if circ else 0)
+    y = m.to(DEV)(x.to(DEV)).cpu()
+    assert y.shape == ref.shape
+    assert rel_l2(y, ref) < TOL
+
+
+def test_residual_block_concat_crop_groupnorm():
+    """UpBlock-style input cat(h, crop(s), crop(vb)) with GN(1)+GELU prologues and crop-pad residual."""
+    from models.enc_proc_dec_components.proc_unet_modern import ResidualBlock
+    from nps_hip import ops
+    torch.manual_seed(0)
+    rb = ResidualBlock(20 + 16 + 4, 16, activation=_gelu(), norm=True, num_spatial_dims=2,
+                       padding_kwargs=dict(padding_mode="circular"))
+    with torch.no_grad():
+        for n in (rb.norm1, rb.norm2):
+            n.weight.uniform_(0.5, 1.5)
+            n.bias.uniform_(-0.3, 0.3)
+    h = torch.randn(2, 20, 30, 30)
+    s = torch.randn(2, 16, 27, 27)   # crop_Nd pads 27 -> 30 (1 top, 2 bottom)
+    v = torch.rand(2, 4, 33, 33)     # crop_Nd crops 33 -> 30
+    x = torch.cat([h, Fo.crop_nd(s, h.shape), Fo.crop_nd(v, h.shape)], dim=1)
+    ref = Fo.residual_block({k: t.detach() for k, t in rb.state_dict().items()}, "", x, True,
+                            dict(padding_mode="circular"))
+    rb = rb.to(DEV)
+    hd, sd_, vd = (ops.nchw_to_nhwc(t.to(DEV)) for t in (h, s, v))
+    srcs = [ops.Src(hd), ops.Src(sd_, ops.crop_offset(27, 30), ops.crop_offset(27, 30)),
+            ops.Src(vd, ops.crop_offset(33, 30), ops.crop_offset(33, 30))]
+    y = ops.nhwc_to_nchw(rb.run(srcs, (30, 30))).cpu()
+    assert rel_l2(y, ref) < TOL
+
+
+# ------------------------------------------------------------------ spectral
+@pytest.mark.parametrize("name", ["spectral2d_a", "spectral2d_overlap", "spectral2d_nyq"])
+def test_spectral2d_golden(name):
+    from models.enc_proc_dec_components.proc_fno import SpectralConv2d
+    g = load_golden(name)
+    kw = g["kwargs"]
+    m = SpectralConv2d(kw["in_channels"], kw["out_channels"], tuple(kw["modes"]))
+    m.load_state_dict(g["state_dict"])
+    y = m.to(DEV)(g["x"].to(DEV)).cpu()
+    assert rel_l2(y, g["y"]) < TOL
+
+
+@pytest.mark.parametrize("H,W,m", [(128, 128, 12), (256, 256, 10), (96, 64, 10)])
+def test_spectral2d_full_size(H, W, m):
+    """U-FNO spectral conv at the BASELINE sizes (196 -> 192 channels) vs the torch.fft oracle."""
+    from models.enc_proc_dec_components.proc_fno import SpectralConv2d
+    torch.manual_seed(1)
+    sc = SpectralConv2d(196, 192, (m, m))
+    x = torch.randn(2, 196, H, W)
+    ref = Fo.spectral_conv2d(x, sc.weights1.detach(), sc.weights2.detach())
+    y = sc.to(DEV)(x.to(DEV)).cpu()
+    assert rel_l2(y, ref) < TOL
+
+
+def test_fno_layer_golden():
+    from models.enc_proc_dec_components.proc_fno import FNO_Layer
+    g = load_golden("fno_layer")
+    m = FNO_Layer(**g["kwargs"])
+    m.load_state_dict(g["state_dict"])
+    y = m.to(DEV)(g["x"].to(DEV)).cpu()
+    assert rel_l2(y, g["y"]) < TOL
+
+
+# ------------------------------------------------------------------ processors
+def _proc(name):
+    from models.enc_proc_dec_components import UNetModern, DilatedResnet, UFNO, FNO
+    cls = {"unet_ufno_style": UNetModern, "unet_cfg": UNetModern, "unet_ones": UNetModern, "drn": DilatedResnet,
+           "ufno": UFNO, "fno": FNO}[name]
+    g = load_golden(name)
+    kw = dict(g["kwargs"])
+    if cls is not FNO:
+        kw["activation"] = _gelu()
+    m = cls(pde=None, **kw)
+    m.load_state_dict(g["state_dict"])
+    return m.to(DEV), g
+
+
+@pytest.mark.parametrize("name", ["unet_ufno_style", "unet_cfg", "unet_ones", "drn", "ufno", "fno"])
+def test_processor_golden(name):
+    m, g = _proc(name)
+    with torch.no_grad():
+        y = m(h=g["h"].to(DEV), variables_broadcast=g["vb"].to(DEV)).cpu()
+    assert y.shape == g["y"].shape
+    assert rel_l2(y, g["y"]) < TOL
+
+
+# ------------------------------------------------------------------ full models + rollout
+def _build_model(g):
+    import models
+    from pdes import PDE2D
+    cfg = dict(g["cfg"])
+    cfg.pop("object")
+    cfg["activation"] = _gelu()
+    cfg["activation_final"] = nn.Tanh()
+    p = g["pde"]
+    pde = PDE2D(tmin=p["tmin"], tmax=p["tmax"], nt=p["nt"], L1=1.0, L2=1.0, nx1=p["nx1"], nx2=p["nx2"], x=None,
+                name="twophase", n_cond_static=p["n_cond_static"], n_cond_spatial=p["n_cond_spatial"])
+    m = models.activation_wrapper(**cfg, pde=pde)
+    m.load_state_dict(g["state_dict"])
+    return m.to(DEV).eval(), pde
+
+
+@pytest.mark.parametrize("name", ["model_ufno", "model_unet", "model_drn", "model_ufno_fno"])
+def test_model_and_simulate_golden(name):
+    import argparse
+    import types
+    from common.interfaces import D
+    from trainers.autoregressivepushforwardtrainer import AutoregressivePushforwardTrainer
+    g = load_golden(name)
+    m, pde = _build_model(g)
+    tw = g["cfg"]["time_window"]
+    u, cond, pos, sc = (g[k].to(DEV) for k in ("u", "cond", "pos", "spatial_cond"))
+    with torch.no_grad():
+        y = m(u[:, :, :tw], cond=cond, bc=None, pos=pos, t_cond=None, spatial_cond=sc).cpu()
+    assert rel_l2(y, g["y"]) < TOL
+    T = u.shape[2]
+    cfg = argparse.Namespace(time_window=tw, base_resolution=(T, u.shape[3], u.shape[4]), device=DEV, nr_gt_steps=1)
+    tr = AutoregressivePushforwardTrainer(model=m, data=types.SimpleNamespace(pde=pde, data_interface=D.sim2d),
+                                          criterion=nn.MSELoss(reduction="sum"), config=cfg)
+    with torch.no_grad():
+        losses, (gt, preds) = tr.simulate(u, cond, pos, compute_loss=True, include_data=True, nr_gt_steps=1, t_res=T,
+                                          spatial_conditioning=sc)
+    pred = torch.cat(preds[1:], dim=2).cpu()
+    assert rel_l2(pred, g["sim_pred"]) < TOL
+    assert rel_l2(torch.stack([l.cpu() for l in losses]), g["sim_losses"]) < TOL
+
+
+def test_ufno_c3_full_size_one_call():
+    """North-star config C3: U-FNO twophase cfg (hidden 192, 3 blocks, modes 10) at 256x256, 3 fields,
+    obstacle, B=1 — one rollout model call vs the CPU oracle."""
+    import __graft_entry__  # noqa: F401
+    from bench import build_model, ORACLE_PDE
+    from trainers.synthetic import twophase_batch
+    m, ocfg, opde = build_model("ufno", res=256, num_c=3, device=DEV)
+    u, cond, pos, sc = twophase_batch(1, 3, 25, 256, 256, seed=7, obstacle="disc")
+    with torch.no_grad():
+        y = m(u.to(DEV), cond=cond.to(DEV), bc=None, pos=pos.to(DEV), t_cond=None, spatial_cond=sc.to(DEV)).cpu()
+    ref = oracle.build_oracle_model(ocfg, opde, {k: v.cpu() for k, v in m.state_dict().items()})(
+        u, cond=cond, pos=pos, spatial_cond=sc)
+    assert rel_l2(y, ref) < TOL

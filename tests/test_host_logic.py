@@ -1,0 +1,91 @@
+"""Host-side logic of the product package on CPU: reference-identical construction (state_dict keys, shapes
+and seeded init values), crop_Nd offset rule, cfg name resolution, synthetic data, oracle-only helpers."""
+import pytest
+import torch
+from torch import nn
+
+from conftest import load_golden
+
+
+def _pde(p):
+    from pdes import PDE2D
+    return PDE2D(tmin=p["tmin"], tmax=p["tmax"], nt=p["nt"], L1=1.0, L2=1.0, nx1=p["nx1"], nx2=p["nx2"], x=None,
+                 name="twophase", n_cond_static=p["n_cond_static"], n_cond_spatial=p["n_cond_spatial"])
+
+
+@pytest.mark.parametrize("name", ["model_ufno", "model_unet", "model_drn", "model_ufno_fno"])
+def test_construction_matches_reference_bitwise(name):
+    """Same kwargs + torch.manual_seed(42) => identical state_dict to the reference (drop-in checkpoints)."""
+    import models
+    g = load_golden(name)
+    cfg = dict(g["cfg"])
+    cfg.pop("object")
+    cfg["activation"] = nn.GELU()
+    cfg["activation_final"] = nn.Tanh()
+    torch.manual_seed(42)
+    m = models.activation_wrapper(**cfg, pde=_pde(g["pde"]))
+    assert type(m).__name__ == "ActWrapper-EncProcDec"
+    sd, gs = m.state_dict(), g["state_dict"]
+    assert list(sd) == list(gs)
+    for k in sd:
+        assert sd[k].dtype == gs[k].dtype and torch.equal(sd[k], gs[k]), k
+
+
+@pytest.mark.parametrize("cur,des", [(252, 256), (27, 30), (33, 30), (260, 256), (127, 127), (15, 20), (5, 8)])
+def test_crop_offset_rule(cur, des):
+    """ops.crop_offset reproduces crop_Nd's pad placement (common.py:20-34) — checked on real F.pad output."""
+    from nps_hip.ops import crop_offset
+    from oracle.functional import crop_nd
+    x = torch.arange(cur * cur, dtype=torch.float32).reshape(1, 1, cur, cur) + 1
+    y = crop_nd(x, (1, 1, des, des))
+    off = crop_offset(cur, des)
+    # locate element (0,0) of x (or the first surviving one) in y
+    i0 = max(0, -off)
+    pos = (y[0, 0] == x[0, 0, i0, i0]).nonzero()[0].tolist()
+    assert pos == [i0 + off, i0 + off]
+
+
+def test_create_model_name_lookup():
+    from models.enc_proc_dec import create_model
+    from models.enc_proc_dec_components.proc_ufno import UFNO
+    from models.enc_proc_dec_components.enc_grid import ElementWise
+    m = create_model("UFNO", None, dict(num_spatial_dims=2, n_cond=4, hidden_features=16, fno_modes=4,
+                                        hidden_blocks=1, ch_mults=[1, 1], norm=True))
+    assert isinstance(m, UFNO)
+    e = create_model(dict(object="enc_grid.ElementWise"), None,
+                     dict(num_c=3, num_spatial_dims=2, time_window=25, hidden_features=16, n_cond=4,
+                          activation=nn.GELU()))
+    assert isinstance(e, ElementWise) and e.n_in == 3 * 25 + 2 + 4
+
+
+def test_synthetic_batch_shapes_and_range():
+    from trainers.synthetic import twophase_batch
+    u, cond, pos, sc = twophase_batch(2, 3, 30, 16, 16, obstacle="disc")
+    assert u.shape == (2, 3, 30, 16, 16) and cond.shape == (2, 3) and pos.shape == (2, 16, 16, 2)
+    assert sc.shape == (2, 1, 16, 16) and 0 < sc.sum() < sc.numel()
+    assert u.min() >= 0 and u.max() <= 1.03
+
+
+def test_unet_structure_matches_module_tree():
+    """oracle.unet_structure restates UNetModern.__init__ (proc_unet_modern.py:91-152)."""
+    from oracle.functional import unet_structure
+    from models.enc_proc_dec_components.proc_unet_modern import UNetModern, Downsample, Upsample
+    m = UNetModern(None, num_spatial_dims=2, n_cond=4, hidden_features=8, ch_mults=[2, 2, 1, 2], n_blocks=2,
+                   norm=True, use1x1=True, padding_mode="circular")
+    down, _, up = unet_structure(8, [2, 2, 1, 2], 2, 4)
+    assert len(down) == len(m.down) and len(up) == len(m.up)
+    for d, mod in zip(down, m.down):
+        assert (d[0] == "downsample") == isinstance(mod, Downsample)
+    for d, mod in zip(up, m.up):
+        assert (d[0] == "upsample") == isinstance(mod, Upsample)
+
+
+def test_simulate_window_indices():
+    """DataCreator windows + simulate loop bounds (autoregressivepushforwardtrainer.py:354-358)."""
+    from trainers.autoregressivepushforwardtrainer import DataCreator
+    dc = DataCreator(time_window=25, t_resolution=501)
+    u = torch.arange(501.0).reshape(1, 1, 501, 1, 1).repeat(2, 1, 1, 1, 1)
+    d, l = dc.create_data(u, [25, 25])
+    assert d[0, 0, :, 0, 0].tolist() == list(range(0, 25)) and l[0, 0, :, 0, 0].tolist() == list(range(25, 50))
+    steps = list(range(25, 501 - 25 + 1, 25))
+    assert len(steps) == (501 - 2 * 25) // 25 + 1 == 19
