@@ -120,49 +120,67 @@ __global__ __launch_bounds__(WAVES * 64) void conv2d_fwd_kernel(const nps_conv2d
     __syncthreads();
     const int cpg = a.gn_stats ? a.Cin / a.gn_groups : 1;
 
+    // Patch element idx of chunk ch = 4 channels of one patch pixel.  Loading is split from the
+    // prologue transform so the global loads of chunk ch+1 stay in flight under chunk ch's MFMAs.
+    auto elem_valid = [&](int ch, int idx, int& yv, int& xv, int& c) -> bool {
+        const int p = idx >> 2, gq = idx & 3;
+        const int pr = p / g.PW, pc = p - pr * g.PW;
+        const int ye = ybase + pr * g.rstep, xe = xbase + pc * g.rstep;
+        c = ch * CK + gq * 4;
+        if (!(ye >= 0 && ye < Hext && xe >= 0 && xe < Wext && c < a.Cin)) return false;
+        yv = a.circ ? nps::wrap_mod(ye - a.circ, a.Hin) : ye;
+        xv = a.circ ? nps::wrap_mod(xe - a.circ, a.Win) : xe;
+        return true;
+    };
+    auto load_raw = [&](int ch, int idx) -> f32x4 {
+        int yv, xv, c;
+        if (!elem_valid(ch, idx, yv, xv, c)) return f32x4{0.f, 0.f, 0.f, 0.f};
+        return fetch4(a, b, yv, xv, c);
+    };
+    auto transform = [&](int ch, int idx, f32x4 v) -> f32x4 {
+        if (a.gn_stats == nullptr && !a.pre_act) return v;
+        int yv, xv, c;
+        if (!elem_valid(ch, idx, yv, xv, c)) return v;  // conv zero padding stays 0
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            if (c + e < a.Cin) {
+                float t = v[e];
+                if (a.gn_stats != nullptr) {
+                    const float2 mr = gn_tab[(c + e) / cpg];
+                    t = (t - mr.x) * mr.y * a.gn_gamma[c + e] + a.gn_beta[c + e];
+                }
+                if (a.pre_act == 1) t = nps::gelu_erf(t);
+                v[e] = t;
+            }
+        }
+        return v;
+    };
+    // register-prefetch staging (patch fits MAXL float4 per thread) or direct staging
+    const bool prefetch = NG <= MAXL * NT;
     f32x4 pre[MAXL];
     auto load_patch = [&](int ch) {
 #pragma unroll
         for (int k = 0; k < MAXL; ++k) {
             const int idx = tid + k * NT;
-            f32x4 v = {0.f, 0.f, 0.f, 0.f};
-            if (idx < NG) {
-                const int p = idx >> 2, gq = idx & 3;
-                const int pr = p / g.PW, pc = p - pr * g.PW;
-                const int ye = ybase + pr * g.rstep, xe = xbase + pc * g.rstep;
-                const int c = ch * CK + gq * 4;
-                if (ye >= 0 && ye < Hext && xe >= 0 && xe < Wext && c < a.Cin) {
-                    const int yv = a.circ ? nps::wrap_mod(ye - a.circ, a.Hin) : ye;
-                    const int xv = a.circ ? nps::wrap_mod(xe - a.circ, a.Win) : xe;
-                    v = fetch4(a, b, yv, xv, c);
-                    if (a.gn_stats != nullptr || a.pre_act) {
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) {
-                            if (c + e < a.Cin) {
-                                float t = v[e];
-                                if (a.gn_stats != nullptr) {
-                                    const float2 mr = gn_tab[(c + e) / cpg];
-                                    t = (t - mr.x) * mr.y * a.gn_gamma[c + e] + a.gn_beta[c + e];
-                                }
-                                if (a.pre_act == 1) t = nps::gelu_erf(t);
-                                v[e] = t;
-                            }
-                        }
-                    }
-                }
-            }
-            pre[k] = v;
+            pre[k] = (idx < NG) ? load_raw(ch, idx) : f32x4{0.f, 0.f, 0.f, 0.f};
         }
     };
-    auto store_patch = [&](int buf) {
+    auto store_patch = [&](int ch, int buf) {
         float* dst = pbuf + buf * bufsz;
 #pragma unroll
         for (int k = 0; k < MAXL; ++k) {
             const int idx = tid + k * NT;
             if (idx < NG) {
                 const int p = idx >> 2, gq = idx & 3;
-                *reinterpret_cast<f32x4*>(dst + p * PIXS + gq * 4) = pre[k];
+                *reinterpret_cast<f32x4*>(dst + p * PIXS + gq * 4) = transform(ch, idx, pre[k]);
             }
+        }
+    };
+    auto stage_direct = [&](int ch, int buf) {
+        float* dst = pbuf + buf * bufsz;
+        for (int idx = tid; idx < NG; idx += NT) {
+            const int p = idx >> 2, gq = idx & 3;
+            *reinterpret_cast<f32x4*>(dst + p * PIXS + gq * 4) = transform(ch, idx, load_raw(ch, idx));
         }
     };
 
@@ -194,13 +212,17 @@ __global__ __launch_bounds__(WAVES * 64) void conv2d_fwd_kernel(const nps_conv2d
 
     f32x4 a_cur[2][2], a_nxt[2][2];
     load_A(a_cur, 0, 0);
-    load_patch(0);
-    store_patch(0);
+    if (prefetch) {
+        load_patch(0);
+        store_patch(0, 0);
+    } else {
+        stage_direct(0, 0);
+    }
     __syncthreads();
 
     for (int ch = 0; ch < nchunks; ++ch) {
         const bool more = ch + 1 < nchunks;
-        if (more) load_patch(ch + 1);
+        if (more && prefetch) load_patch(ch + 1);
         const float* buf = pbuf + (ch & 1) * bufsz;
         for (int tap = 0; tap < ntaps; ++tap) {
             int nch = ch, ntap = tap + 1;
@@ -226,7 +248,12 @@ __global__ __launch_bounds__(WAVES * 64) void conv2d_fwd_kernel(const nps_conv2d
 #pragma unroll
                 for (int q = 0; q < 2; ++q) a_cur[cb][q] = a_nxt[cb][q];
         }
-        if (more) store_patch((ch + 1) & 1);
+        if (more) {
+            if (prefetch)
+                store_patch(ch + 1, (ch + 1) & 1);
+            else
+                stage_direct(ch + 1, (ch + 1) & 1);
+        }
         __syncthreads();
     }
 
@@ -349,7 +376,6 @@ extern "C" int nps_conv2d_plan(nps_conv2d_t* a) {
         if (t.stride > 1 && t.TH * t.TW > 128) continue;  // stride-2 patches grow 4x
         if (lds_bytes(t) > 160 * 1024) continue;
         const Geo g = make_geo(t);
-        if (g.PH * g.PW * (CK / 4) > MAXL * 64 * t.waves) continue;
         const long waves = (long)g.tiles_x * g.tiles_y * a->B * units_co * t.waves;
         if (waves > best_waves) {
             best_waves = waves;
@@ -384,7 +410,6 @@ extern "C" int nps_conv2d_fwd(const nps_conv2d_t* ap, void* stream) {
     NPS_CHECK_ARG(a.waves == 1 || a.waves == 2 || a.waves == 4, "conv2d_fwd: call nps_conv2d_plan first");
     NPS_CHECK_ARG(a.TH * a.TW == 64 * a.waves, "conv2d_fwd: tile %dx%d != 64*waves", a.TH, a.TW);
     const Geo g = make_geo(a);
-    NPS_CHECK_ARG(g.PH * g.PW * (CK / 4) <= MAXL * 64 * a.waves, "conv2d_fwd: patch too large for tile");
     const int lds = lds_bytes(a);
     NPS_CHECK_ARG(lds <= 160 * 1024, "conv2d_fwd: LDS %d B too large", lds);
     dim3 grid((unsigned)(g.tiles_x * g.tiles_y), (unsigned)((a.Cout + 63) / 64), (unsigned)a.B);
