@@ -98,6 +98,12 @@ int nps_conv2d_pack_weights(const float* w, float* wpack, int Cout, int Cin, int
 int nps_conv2d_plan(nps_conv2d_t* a);
 int nps_conv2d_fwd(const nps_conv2d_t* a, void* stream);
 
+/* Materialise a virtual frame: out[B][Hin][Win][Cin] = act(GN(frame)) using the prologue fields
+ * of `a` (or the plain concat/crop when there is none).  One HBM pass that evaluates the
+ * GroupNorm affine + GELU once per element (proc_unet_modern.py:245-247) ahead of a conv that
+ * then stages raw bytes only. */
+int nps_frame_pack(const nps_conv2d_t* a, float* out, void* stream);
+
 /* GroupNorm statistics over a virtual frame (same source semantics as the conv):
  * stats[B][G][2] += (sum, sumsq) in fp64.  Replaces the moments of
  * nn.GroupNorm (proc_unet_modern.py:235-236, :155).  stats must be zeroed

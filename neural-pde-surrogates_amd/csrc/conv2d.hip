@@ -88,6 +88,69 @@ __device__ __forceinline__ f32x4 fetch4(const nps_conv2d_t& a, int b, int y, int
     return v;
 }
 
+// Epilogue of one 32x32 accumulator tile for this lane's output pixel (dy, dx): the lane holds
+// co = co_base + 8m + 4h + e (m, e < 4).  NHWC outputs with 4-aligned channels take a
+// vectorised path: all loads of the tile (bias, addends, accumulate source) are issued before
+// any store, then 16-B stores.  Order of the float ops matches the reference:
+// act(acc + bias + addends) or act(acc + bias) + addends, then + out when accumulating.
+__device__ __forceinline__ void store_tile(const nps_conv2d_t& a, int b, int co_base, int h, const f32x16& acc,
+                                           int dy, int dx) {
+    if (!a.out_nchw && (a.out_C & 3) == 0 && (a.Cout & 3) == 0) {
+        const size_t base = (((size_t)b * a.out_H + dy) * a.out_W + dx) * a.out_C;
+        f32x4 bi[4], a0[4], a1[4], o[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const int co0 = co_base + 8 * m + 4 * h;
+            const bool ok = co0 < a.Cout;
+            const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+            bi[m] = (ok && a.bias) ? *reinterpret_cast<const f32x4*>(a.bias + co0) : z;
+            a0[m] = (ok && a.addend0) ? *reinterpret_cast<const f32x4*>(a.addend0 + base + co0) : z;
+            a1[m] = (ok && a.addend1) ? *reinterpret_cast<const f32x4*>(a.addend1 + base + co0) : z;
+            o[m] = (ok && a.accumulate) ? *reinterpret_cast<const f32x4*>(a.out + base + co0) : z;
+        }
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const int co0 = co_base + 8 * m + 4 * h;
+            if (co0 >= a.Cout) continue;
+            f32x4 r;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float v = acc[4 * m + e] + bi[m][e];
+                if (!a.add_after_act) v = v + a0[m][e] + a1[m][e];
+                if (a.act == 1) v = nps::gelu_erf(v);
+                if (a.add_after_act) v = v + a0[m][e] + a1[m][e];
+                if (a.accumulate) v += o[m][e];
+                r[e] = v;
+            }
+            *reinterpret_cast<f32x4*>(a.out + base + co0) = r;
+        }
+        return;
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int co = co_base + 8 * m + 4 * h + e;
+            if (co >= a.Cout) continue;
+            const size_t di = a.out_nchw ? (((size_t)b * a.out_C + co) * a.out_H + dy) * a.out_W + dx
+                                         : (((size_t)b * a.out_H + dy) * a.out_W + dx) * a.out_C + co;
+            float v = acc[4 * m + e];
+            if (a.bias) v += a.bias[co];
+            if (!a.add_after_act) {
+                if (a.addend0) v += a.addend0[di];
+                if (a.addend1) v += a.addend1[di];
+            }
+            if (a.act == 1) v = nps::gelu_erf(v);
+            if (a.add_after_act) {
+                if (a.addend0) v += a.addend0[di];
+                if (a.addend1) v += a.addend1[di];
+            }
+            if (a.accumulate) v += a.out[di];
+            a.out[di] = v;
+        }
+    }
+}
+
 template <int WAVES>
 __global__ __launch_bounds__(WAVES * 64) void conv2d_fwd_kernel(const nps_conv2d_t a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -268,32 +331,224 @@ __global__ __launch_bounds__(WAVES * 64) void conv2d_fwd_kernel(const nps_conv2d
         const int dy = oy * a.out_os + a.out_off_y, dx = ox * a.out_os + a.out_off_x;
         if (dy < 0 || dy >= a.out_H || dx < 0 || dx >= a.out_W) continue;
 #pragma unroll
-        for (int cb = 0; cb < 2; ++cb) {
+        for (int cb = 0; cb < 2; ++cb) store_tile(a, b, cob * 64 + cb * 32, h, acc[cb][pb], dy, dx);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Producer/consumer variant for stride-1, undilated convs with 1, 4 or 9 taps (every U-Net conv,
+// the transposed-conv phases, all 1x1s).  512 threads: waves 0-3 are MFMA consumers that only
+// read LDS (no global loads, no VALU beyond address math), waves 4-7 are producers that stage
+// the next K-stage (weights + input patch with the crop/concat/wrap/GN/GELU prologue) while the
+// consumers run the current one.  Producers hold stage s+2's global loads in registers across
+// the barrier (raw s_barrier, only lgkmcnt drained) so their HBM/L2 latency overlaps two stages.
+template <int NTAPS, int CKB, int PB>
+__global__ __launch_bounds__(512) void conv2d_pc_kernel(const nps_conv2d_t a) {
+    constexpr int KWT = NTAPS == 9 ? 3 : (NTAPS == 4 ? 2 : 1);
+    constexpr int SUB = CKB / CK;                       // 16-channel sub-chunks per stage
+    constexpr int PIXSB = CKB + 4;                      // LDS floats per patch pixel
+    constexpr int AFL = SUB * NTAPS * 4 * 64 * 4;       // floats of the A (weight) tile per stage
+    constexpr int NAP = SUB * NTAPS;                    // A float4 per producer thread per stage
+    constexpr int MAXP = 9;                             // max patch float4 per producer thread
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const bool producer = wave >= 4;
+    const int b = blockIdx.z, cob = blockIdx.y;
+    const Geo g = make_geo(a);
+    const int ty = blockIdx.x / g.tiles_x, tx = blockIdx.x % g.tiles_x;
+    const int oy0 = ty * a.TH, ox0 = tx * a.TW;
+    const int ybase = oy0 - a.pad_y, xbase = ox0 - a.pad_x;
+    const int Hext = a.Hin + 2 * a.circ, Wext = a.Win + 2 * a.circ;
+    const int npix = g.PH * g.PW;
+    const int NG = npix * (CKB / 4);
+    const int patch_fl = (npix * PIXSB + 3) & ~3;
+    const int stage_fl = AFL + patch_fl;
+    float2* gn_tab = reinterpret_cast<float2*>(smem);
+    float* ring = smem + 32;
+    const int n16 = (a.Cin + CK - 1) / CK;              // 16-channel chunks of the packed weight
+    const int nstages = (n16 + SUB - 1) / SUB;
+    const int ncb = 2 * ((a.Cout + 63) / 64);
+
+    if (a.gn_stats != nullptr && tid < a.gn_groups) {
+        const double cnt = (double)(a.Cin / a.gn_groups) * a.Hin * a.Win;
+        const double s1 = a.gn_stats[(b * a.gn_groups + tid) * 2], s2 = a.gn_stats[(b * a.gn_groups + tid) * 2 + 1];
+        const double mean = s1 / cnt;
+        double var = s2 / cnt - mean * mean;
+        var = var < 0.0 ? 0.0 : var;
+        gn_tab[tid] = make_float2((float)mean, (float)(1.0 / sqrt(var + (double)a.gn_eps)));
+    }
+    __syncthreads();
+    const int cpg = a.gn_stats ? a.Cin / a.gn_groups : 1;
+
+    if (producer) {
+        // ------------------------------------------------------------------ producers
+        // Pure data movement (the GroupNorm/GELU prologue is materialised by nps_frame_pack when
+        // this kernel is used): on gfx950 f32 MFMA and VALU share the FP32 datapath, so every
+        // producer VALU instruction is MFMA time lost.  Slot geometry is computed once.
+        const int ptid = tid - 256;
+        const f32x4* wp = reinterpret_cast<const f32x4*>(a.wpack);
+        f32x4 ra[NAP], rp[MAXP];
+        int sy[MAXP], sx[MAXP];  // virtual-frame pixel of each slot (after circular wrap); sy = -1: zero pad
 #pragma unroll
-            for (int m = 0; m < 4; ++m) {
-                const int co0 = cob * 64 + cb * 32 + 8 * m + 4 * h;
+        for (int k = 0; k < MAXP; ++k) {
+            const int idx = ptid + k * 256;
+            const int p = idx / (CKB / 4);
+            const int pr = p / g.PW, pc = p - pr * g.PW;
+            const int ye = ybase + pr, xe = xbase + pc;
+            const bool ok = idx < NG && ye >= 0 && ye < Hext && xe >= 0 && xe < Wext;
+            sy[k] = ok ? (a.circ ? nps::wrap_mod(ye - a.circ, a.Hin) : ye) : -1;
+            sx[k] = ok ? (a.circ ? nps::wrap_mod(xe - a.circ, a.Win) : xe) : 0;
+        }
+        auto issue = [&](int st) {  // global loads of stage st into registers
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int co = co0 + e;
-                    if (co >= a.Cout) continue;
-                    const size_t di = a.out_nchw ? (((size_t)b * a.out_C + co) * a.out_H + dy) * a.out_W + dx
-                                                 : (((size_t)b * a.out_H + dy) * a.out_W + dx) * a.out_C + co;
-                    float v = acc[cb][pb][4 * m + e];
-                    if (a.bias) v += a.bias[co];
-                    if (!a.add_after_act) {
-                        if (a.addend0) v += a.addend0[di];
-                        if (a.addend1) v += a.addend1[di];
+            for (int k = 0; k < NAP; ++k) {
+                const int sub = k / NTAPS, tap = k - sub * NTAPS;
+                const int ch16 = st * SUB + sub;
+                f32x4 v = {0.f, 0.f, 0.f, 0.f};
+                if (ch16 < n16) v = wp[(((size_t)ch16 * NTAPS + tap) * ncb + 2 * cob) * 2 * 64 + ptid];
+                ra[k] = v;
+            }
+            // source holding this stage's channels (uniform); fast path when one 4-aligned source covers it
+            const int c0 = st * CKB;
+            const int cend = min(c0 + CKB, a.Cin);
+            int sidx = -1, cbase = 0;
+            {
+                int lo = 0;
+                for (int si = 0; si < a.nsrc; ++si) {
+                    const int hi = lo + a.src[si].C;
+                    if (c0 >= lo && cend <= hi && (a.src[si].C & 3) == 0 && ((c0 - lo) & 3) == 0) {
+                        sidx = si;
+                        cbase = lo;
                     }
-                    if (a.act == 1) v = nps::gelu_erf(v);
-                    if (a.add_after_act) {
-                        if (a.addend0) v += a.addend0[di];
-                        if (a.addend1) v += a.addend1[di];
-                    }
-                    if (a.accumulate) v += a.out[di];
-                    a.out[di] = v;
+                    lo = hi;
                 }
             }
+            if (sidx >= 0) {
+                const nps_src_t S = a.src[sidx];
+                const int cs = c0 - cbase;
+#pragma unroll
+                for (int k = 0; k < MAXP; ++k) {
+                    const int idx = ptid + k * 256;
+                    const int gq = idx % (CKB / 4);
+                    const int yy = sy[k] - S.off_y, xx = sx[k] - S.off_x;
+                    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+                    if (sy[k] >= 0 && yy >= 0 && yy < S.H && xx >= 0 && xx < S.W && c0 + gq * 4 < cend)
+                        v = *reinterpret_cast<const f32x4*>(S.ptr + ((size_t)(b * S.H + yy) * S.W + xx) * S.C + cs +
+                                                            gq * 4);
+                    rp[k] = v;
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < MAXP; ++k) {
+                    const int idx = ptid + k * 256;
+                    const int gq = idx % (CKB / 4);
+                    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+                    if (sy[k] >= 0 && c0 + gq * 4 < a.Cin) v = fetch4(a, b, sy[k], sx[k], c0 + gq * 4);
+                    rp[k] = v;
+                }
+            }
+        };
+        auto commit = [&](int buf) {  // LDS store of the staged stage
+            float* A = ring + buf * stage_fl;
+            float* Pt = A + AFL;
+#pragma unroll
+            for (int k = 0; k < NAP; ++k) *reinterpret_cast<f32x4*>(A + (k * 256 + ptid) * 4) = ra[k];
+#pragma unroll
+            for (int k = 0; k < MAXP; ++k) {
+                const int idx = ptid + k * 256;
+                if (idx < NG) {
+                    const int p = idx / (CKB / 4), gq = idx - p * (CKB / 4);
+                    *reinterpret_cast<f32x4*>(Pt + p * PIXSB + gq * 4) = rp[k];
+                }
+            }
+        };
+#ifndef NPS_ABLATE_PRODUCER
+        issue(0);
+        commit(0);
+        if (nstages > 1) issue(1);
+#endif
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        for (int st = 0; st < nstages; ++st) {
+#ifdef NPS_ABLATE_PRODUCER
+            if (false) {
+#else
+            if (st + 1 < nstages) {
+#endif
+                commit((st + 1) & 1);
+                if (st + 2 < nstages) issue(st + 2);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         }
+        return;
+    }
+
+    // ---------------------------------------------------------------------- consumers
+    int boff[PB];
+#pragma unroll
+    for (int pb = 0; pb < PB; ++pb) {
+        const int P = wave * 32 * PB + pb * 32 + (lane & 31);
+        const int ti = P / a.TW, tj = P - (P / a.TW) * a.TW;
+        boff[pb] = (ti * g.PW + tj) * PIXSB + (lane >> 5) * 8;
+    }
+    f32x16 acc[2][PB];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < PB; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    // Operands of K-group gi = (sub, tap, q) are read one group ahead into a second register set,
+    // so every group's 8*PB MFMAs (>= 512 cycles) cover the LDS latency of the next group's reads.
+    constexpr int G = SUB * NTAPS * 2;
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    for (int st = 0; st < nstages; ++st) {
+        const float* A = ring + (st & 1) * stage_fl;
+        const float* Pt = A + AFL;
+        f32x4 av[2][2], bv[2][PB];
+        auto load_group = [&](int gi, f32x4 (&ad)[2], f32x4 (&bd)[PB]) {
+            const int q = gi & 1, tq = gi >> 1;
+            const int sub = tq / NTAPS, tap = tq - sub * NTAPS;
+            const int ky = tap / KWT, kx = tap % KWT;
+            const int toff = (ky * g.PW + kx) * PIXSB + sub * CK;
+#pragma unroll
+            for (int cb = 0; cb < 2; ++cb)
+                ad[cb] = *reinterpret_cast<const f32x4*>(A + (((sub * NTAPS + tap) * 4 + cb * 2 + q) * 64 + lane) * 4);
+#pragma unroll
+            for (int pb = 0; pb < PB; ++pb) bd[pb] = *reinterpret_cast<const f32x4*>(Pt + boff[pb] + toff + q * 4);
+        };
+#ifndef NPS_ABLATE_CONSUMER
+        load_group(0, av[0], bv[0]);
+#pragma unroll
+        for (int gi = 0; gi < G; ++gi) {
+            const int cur = gi & 1;
+            if (gi + 1 < G) load_group(gi + 1, av[cur ^ 1], bv[cur ^ 1]);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+                    for (int pb = 0; pb < PB; ++pb)
+                        acc[cb][pb] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[cur][cb][e], bv[cur][pb][e], acc[cb][pb], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#endif
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+
+    // epilogue
+    const int h = lane >> 5;
+#pragma unroll
+    for (int pb = 0; pb < PB; ++pb) {
+        const int P = wave * 32 * PB + pb * 32 + (lane & 31);
+        const int ti = P / a.TW, tj = P - (P / a.TW) * a.TW;
+        const int oy = oy0 + ti, ox = ox0 + tj;
+        if (oy >= a.Hout || ox >= a.Wout) continue;
+        const int dy = oy * a.out_os + a.out_off_y, dx = ox * a.out_os + a.out_off_x;
+        if (dy < 0 || dy >= a.out_H || dx < 0 || dx >= a.out_W) continue;
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) store_tile(a, b, cob * 64 + cb * 32, h, acc[cb][pb], dy, dx);
     }
 }
 
@@ -335,7 +590,24 @@ size_t packed_size(int Cout, int Cin, int ntaps) {
     return nchunks * ntaps * ncb * 2 * 64 * 4;
 }
 
+bool pc_eligible(const nps_conv2d_t& a) {
+    const int nt = a.KH * a.KW;
+    // the producer/consumer kernel does no prologue (callers materialise it with nps_frame_pack)
+    return a.stride == 1 && a.dil == 1 && a.KH == a.KW && (nt == 1 || nt == 4 || nt == 9) && a.gn_stats == nullptr &&
+           a.pre_act == 0;
+}
+
+int pc_lds_bytes(const nps_conv2d_t& a) {
+    const Geo g = make_geo(a);
+    const int nt = a.KH * a.KW;
+    const int ckb = nt == 1 ? 32 : 16;
+    const int afl = (ckb / CK) * nt * 4 * 64 * 4;
+    const int patch = (g.PH * g.PW * (ckb + 4) + 3) & ~3;
+    return (32 + 2 * (afl + patch)) * 4;
+}
+
 int lds_bytes(const nps_conv2d_t& a) {
+    if (a.waves == 8) return pc_lds_bytes(a);
     const Geo g = make_geo(a);
     const int bufsz = ((g.PH * g.PW * PIXS + 3) & ~3);
     return (32 + 2 * bufsz) * 4;
@@ -363,6 +635,37 @@ extern "C" int nps_conv2d_plan(nps_conv2d_t* a) {
     // dilated stride-1 convs tile on the dilation lattice (patch independent of d)
     a->lattice = (a->dil > 1 && a->stride == 1) ? 1 : 0;
     const long units_co = (a->Cout + 63) / 64;
+    if (pc_eligible(*a)) {
+        // producer/consumer kernel: 256-pixel tiles (16x16 or 8x32), 128-pixel (8x16) when the grid is small
+        const int cand[3][2] = {{16, 16}, {8, 32}, {8, 16}};
+        int best = -1;
+        long best_px = -1;
+        for (int i = 0; i < 3; ++i) {
+            nps_conv2d_t t = *a;
+            t.waves = 8;
+            t.TH = cand[i][0];
+            t.TW = cand[i][1];
+            if (pc_lds_bytes(t) > 160 * 1024) continue;
+            const Geo g = make_geo(t);
+            const int nt = t.KH * t.KW, ckb = nt == 1 ? 32 : 16;
+            if (g.PH * g.PW * (ckb / 4) > 9 * 256) continue;
+            const long wgs = (long)g.tiles_x * g.tiles_y * a->B * units_co;
+            // score: work-groups that fill the 256 CUs, penalising halo/edge waste
+            const long useful = (long)a->Hout * a->Wout * a->B * units_co;
+            const long covered = wgs * t.TH * t.TW;
+            const long px = (wgs >= 512 ? 2 * 512 : 2 * wgs) * 1000 + (1000 * useful) / covered;
+            if (px > best_px) {
+                best_px = px;
+                best = i;
+            }
+        }
+        if (best >= 0) {
+            a->waves = 8;
+            a->TH = cand[best][0];
+            a->TW = cand[best][1];
+            return pc_lds_bytes(*a);
+        }
+    }
     // candidate tiles (waves, TH, TW), largest first: take the first one whose grid
     // puts >= 8 waves on each of the 256 CUs, else the one with the most waves.
     const int cand[5][3] = {{4, 16, 16}, {4, 8, 32}, {2, 8, 16}, {1, 8, 8}, {1, 4, 16}};
@@ -391,6 +694,33 @@ extern "C" int nps_conv2d_plan(nps_conv2d_t* a) {
     return lds_bytes(*a);
 }
 
+namespace {
+template <int NT, int CKB, int PB>
+void launch_pc_one(const nps_conv2d_t& a, dim3 grid, int lds, hipStream_t s) {
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)conv2d_pc_kernel<NT, CKB, PB>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr_set = true;
+    }
+    conv2d_pc_kernel<NT, CKB, PB><<<grid, 512, lds, s>>>(a);
+}
+
+int launch_pc(const nps_conv2d_t& a, dim3 grid, int lds, hipStream_t s) {
+    const int nt = a.KH * a.KW;
+    const bool pb2 = a.TH * a.TW == 256;
+    if (nt == 9) {
+        if (pb2) launch_pc_one<9, 16, 2>(a, grid, lds, s); else launch_pc_one<9, 16, 1>(a, grid, lds, s);
+    } else if (nt == 4) {
+        if (pb2) launch_pc_one<4, 16, 2>(a, grid, lds, s); else launch_pc_one<4, 16, 1>(a, grid, lds, s);
+    } else {
+        if (pb2) launch_pc_one<1, 32, 2>(a, grid, lds, s); else launch_pc_one<1, 32, 1>(a, grid, lds, s);
+    }
+    NPS_CHECK_LAUNCH("conv2d_fwd (producer/consumer)");
+    return 0;
+}
+}  // namespace
+
 extern "C" int nps_conv2d_fwd(const nps_conv2d_t* ap, void* stream) {
     NPS_CHECK_ARG(ap != nullptr, "conv2d_fwd: null args");
     const nps_conv2d_t& a = *ap;
@@ -407,13 +737,16 @@ extern "C" int nps_conv2d_fwd(const nps_conv2d_t* ap, void* stream) {
                                   a.gn_beta),
                   "conv2d_fwd: bad GroupNorm prologue");
     NPS_CHECK_ARG(a.circ == 0 || (a.Hin > 0 && a.Win > 0), "conv2d_fwd: circular padding of empty frame");
-    NPS_CHECK_ARG(a.waves == 1 || a.waves == 2 || a.waves == 4, "conv2d_fwd: call nps_conv2d_plan first");
-    NPS_CHECK_ARG(a.TH * a.TW == 64 * a.waves, "conv2d_fwd: tile %dx%d != 64*waves", a.TH, a.TW);
+    NPS_CHECK_ARG(a.waves == 1 || a.waves == 2 || a.waves == 4 || a.waves == 8, "conv2d_fwd: call nps_conv2d_plan first");
+    NPS_CHECK_ARG(a.waves == 8 ? (a.TH * a.TW == 256 || a.TH * a.TW == 128) && pc_eligible(a)
+                               : a.TH * a.TW == 64 * a.waves,
+                  "conv2d_fwd: tile %dx%d does not match waves=%d", a.TH, a.TW, a.waves);
     const Geo g = make_geo(a);
     const int lds = lds_bytes(a);
     NPS_CHECK_ARG(lds <= 160 * 1024, "conv2d_fwd: LDS %d B too large", lds);
     dim3 grid((unsigned)(g.tiles_x * g.tiles_y), (unsigned)((a.Cout + 63) / 64), (unsigned)a.B);
     hipStream_t s = (hipStream_t)stream;
+    if (a.waves == 8) return launch_pc(a, grid, lds, s);
     static bool attr_set = false;  // allow > 64 KiB dynamic LDS (gfx950 has 160 KiB per CU)
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void*)conv2d_fwd_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -497,5 +830,73 @@ extern "C" int nps_group_norm_stats(const nps_src_t* src, int nsrc, int B, int H
     nblk = nblk < 1 ? 1 : (nblk > 512 ? 512 : nblk);
     gn_stats_kernel<<<dim3(nblk, G, B), 256, 0, s>>>(a, G, stats);
     NPS_CHECK_LAUNCH("group_norm_stats");
+    return 0;
+}
+
+// ------------------------------------------------------------------ frame materialisation
+namespace {
+// out[B][Hin][Win][Cin] = act(GN(frame)) of the virtual frame (or the plain concat/crop when no
+// prologue): one pass, 16-B loads/stores, GELU evaluated once per element instead of once per
+// consuming conv tile.
+__global__ void frame_pack_kernel(nps_conv2d_t a, float* __restrict__ out) {
+    __shared__ float2 tab[16];
+    const int b = blockIdx.y;
+    if (a.gn_stats != nullptr && threadIdx.x < a.gn_groups) {
+        const double cnt = (double)(a.Cin / a.gn_groups) * a.Hin * a.Win;
+        const double s1 = a.gn_stats[(b * a.gn_groups + threadIdx.x) * 2];
+        const double s2 = a.gn_stats[(b * a.gn_groups + threadIdx.x) * 2 + 1];
+        const double mean = s1 / cnt;
+        double var = s2 / cnt - mean * mean;
+        var = var < 0.0 ? 0.0 : var;
+        tab[threadIdx.x] = make_float2((float)mean, (float)(1.0 / sqrt(var + (double)a.gn_eps)));
+    }
+    __syncthreads();
+    const int cpg = a.gn_stats ? a.Cin / a.gn_groups : 1;
+    const int C4 = (a.Cin + 3) / 4;
+    const long n = (long)a.Hin * a.Win * C4;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+        const long pix = i / C4;
+        const int c = (int)(i - pix * C4) * 4;
+        const int y = (int)(pix / a.Win), x = (int)(pix % a.Win);
+        f32x4 v = fetch4(a, b, y, x, c);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            if (c + e < a.Cin) {
+                float t = v[e];
+                if (a.gn_stats != nullptr) {
+                    const float2 mr = tab[(c + e) / cpg];
+                    t = (t - mr.x) * mr.y * a.gn_gamma[c + e] + a.gn_beta[c + e];
+                }
+                if (a.pre_act == 1) t = nps::gelu_erf(t);
+                v[e] = t;
+            }
+        }
+        float* dst = out + ((size_t)(b * a.Hin + y) * a.Win + x) * a.Cin + c;
+        if ((a.Cin & 3) == 0) {
+            *reinterpret_cast<f32x4*>(dst) = v;
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (c + e < a.Cin) dst[e] = v[e];
+        }
+    }
+}
+}  // namespace
+
+extern "C" int nps_frame_pack(const nps_conv2d_t* ap, float* out, void* stream) {
+    NPS_CHECK_ARG(ap && out, "frame_pack: null");
+    const nps_conv2d_t& a = *ap;
+    NPS_CHECK_ARG(a.nsrc >= 1 && a.nsrc <= NPS_MAX_SRC && a.B > 0 && a.Hin > 0 && a.Win > 0 && a.Cin > 0,
+                  "frame_pack: bad frame");
+    int csum = 0;
+    for (int i = 0; i < a.nsrc; ++i) csum += a.src[i].C;
+    NPS_CHECK_ARG(csum == a.Cin, "frame_pack: Cin mismatch");
+    NPS_CHECK_ARG(!a.gn_stats || (a.gn_groups > 0 && a.gn_groups <= 16 && a.Cin % a.gn_groups == 0),
+                  "frame_pack: bad GroupNorm");
+    const long n = (long)a.Hin * a.Win * ((a.Cin + 3) / 4);
+    int nb = (int)((n + 255) / 256);
+    nb = nb > 2048 ? 2048 : nb;
+    frame_pack_kernel<<<dim3(nb, a.B), 256, 0, (hipStream_t)stream>>>(a, out);
+    NPS_CHECK_LAUNCH("frame_pack");
     return 0;
 }

@@ -112,6 +112,10 @@ def conv2d(srcs: Sequence[Src], frame_hw, wpack: torch.Tensor, bias: Optional[to
     B = t0.shape[0]
     Hin, Win = int(frame_hw[0]), int(frame_hw[1])
     Cin = sum(s.t.shape[3] for s in srcs)
+    if (gn is not None or pre_act) and stride == 1 and dil == 1 and KH == KW and KH in (1, 2, 3):
+        # the stride-1 producer/consumer conv stages raw bytes only: materialise act(GN(frame)) once
+        srcs = [Src(frame_pack(srcs, (Hin, Win), gn, pre_act))]
+        gn, pre_act = None, 0
     pb = pad if pad_bottom is None else pad_bottom
     if out_hw is None:
         Hout = (Hin + 2 * circ + pad[0] + pb[0] - dil * (KH - 1) - 1) // stride + 1
@@ -157,6 +161,25 @@ def conv2d(srcs: Sequence[Src], frame_hw, wpack: torch.Tensor, bias: Optional[to
         conv_probe.append((e0, e1, 2.0 * B * Hout * Wout * Cout * Cin * KH * KW))
     else:
         check(lib.nps_conv2d_fwd(ctypes_byref(a), stream_ptr()), "conv2d_fwd")
+    return out
+
+
+def frame_pack(srcs: Sequence[Src], frame_hw, gn: Optional[GN] = None, pre_act=0) -> torch.Tensor:
+    """(B, Hin, Win, Cin) = act(GN(virtual frame)) — nps_frame_pack."""
+    t0 = srcs[0].t
+    B = t0.shape[0]
+    Hin, Win = int(frame_hw[0]), int(frame_hw[1])
+    Cin = sum(s.t.shape[3] for s in srcs)
+    a = Conv2dArgs()
+    a.nsrc = len(srcs)
+    a.src = _c_src(srcs)
+    a.B, a.Hin, a.Win, a.Cin = B, Hin, Win, Cin
+    if gn is not None:
+        a.gn_stats, a.gn_gamma, a.gn_beta = ptr(gn.stats), ptr(gn.gamma), ptr(gn.beta)
+        a.gn_groups, a.gn_eps = gn.groups, gn.eps
+    a.pre_act = pre_act
+    out = empty_nhwc(B, Hin, Win, Cin, t0)
+    check(lib.nps_frame_pack(ctypes_byref(a), ptr(out), stream_ptr()), "frame_pack")
     return out
 
 

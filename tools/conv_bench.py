@@ -1,0 +1,70 @@
+"""Micro-benchmark of one fused conv launch shape (dev tool, not part of the product).
+
+python tools/conv_bench.py [--cin 388 --cout 192 --k 3 --hw 260 --b 16 --gn 1 --iters 20]
+Prints algorithmic TFLOP/s of nps_conv2d_fwd measured with HIP events; with --check compares a
+B=1 slice against torch.nn.functional.conv2d on the CPU.
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "neural-pde-surrogates_amd")]
+import torch  # noqa: E402
+
+from nps_hip import ops  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cin", type=int, default=388)
+    ap.add_argument("--cout", type=int, default=192)
+    ap.add_argument("--k", type=int, default=3)
+    ap.add_argument("--dil", type=int, default=1)
+    ap.add_argument("--stride", type=int, default=1)
+    ap.add_argument("--circ", type=int, default=0)
+    ap.add_argument("--hw", type=int, default=260)
+    ap.add_argument("--b", type=int, default=16)
+    ap.add_argument("--gn", type=int, default=1)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--check", action="store_true")
+    a = ap.parse_args()
+    dev = "cuda"
+    torch.manual_seed(0)
+    x = torch.randn(a.b, a.hw, a.hw, a.cin, device=dev)
+    w = torch.randn(a.cout, a.cin, a.k, a.k, device=dev) * (1.0 / (a.cin * a.k * a.k) ** 0.5)
+    bias = torch.randn(a.cout, device=dev)
+    wp = ops.pack_conv_weight(w)
+    gn = None
+    if a.gn:
+        st = ops.group_norm_stats([ops.Src(x)], (a.hw, a.hw), 1)
+        gn = ops.GN(st, torch.rand(a.cin, device=dev) + 0.5, torch.rand(a.cin, device=dev) - 0.5, 1, 1e-5)
+    kw = dict(stride=a.stride, dil=a.dil, circ=a.circ, gn=gn, pre_act=1 if a.gn else 0)
+    out = ops.conv2d([ops.Src(x)], (a.hw, a.hw), wp, bias, a.cout, a.k, a.k, **kw)
+    torch.cuda.synchronize()
+    Ho, Wo = out.shape[1:3]
+    flops = 2.0 * a.b * Ho * Wo * a.cout * a.cin * a.k * a.k
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(a.iters):
+        ops.conv2d([ops.Src(x)], (a.hw, a.hw), wp, bias, a.cout, a.k, a.k, out=out, **kw)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / a.iters
+    print(f"conv cin={a.cin} cout={a.cout} k={a.k} d={a.dil} s={a.stride} hw={a.hw} B={a.b} gn={a.gn}: "
+          f"{ms:.3f} ms  {flops / ms / 1e9:.1f} TFLOP/s  ({flops / ms / 1e9 / 157.3 * 100:.1f}% of fp32 MFMA peak)")
+    if a.check:
+        import torch.nn.functional as F
+        xc = x[:1].permute(0, 3, 1, 2).cpu()
+        if a.gn:
+            xc = F.gelu(F.group_norm(xc, 1, gn.gamma.cpu(), gn.beta.cpu(), 1e-5))
+        if a.circ:
+            xc = F.pad(xc, (a.circ,) * 4, mode="circular")
+        ref = F.conv2d(xc, w.cpu(), bias.cpu(), stride=a.stride, dilation=a.dil)
+        y = out[:1].permute(0, 3, 1, 2).cpu()
+        err = (torch.linalg.vector_norm(y.double() - ref.double()) / torch.linalg.vector_norm(ref.double())).item()
+        print(f"  rel-L2 vs torch CPU: {err:.2e}")
+
+
+if __name__ == "__main__":
+    main()
