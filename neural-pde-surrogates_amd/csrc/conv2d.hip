@@ -47,42 +47,41 @@ __host__ __device__ inline Geo make_geo(const nps_conv2d_t& a) {
 }
 
 // Fetch 4 consecutive virtual channels [c, c+4) at virtual-frame position (y, x) of sample b.
+// Written without loops over a.src[] (explicitly per source) so the kernarg struct is never indexed
+// dynamically — a dynamic index makes the compiler copy the whole struct to scratch.
+__device__ __forceinline__ bool fetch4_fast(const nps_src_t& S, int lo, int b, int y, int x, int c, f32x4& v) {
+    const int hi = lo + S.C;
+    if (c >= lo && c + 4 <= hi && ((c - lo) & 3) == 0 && (S.C & 3) == 0) {
+        const int yy = y - S.off_y, xx = x - S.off_x;
+        if (yy >= 0 && yy < S.H && xx >= 0 && xx < S.W)
+            v = *reinterpret_cast<const f32x4*>(S.ptr + ((size_t)(b * S.H + yy) * S.W + xx) * S.C + (c - lo));
+        return true;
+    }
+    return false;
+}
+
+__device__ __forceinline__ float fetch1(const nps_src_t& S, int lo, int b, int y, int x, int ce) {
+    if (ce >= lo && ce < lo + S.C) {
+        const int yy = y - S.off_y, xx = x - S.off_x;
+        if (yy >= 0 && yy < S.H && xx >= 0 && xx < S.W)
+            return S.ptr[((size_t)(b * S.H + yy) * S.W + xx) * S.C + (ce - lo)];
+    }
+    return 0.f;
+}
+
 __device__ __forceinline__ f32x4 fetch4(const nps_conv2d_t& a, int b, int y, int x, int c) {
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    int c0 = 0;
-#pragma unroll
-    for (int s = 0; s < NPS_MAX_SRC; ++s) {
-        if (s < a.nsrc) {
-            const nps_src_t& S = a.src[s];
-            const int lo = c0, hi = c0 + S.C;
-            // fast path: all 4 channels inside this source and 16-B aligned
-            if (c >= lo && c + 4 <= hi && ((c - lo) & 3) == 0 && (S.C & 3) == 0) {
-                const int yy = y - S.off_y, xx = x - S.off_x;
-                if (yy >= 0 && yy < S.H && xx >= 0 && xx < S.W)
-                    v = *reinterpret_cast<const f32x4*>(S.ptr + ((size_t)(b * S.H + yy) * S.W + xx) * S.C + (c - lo));
-                return v;
-            }
-            c0 = hi;
-        }
-    }
+    const int lo1 = a.src[0].C, lo2 = a.src[0].C + a.src[1].C;
+    if (fetch4_fast(a.src[0], 0, b, y, x, c, v)) return v;
+    if (a.nsrc > 1 && fetch4_fast(a.src[1], lo1, b, y, x, c, v)) return v;
+    if (a.nsrc > 2 && fetch4_fast(a.src[2], lo2, b, y, x, c, v)) return v;
     // general path: per-channel gather (sources with C % 4 != 0, straddling chunks)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
         const int ce = c + e;
-        int base = 0;
-        float r = 0.f;
-#pragma unroll
-        for (int s = 0; s < NPS_MAX_SRC; ++s) {
-            if (s < a.nsrc) {
-                const nps_src_t& S = a.src[s];
-                if (ce >= base && ce < base + S.C) {
-                    const int yy = y - S.off_y, xx = x - S.off_x;
-                    if (yy >= 0 && yy < S.H && xx >= 0 && xx < S.W)
-                        r = S.ptr[((size_t)(b * S.H + yy) * S.W + xx) * S.C + (ce - base)];
-                }
-                base += S.C;
-            }
-        }
+        float r = fetch1(a.src[0], 0, b, y, x, ce);
+        if (a.nsrc > 1 && ce >= lo1) r = fetch1(a.src[1], lo1, b, y, x, ce);
+        if (a.nsrc > 2 && ce >= lo2) r = fetch1(a.src[2], lo2, b, y, x, ce);
         v[e] = r;
     }
     return v;
@@ -349,7 +348,8 @@ __global__ __launch_bounds__(512) void conv2d_pc_kernel(const nps_conv2d_t a) {
     constexpr int PIXSB = CKB + 4;                      // LDS floats per patch pixel
     constexpr int AFL = SUB * NTAPS * 4 * 64 * 4;       // floats of the A (weight) tile per stage
     constexpr int NAP = SUB * NTAPS;                    // A float4 per producer thread per stage
-    constexpr int MAXP = 9;                             // max patch float4 per producer thread
+    // max patch float4 per producer thread: ceil(patch pixels * CKB/4 / 256) for the tile shapes of nps_conv2d_plan
+    constexpr int MAXP = PB == 2 ? (NTAPS == 9 ? 6 : (NTAPS == 4 ? 5 : 8)) : (NTAPS == 1 ? 4 : 3);
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const bool producer = wave >= 4;
@@ -414,27 +414,36 @@ __global__ __launch_bounds__(512) void conv2d_pc_kernel(const nps_conv2d_t a) {
             int sidx = -1, cbase = 0;
             {
                 int lo = 0;
-                for (int si = 0; si < a.nsrc; ++si) {
-                    const int hi = lo + a.src[si].C;
-                    if (c0 >= lo && cend <= hi && (a.src[si].C & 3) == 0 && ((c0 - lo) & 3) == 0) {
-                        sidx = si;
-                        cbase = lo;
+#pragma unroll
+                for (int si = 0; si < NPS_MAX_SRC; ++si) {  // unrolled: static kernarg indexing
+                    if (si < a.nsrc) {
+                        const int hi = lo + a.src[si].C;
+                        if (c0 >= lo && cend <= hi && (a.src[si].C & 3) == 0 && ((c0 - lo) & 3) == 0) {
+                            sidx = si;
+                            cbase = lo;
+                        }
+                        lo = hi;
                     }
-                    lo = hi;
                 }
             }
             if (sidx >= 0) {
-                const nps_src_t S = a.src[sidx];
+                // scalar selects over per-source locals (an indexed kernarg struct would go to scratch)
+                const nps_src_t S0 = a.src[0], S1 = a.src[1], S2 = a.src[2];
+                const float* sptr = sidx == 0 ? S0.ptr : (sidx == 1 ? S1.ptr : S2.ptr);
+                const int sC = sidx == 0 ? S0.C : (sidx == 1 ? S1.C : S2.C);
+                const int sH = sidx == 0 ? S0.H : (sidx == 1 ? S1.H : S2.H);
+                const int sW = sidx == 0 ? S0.W : (sidx == 1 ? S1.W : S2.W);
+                const int soy = sidx == 0 ? S0.off_y : (sidx == 1 ? S1.off_y : S2.off_y);
+                const int sox = sidx == 0 ? S0.off_x : (sidx == 1 ? S1.off_x : S2.off_x);
                 const int cs = c0 - cbase;
 #pragma unroll
                 for (int k = 0; k < MAXP; ++k) {
                     const int idx = ptid + k * 256;
                     const int gq = idx % (CKB / 4);
-                    const int yy = sy[k] - S.off_y, xx = sx[k] - S.off_x;
+                    const int yy = sy[k] - soy, xx = sx[k] - sox;
                     f32x4 v = {0.f, 0.f, 0.f, 0.f};
-                    if (sy[k] >= 0 && yy >= 0 && yy < S.H && xx >= 0 && xx < S.W && c0 + gq * 4 < cend)
-                        v = *reinterpret_cast<const f32x4*>(S.ptr + ((size_t)(b * S.H + yy) * S.W + xx) * S.C + cs +
-                                                            gq * 4);
+                    if (sy[k] >= 0 && yy >= 0 && yy < sH && xx >= 0 && xx < sW && c0 + gq * 4 < cend)
+                        v = *reinterpret_cast<const f32x4*>(sptr + ((size_t)(b * sH + yy) * sW + xx) * sC + cs + gq * 4);
                     rp[k] = v;
                 }
             } else {
@@ -648,7 +657,9 @@ extern "C" int nps_conv2d_plan(nps_conv2d_t* a) {
             if (pc_lds_bytes(t) > 160 * 1024) continue;
             const Geo g = make_geo(t);
             const int nt = t.KH * t.KW, ckb = nt == 1 ? 32 : 16;
-            if (g.PH * g.PW * (ckb / 4) > 9 * 256) continue;
+            const bool pb2 = t.TH * t.TW == 256;
+            const int maxp = pb2 ? (nt == 9 ? 6 : (nt == 4 ? 5 : 8)) : (nt == 1 ? 4 : 3);
+            if (g.PH * g.PW * (ckb / 4) > maxp * 256) continue;
             const long wgs = (long)g.tiles_x * g.tiles_y * a->B * units_co;
             // score: work-groups that fill the 256 CUs, penalising halo/edge waste
             const long useful = (long)a->Hout * a->Wout * a->B * units_co;

@@ -109,6 +109,71 @@ __global__ void timeconv_kernel(const float* __restrict__ pre, const float* __re
     }
 }
 
+
+// Specialised TimeConvDense for a compile-time (num_c, tw): the block's 64 pixels of the planar
+// pre-decoder output are staged in LDS once (coalesced), both conv1d layers run from LDS with fully
+// unrolled taps and the weights read as wave-uniform (scalar-cache) loads.
+template <int NC, int TW>
+__global__ __launch_bounds__(256) void timeconv_fast_kernel(const float* __restrict__ pre, const float* __restrict__ u,
+                                                            const float* __restrict__ w1, const float* __restrict__ b1,
+                                                            const float* __restrict__ w2, const float* __restrict__ b2,
+                                                            const float* __restrict__ dtcum, const float* __restrict__ mask,
+                                                            int mask_S, int mask_ch, float* __restrict__ out, int HW,
+                                                            int act_tanh) {
+    constexpr int L = 3 * TW;
+    constexpr int KA = (TW + 1) / 2;
+    constexpr int KB = (TW + 3) / 4 + 1 + (TW % 4 == 0 ? 1 : 0);
+    constexpr int L1 = (L - KA) / 2 + 1;
+    constexpr int C2 = 2 * NC;
+    static_assert(L1 - KB + 1 == TW, "TimeConvDense kernel sizes");
+    extern __shared__ float lds[];
+    float* xs = lds;                 // [NC*L][64]
+    float* d1 = lds + NC * L * 64;   // [C2][L1][64]
+    const int b = blockIdx.y;
+    const int p = threadIdx.x & 63, slot = threadIdx.x >> 6;
+    const int p0 = blockIdx.x * 64;
+    const int np = min(64, HW - p0);
+    const float* src = pre + (size_t)b * NC * L * HW + p0;
+    for (int i = threadIdx.x; i < NC * L * 64; i += 256) {
+        const int r = i >> 6, q = i & 63;
+        xs[i] = q < np ? src[(size_t)r * HW + q] : 0.f;
+    }
+    __syncthreads();
+    // conv1 (stride 2) + GELU: C2*L1 outputs per pixel, split over the 4 slots
+    for (int j = slot; j < C2 * L1; j += 4) {
+        const int o = j / L1, t1 = j - o * L1;
+        float acc = b1[o];
+#pragma unroll
+        for (int ci = 0; ci < NC; ++ci) {
+            const float* xr = xs + (ci * L + 2 * t1) * 64 + p;
+            const float* wr = w1 + (o * NC + ci) * KA;
+#pragma unroll
+            for (int k = 0; k < KA; ++k) acc = fmaf(wr[k], xr[k * 64], acc);
+        }
+        d1[(o * L1 + t1) * 64 + p] = nps::gelu_erf(acc);
+    }
+    __syncthreads();
+    if (p >= np) return;
+    const int pix = p0 + p;
+    const float m = mask ? mask[((size_t)b * mask_S + mask_ch) * HW + pix] : 0.f;
+    for (int j = slot; j < NC * TW; j += 4) {
+        const int o2 = j / TW, t2 = j - o2 * TW;
+        float acc = b2[o2];
+#pragma unroll
+        for (int o = 0; o < C2; ++o) {
+            const float* dr = d1 + (o * L1 + t2) * 64 + p;
+            const float* wr = w2 + (o2 * C2 + o) * KB;
+#pragma unroll
+            for (int k = 0; k < KB; ++k) acc = fmaf(wr[k], dr[k * 64], acc);
+        }
+        const float ulast = u[(((size_t)b * NC + o2) * TW + (TW - 1)) * HW + pix];
+        float v = ulast + dtcum[t2] * acc;
+        if (act_tanh) v = tanhf(v);
+        if (mask) v = v - m * v;
+        out[(((size_t)b * NC + o2) * TW + t2) * HW + pix] = v;
+    }
+}
+
 // sums[p] = sum of plane p (fp64)
 __global__ void plane_sums_kernel(const float* __restrict__ base, long plane_stride, int plane_size,
                                   double* __restrict__ sums) {
@@ -208,6 +273,31 @@ extern "C" int nps_timeconv_decode(const float* pre, const float* u, const float
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void*)timeconv_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
         attr_set = true;
+    }
+    if (tw == 25 && (num_c == 1 || num_c == 3)) {
+        const size_t lds2 = sizeof(float) * 64 * num_c * (3 * 25 + 2 * L1);
+        hipStream_t st = (hipStream_t)stream;
+        if (num_c == 1) {
+            static bool set1 = false;
+            if (!set1) {
+                (void)hipFuncSetAttribute((const void*)timeconv_fast_kernel<1, 25>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                set1 = true;
+            }
+            timeconv_fast_kernel<1, 25><<<dim3((HW + 63) / 64, B), 256, lds2, st>>>(
+                pre, u, w1, b1, w2, b2, dtcum, mask, mask_S, mask_ch, out, HW, act_tanh);
+        } else {
+            static bool set3 = false;
+            if (!set3) {
+                (void)hipFuncSetAttribute((const void*)timeconv_fast_kernel<3, 25>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                set3 = true;
+            }
+            timeconv_fast_kernel<3, 25><<<dim3((HW + 63) / 64, B), 256, lds2, st>>>(
+                pre, u, w1, b1, w2, b2, dtcum, mask, mask_S, mask_ch, out, HW, act_tanh);
+        }
+        NPS_CHECK_LAUNCH("timeconv_decode");
+        return 0;
     }
     timeconv_kernel<<<dim3((HW + 63) / 64, B), 256, lds, (hipStream_t)stream>>>(
         pre, u, w1, b1, w2, b2, dtcum, mask, mask_S, mask_ch, out, num_c, tw, HW, ka, kb, L1, act_tanh);
