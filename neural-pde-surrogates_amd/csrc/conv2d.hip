@@ -28,6 +28,10 @@ constexpr int CK = 16;          // input channels per K chunk
 constexpr int PIXS = CK + 4;    // LDS floats per patch pixel (+4 pad: conflict-free ds_read_b128)
 constexpr int MAXL = 12;        // max float4 patch loads per thread per chunk
 
+// 32-channel output blocks in the packed weight layout: a multiple of 6 so both the 64-co (2-block)
+// and the 192-co (6-block) work-group tiles index inside the buffer
+__host__ __device__ inline int packed_ncb(int Cout) { return 6 * ((Cout + 191) / 192); }
+
 struct Geo {
     int T, ri, rk, rstep, PH, PW, tiles_x, tiles_y;
 };
@@ -125,14 +129,17 @@ __device__ __forceinline__ void store_tile(const nps_conv2d_t& a, int b, int co_
         }
         return;
     }
+    // generic path: element address linear in co (NHWC stride 1, NCHW stride H*W)
+    const size_t base = a.out_nchw ? (((size_t)b * a.out_C) * a.out_H + dy) * a.out_W + dx
+                                   : (((size_t)b * a.out_H + dy) * a.out_W + dx) * a.out_C;
+    const size_t cstride = a.out_nchw ? (size_t)a.out_H * a.out_W : 1;
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const int co = co_base + 8 * m + 4 * h + e;
             if (co >= a.Cout) continue;
-            const size_t di = a.out_nchw ? (((size_t)b * a.out_C + co) * a.out_H + dy) * a.out_W + dx
-                                         : (((size_t)b * a.out_H + dy) * a.out_W + dx) * a.out_C + co;
+            const size_t di = base + (size_t)co * cstride;
             float v = acc[4 * m + e];
             if (a.bias) v += a.bias[co];
             if (!a.add_after_act) {
@@ -169,7 +176,7 @@ __global__ __launch_bounds__(WAVES * 64) void conv2d_fwd_kernel(const nps_conv2d
     float* pbuf = smem + 32;                                   // 2 patch buffers (128 B header keeps 16-B alignment)
     const int nchunks = (a.Cin + CK - 1) / CK;
     const int ntaps = a.KH * a.KW;
-    const int ncb = 2 * ((a.Cout + 63) / 64);
+    const int ncb = packed_ncb(a.Cout);
 
     if (a.gn_stats != nullptr && tid < a.gn_groups) {
         const double cnt = (double)(a.Cin / a.gn_groups) * a.Hin * a.Win;
@@ -341,15 +348,24 @@ __global__ __launch_bounds__(WAVES * 64) void conv2d_fwd_kernel(const nps_conv2d
 // the next K-stage (weights + input patch with the crop/concat/wrap/GN/GELU prologue) while the
 // consumers run the current one.  Producers hold stage s+2's global loads in registers across
 // the barrier (raw s_barrier, only lgkmcnt drained) so their HBM/L2 latency overlaps two stages.
-template <int NTAPS, int CKB, int PB>
+// Wave tile = CBW*32 output channels x PB*32 pixels; the 4 consumer waves are WCO (channel) x
+// 4/WCO (pixel); a work-group covers WCO*CBW*32 channels x (4/WCO)*PB*32 pixels.
+__host__ __device__ constexpr int pc_patch_px_max(int ntaps, int tile_px) {
+    return ntaps == 1 ? tile_px : (tile_px == 256 ? (ntaps == 4 ? 297 : 340) : (ntaps == 4 ? 153 : 180));
+}
+
+template <int NTAPS, int CKB, int PB, int CBW, int WCO>
 __global__ __launch_bounds__(512) void conv2d_pc_kernel(const nps_conv2d_t a) {
     constexpr int KWT = NTAPS == 9 ? 3 : (NTAPS == 4 ? 2 : 1);
     constexpr int SUB = CKB / CK;                       // 16-channel sub-chunks per stage
     constexpr int PIXSB = CKB + 4;                      // LDS floats per patch pixel
-    constexpr int AFL = SUB * NTAPS * 4 * 64 * 4;       // floats of the A (weight) tile per stage
-    constexpr int NAP = SUB * NTAPS;                    // A float4 per producer thread per stage
-    // max patch float4 per producer thread: ceil(patch pixels * CKB/4 / 256) for the tile shapes of nps_conv2d_plan
-    constexpr int MAXP = PB == 2 ? (NTAPS == 9 ? 6 : (NTAPS == 4 ? 5 : 8)) : (NTAPS == 1 ? 4 : 3);
+    constexpr int NCBG = WCO * CBW;                     // 32-channel output blocks per work-group
+    constexpr int WPX = 4 / WCO;
+    constexpr int TILE_PX = WPX * PB * 32;
+    constexpr int AROW = NCBG * 2 * 64;                 // float4 of A per (sub, tap)
+    constexpr int AFL = SUB * NTAPS * AROW * 4;         // floats of the A (weight) tile per stage
+    constexpr int NAP = SUB * NTAPS * AROW / 256;       // A float4 per producer thread per stage
+    constexpr int MAXP = (pc_patch_px_max(NTAPS, TILE_PX) * (CKB / 4) + 255) / 256;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const bool producer = wave >= 4;
@@ -363,22 +379,10 @@ __global__ __launch_bounds__(512) void conv2d_pc_kernel(const nps_conv2d_t a) {
     const int NG = npix * (CKB / 4);
     const int patch_fl = (npix * PIXSB + 3) & ~3;
     const int stage_fl = AFL + patch_fl;
-    float2* gn_tab = reinterpret_cast<float2*>(smem);
     float* ring = smem + 32;
     const int n16 = (a.Cin + CK - 1) / CK;              // 16-channel chunks of the packed weight
     const int nstages = (n16 + SUB - 1) / SUB;
-    const int ncb = 2 * ((a.Cout + 63) / 64);
-
-    if (a.gn_stats != nullptr && tid < a.gn_groups) {
-        const double cnt = (double)(a.Cin / a.gn_groups) * a.Hin * a.Win;
-        const double s1 = a.gn_stats[(b * a.gn_groups + tid) * 2], s2 = a.gn_stats[(b * a.gn_groups + tid) * 2 + 1];
-        const double mean = s1 / cnt;
-        double var = s2 / cnt - mean * mean;
-        var = var < 0.0 ? 0.0 : var;
-        gn_tab[tid] = make_float2((float)mean, (float)(1.0 / sqrt(var + (double)a.gn_eps)));
-    }
-    __syncthreads();
-    const int cpg = a.gn_stats ? a.Cin / a.gn_groups : 1;
+    const int ncb = packed_ncb(a.Cout);
 
     if (producer) {
         // ------------------------------------------------------------------ producers
@@ -402,10 +406,13 @@ __global__ __launch_bounds__(512) void conv2d_pc_kernel(const nps_conv2d_t a) {
         auto issue = [&](int st) {  // global loads of stage st into registers
 #pragma unroll
             for (int k = 0; k < NAP; ++k) {
-                const int sub = k / NTAPS, tap = k - sub * NTAPS;
+                const int e = k * 256 + ptid;
+                const int stp = (k * 256) / AROW;                 // (sub, tap) of this float4 (static)
+                const int rem = e - stp * AROW;
+                const int sub = stp / NTAPS, tap = stp - sub * NTAPS;
                 const int ch16 = st * SUB + sub;
                 f32x4 v = {0.f, 0.f, 0.f, 0.f};
-                if (ch16 < n16) v = wp[(((size_t)ch16 * NTAPS + tap) * ncb + 2 * cob) * 2 * 64 + ptid];
+                if (ch16 < n16) v = wp[(((size_t)ch16 * NTAPS + tap) * ncb + cob * NCBG) * 2 * 64 + rem];
                 ra[k] = v;
             }
             // source holding this stage's channels (uniform); fast path when one 4-aligned source covers it
@@ -492,16 +499,17 @@ __global__ __launch_bounds__(512) void conv2d_pc_kernel(const nps_conv2d_t a) {
     }
 
     // ---------------------------------------------------------------------- consumers
+    const int wco = wave % WCO, wpx = wave / WCO;
     int boff[PB];
 #pragma unroll
     for (int pb = 0; pb < PB; ++pb) {
-        const int P = wave * 32 * PB + pb * 32 + (lane & 31);
+        const int P = wpx * 32 * PB + pb * 32 + (lane & 31);
         const int ti = P / a.TW, tj = P - (P / a.TW) * a.TW;
         boff[pb] = (ti * g.PW + tj) * PIXSB + (lane >> 5) * 8;
     }
-    f32x16 acc[2][PB];
+    f32x16 acc[CBW][PB];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < CBW; ++i)
 #pragma unroll
         for (int j = 0; j < PB; ++j)
 #pragma unroll
@@ -514,15 +522,16 @@ __global__ __launch_bounds__(512) void conv2d_pc_kernel(const nps_conv2d_t a) {
     for (int st = 0; st < nstages; ++st) {
         const float* A = ring + (st & 1) * stage_fl;
         const float* Pt = A + AFL;
-        f32x4 av[2][2], bv[2][PB];
-        auto load_group = [&](int gi, f32x4 (&ad)[2], f32x4 (&bd)[PB]) {
+        f32x4 av[2][CBW], bv[2][PB];
+        auto load_group = [&](int gi, f32x4 (&ad)[CBW], f32x4 (&bd)[PB]) {
             const int q = gi & 1, tq = gi >> 1;
             const int sub = tq / NTAPS, tap = tq - sub * NTAPS;
             const int ky = tap / KWT, kx = tap % KWT;
             const int toff = (ky * g.PW + kx) * PIXSB + sub * CK;
 #pragma unroll
-            for (int cb = 0; cb < 2; ++cb)
-                ad[cb] = *reinterpret_cast<const f32x4*>(A + (((sub * NTAPS + tap) * 4 + cb * 2 + q) * 64 + lane) * 4);
+            for (int cb = 0; cb < CBW; ++cb)
+                ad[cb] = *reinterpret_cast<const f32x4*>(
+                    A + (((sub * NTAPS + tap) * NCBG + wco * CBW + cb) * 2 + q) * 256 + lane * 4);
 #pragma unroll
             for (int pb = 0; pb < PB; ++pb) bd[pb] = *reinterpret_cast<const f32x4*>(Pt + boff[pb] + toff + q * 4);
         };
@@ -536,7 +545,7 @@ __global__ __launch_bounds__(512) void conv2d_pc_kernel(const nps_conv2d_t a) {
 #pragma unroll
             for (int e = 0; e < 4; ++e)
 #pragma unroll
-                for (int cb = 0; cb < 2; ++cb)
+                for (int cb = 0; cb < CBW; ++cb)
 #pragma unroll
                     for (int pb = 0; pb < PB; ++pb)
                         acc[cb][pb] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[cur][cb][e], bv[cur][pb][e], acc[cb][pb], 0, 0, 0);
@@ -550,14 +559,17 @@ __global__ __launch_bounds__(512) void conv2d_pc_kernel(const nps_conv2d_t a) {
     const int h = lane >> 5;
 #pragma unroll
     for (int pb = 0; pb < PB; ++pb) {
-        const int P = wave * 32 * PB + pb * 32 + (lane & 31);
+        const int P = wpx * 32 * PB + pb * 32 + (lane & 31);
         const int ti = P / a.TW, tj = P - (P / a.TW) * a.TW;
         const int oy = oy0 + ti, ox = ox0 + tj;
         if (oy >= a.Hout || ox >= a.Wout) continue;
         const int dy = oy * a.out_os + a.out_off_y, dx = ox * a.out_os + a.out_off_x;
         if (dy < 0 || dy >= a.out_H || dx < 0 || dx >= a.out_W) continue;
 #pragma unroll
-        for (int cb = 0; cb < 2; ++cb) store_tile(a, b, cob * 64 + cb * 32, h, acc[cb][pb], dy, dx);
+        for (int cb = 0; cb < CBW; ++cb) {
+            store_tile(a, b, (cob * NCBG + wco * CBW + cb) * 32, h, acc[cb][pb], dy, dx);
+            __builtin_amdgcn_sched_barrier(0);  // keep each tile's epilogue loads local (register pressure)
+        }
     }
 }
 
@@ -568,7 +580,7 @@ __global__ void pack_weights_kernel(const float* __restrict__ w, float* __restri
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= total) return;
     const int ntaps = KH * KW;
-    const int ncb = 2 * ((Cout + 63) / 64);
+    const int ncb = packed_ncb(Cout);
     const int e = i & 3;
     size_t r = i >> 2;
     const int lane = r & 63; r >>= 6;
@@ -595,7 +607,7 @@ __global__ void pack_weights_kernel(const float* __restrict__ w, float* __restri
 }
 
 size_t packed_size(int Cout, int Cin, int ntaps) {
-    const size_t nchunks = (Cin + CK - 1) / CK, ncb = 2 * ((Cout + 63) / 64);
+    const size_t nchunks = (Cin + CK - 1) / CK, ncb = packed_ncb(Cout);
     return nchunks * ntaps * ncb * 2 * 64 * 4;
 }
 
@@ -606,11 +618,16 @@ bool pc_eligible(const nps_conv2d_t& a) {
            a.pre_act == 0;
 }
 
+// producer/consumer variant per tap count: 1x1 convs use 192-channel x 128-pixel work-groups
+// (the input is streamed once); 2x2 / 3x3 use 64 x 256 (or 64 x 128) so the weight tile of a
+// 16-channel stage fits LDS twice
+inline int pc_ncbg(int nt) { return nt == 1 ? 6 : 2; }
+
 int pc_lds_bytes(const nps_conv2d_t& a) {
     const Geo g = make_geo(a);
     const int nt = a.KH * a.KW;
     const int ckb = nt == 1 ? 32 : 16;
-    const int afl = (ckb / CK) * nt * 4 * 64 * 4;
+    const int afl = (ckb / CK) * nt * pc_ncbg(nt) * 2 * 64 * 4;
     const int patch = (g.PH * g.PW * (ckb + 4) + 3) & ~3;
     return (32 + 2 * (afl + patch)) * 4;
 }
@@ -645,29 +662,33 @@ extern "C" int nps_conv2d_plan(nps_conv2d_t* a) {
     a->lattice = (a->dil > 1 && a->stride == 1) ? 1 : 0;
     const long units_co = (a->Cout + 63) / 64;
     if (pc_eligible(*a)) {
-        // producer/consumer kernel: 256-pixel tiles (16x16 or 8x32), 128-pixel (8x16) when the grid is small
+        // producer/consumer kernel: 256-pixel tiles (16x16 or 8x32, whichever wastes less of the
+        // output edge); 128-pixel 8x16 tiles only when the 256-pixel grid cannot give every CU a
+        // work-group (the 8x16 tile does half the MFMAs per LDS byte).
+        const int nt = a->KH * a->KW;
+        const long units = (a->Cout + pc_ncbg(nt) * 32 - 1) / (pc_ncbg(nt) * 32);
         const int cand[3][2] = {{16, 16}, {8, 32}, {8, 16}};
         int best = -1;
-        long best_px = -1;
+        double best_eff = -1.0;
+        long best_wgs = 0;
         for (int i = 0; i < 3; ++i) {
             nps_conv2d_t t = *a;
             t.waves = 8;
             t.TH = cand[i][0];
             t.TW = cand[i][1];
+            const bool pb2 = t.TH * t.TW == 256;
+            if (nt == 1 && pb2) continue;  // 1x1: 192 x 128 work-groups only
             if (pc_lds_bytes(t) > 160 * 1024) continue;
             const Geo g = make_geo(t);
-            const int nt = t.KH * t.KW, ckb = nt == 1 ? 32 : 16;
-            const bool pb2 = t.TH * t.TW == 256;
-            const int maxp = pb2 ? (nt == 9 ? 6 : (nt == 4 ? 5 : 8)) : (nt == 1 ? 4 : 3);
-            if (g.PH * g.PW * (ckb / 4) > maxp * 256) continue;
-            const long wgs = (long)g.tiles_x * g.tiles_y * a->B * units_co;
-            // score: work-groups that fill the 256 CUs, penalising halo/edge waste
-            const long useful = (long)a->Hout * a->Wout * a->B * units_co;
-            const long covered = wgs * t.TH * t.TW;
-            const long px = (wgs >= 512 ? 2 * 512 : 2 * wgs) * 1000 + (1000 * useful) / covered;
-            if (px > best_px) {
-                best_px = px;
+            const long wgs = (long)g.tiles_x * g.tiles_y * a->B * units;
+            if (!pb2 && nt != 1 && best >= 0 && best_wgs >= 256) continue;  // 256-pixel tiles already fill the chip
+            const double useful = (double)a->Hout * a->Wout * a->B * units;
+            const double eff = useful / ((double)wgs * t.TH * t.TW) * (wgs < 256 ? (double)wgs / 256.0 : 1.0) *
+                               (pb2 || nt == 1 ? 1.0 : 0.8);
+            if (eff > best_eff) {
+                best_eff = eff;
                 best = i;
+                best_wgs = wgs;
             }
         }
         if (best >= 0) {
@@ -706,26 +727,27 @@ extern "C" int nps_conv2d_plan(nps_conv2d_t* a) {
 }
 
 namespace {
-template <int NT, int CKB, int PB>
+template <int NT, int CKB, int PB, int CBW, int WCO>
 void launch_pc_one(const nps_conv2d_t& a, dim3 grid, int lds, hipStream_t s) {
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)conv2d_pc_kernel<NT, CKB, PB>,
+        (void)hipFuncSetAttribute((const void*)conv2d_pc_kernel<NT, CKB, PB, CBW, WCO>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_set = true;
     }
-    conv2d_pc_kernel<NT, CKB, PB><<<grid, 512, lds, s>>>(a);
+    conv2d_pc_kernel<NT, CKB, PB, CBW, WCO><<<grid, 512, lds, s>>>(a);
 }
 
 int launch_pc(const nps_conv2d_t& a, dim3 grid, int lds, hipStream_t s) {
     const int nt = a.KH * a.KW;
     const bool pb2 = a.TH * a.TW == 256;
+    grid.y = (a.Cout + pc_ncbg(nt) * 32 - 1) / (pc_ncbg(nt) * 32);
     if (nt == 9) {
-        if (pb2) launch_pc_one<9, 16, 2>(a, grid, lds, s); else launch_pc_one<9, 16, 1>(a, grid, lds, s);
+        if (pb2) launch_pc_one<9, 16, 2, 2, 1>(a, grid, lds, s); else launch_pc_one<9, 16, 1, 2, 1>(a, grid, lds, s);
     } else if (nt == 4) {
-        if (pb2) launch_pc_one<4, 16, 2>(a, grid, lds, s); else launch_pc_one<4, 16, 1>(a, grid, lds, s);
+        if (pb2) launch_pc_one<4, 16, 2, 2, 1>(a, grid, lds, s); else launch_pc_one<4, 16, 1, 2, 1>(a, grid, lds, s);
     } else {
-        if (pb2) launch_pc_one<1, 32, 2>(a, grid, lds, s); else launch_pc_one<1, 32, 1>(a, grid, lds, s);
+        launch_pc_one<1, 32, 2, 3, 2>(a, grid, lds, s);
     }
     NPS_CHECK_LAUNCH("conv2d_fwd (producer/consumer)");
     return 0;
@@ -749,7 +771,8 @@ extern "C" int nps_conv2d_fwd(const nps_conv2d_t* ap, void* stream) {
                   "conv2d_fwd: bad GroupNorm prologue");
     NPS_CHECK_ARG(a.circ == 0 || (a.Hin > 0 && a.Win > 0), "conv2d_fwd: circular padding of empty frame");
     NPS_CHECK_ARG(a.waves == 1 || a.waves == 2 || a.waves == 4 || a.waves == 8, "conv2d_fwd: call nps_conv2d_plan first");
-    NPS_CHECK_ARG(a.waves == 8 ? (a.TH * a.TW == 256 || a.TH * a.TW == 128) && pc_eligible(a)
+    NPS_CHECK_ARG(a.waves == 8 ? (a.TH * a.TW == 256 || a.TH * a.TW == 128) && pc_eligible(a) &&
+                                     (a.KH * a.KW != 1 || a.TH * a.TW == 128)
                                : a.TH * a.TW == 64 * a.waves,
                   "conv2d_fwd: tile %dx%d does not match waves=%d", a.TH, a.TW, a.waves);
     const Geo g = make_geo(a);
@@ -776,34 +799,61 @@ extern "C" int nps_conv2d_fwd(const nps_conv2d_t* ap, void* stream) {
 
 // ------------------------------------------------------------------ GroupNorm statistics
 namespace {
+// One (group, sample) pair per blockIdx.(y,z); the frame is swept as contiguous 16-B runs per source
+// with 32-bit index math; per-thread fp32 partials over each float4, fp64 above that.
+__device__ __forceinline__ void gn_accum_src(const nps_src_t& S, int lo, int g0, int g1, int b, int Hin, int Win,
+                                             double& s, double& ss) {
+    const int clo = max(lo, g0), chi = min(lo + S.C, g1);
+    if (clo >= chi) return;
+    const int nc = chi - clo, lc0 = clo - lo;
+    const int y0 = max(0, S.off_y), y1 = min(Hin, S.off_y + S.H);
+    const int x0 = max(0, S.off_x), x1 = min(Win, S.off_x + S.W);
+    if (y0 >= y1 || x0 >= x1) return;
+    const int wi = x1 - x0;
+    const int stride = gridDim.x * blockDim.x;
+    if (nc == S.C && wi == S.W && (S.C & 3) == 0) {
+        // whole rows of the source, all channels: one contiguous run, no index math
+        const int n = (y1 - y0) * S.W * (S.C >> 2);
+        const f32x4* p = reinterpret_cast<const f32x4*>(S.ptr + ((size_t)(b * S.H + (y0 - S.off_y)) * S.W) * S.C);
+        for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+            const f32x4 v = p[i];
+            s += (double)((v[0] + v[1]) + (v[2] + v[3]));
+            ss += (double)((v[0] * v[0] + v[1] * v[1]) + (v[2] * v[2] + v[3] * v[3]));
+        }
+        return;
+    }
+    if ((nc & 3) == 0 && (lc0 & 3) == 0 && (S.C & 3) == 0) {
+        const int nq = nc >> 2;
+        const int n = (y1 - y0) * wi * nq;
+        for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+            const int pix = i / nq, q = i - pix * nq;
+            const int y = pix / wi, x = pix - y * wi;
+            const f32x4 v = *reinterpret_cast<const f32x4*>(
+                S.ptr + ((size_t)(b * S.H + (y + y0 - S.off_y)) * S.W + (x + x0 - S.off_x)) * S.C + lc0 + q * 4);
+            s += (double)((v[0] + v[1]) + (v[2] + v[3]));
+            ss += (double)((v[0] * v[0] + v[1] * v[1]) + (v[2] * v[2] + v[3] * v[3]));
+        }
+    } else {
+        const int n = (y1 - y0) * wi * nc;
+        for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+            const int pix = i / nc, cc = i - pix * nc;
+            const int y = pix / wi, x = pix - y * wi;
+            const float v = S.ptr[((size_t)(b * S.H + (y + y0 - S.off_y)) * S.W + (x + x0 - S.off_x)) * S.C + lc0 + cc];
+            s += v;
+            ss += (double)v * v;
+        }
+    }
+}
+
 __global__ void gn_stats_kernel(nps_conv2d_t a, int G, double* __restrict__ stats) {
-    // a.src / a.nsrc / frame fields only
     __shared__ double red[16];
     const int b = blockIdx.z, gidx = blockIdx.y;
     const int cpg = a.Cin / G;
     const int g0 = gidx * cpg, g1 = g0 + cpg;
     double s = 0.0, ss = 0.0;
-    int c0 = 0;
-    for (int si = 0; si < a.nsrc; ++si) {
-        const nps_src_t S = a.src[si];
-        const int lo = max(c0, g0), hi = min(c0 + S.C, g1);
-        c0 += S.C;
-        if (lo >= hi) continue;
-        const int nc = hi - lo, lc0 = lo - (c0 - S.C);
-        const int y0 = max(0, S.off_y), y1 = min(a.Hin, S.off_y + S.H);
-        const int x0 = max(0, S.off_x), x1 = min(a.Win, S.off_x + S.W);
-        if (y0 >= y1 || x0 >= x1) continue;
-        const int wi = x1 - x0;
-        const long n = (long)(y1 - y0) * wi * nc;
-        for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-            const long pix = i / nc;
-            const int cc = (int)(i - pix * nc);
-            const int y = (int)(pix / wi) + y0, x = (int)(pix % wi) + x0;
-            const float v = S.ptr[((size_t)(b * S.H + (y - S.off_y)) * S.W + (x - S.off_x)) * S.C + lc0 + cc];
-            s += v;
-            ss += (double)v * v;
-        }
-    }
+    gn_accum_src(a.src[0], 0, g0, g1, b, a.Hin, a.Win, s, ss);
+    if (a.nsrc > 1) gn_accum_src(a.src[1], a.src[0].C, g0, g1, b, a.Hin, a.Win, s, ss);
+    if (a.nsrc > 2) gn_accum_src(a.src[2], a.src[0].C + a.src[1].C, g0, g1, b, a.Hin, a.Win, s, ss);
     s = nps::block_sum(s, red);
     ss = nps::block_sum(ss, red);
     if (threadIdx.x == 0) {
@@ -836,9 +886,11 @@ extern "C" int nps_group_norm_stats(const nps_src_t* src, int nsrc, int B, int H
             return -2;
         }
     }
-    const long per = (long)Hin * Win * (Cin / G);
-    int nblk = (int)((per + 256 * 16 - 1) / (256 * 16));
-    nblk = nblk < 1 ? 1 : (nblk > 512 ? 512 : nblk);
+    // few blocks per (group, sample): each adds its fp64 partials with 2 atomics to one word, so
+    // the block count bounds the same-address atomic serialisation
+    const long per = (long)Hin * Win * (Cin / G) / 4;
+    int nblk = (int)((per + 256 * 32 - 1) / (256 * 32));
+    nblk = nblk < 1 ? 1 : (nblk > 96 ? 96 : nblk);
     gn_stats_kernel<<<dim3(nblk, G, B), 256, 0, s>>>(a, G, stats);
     NPS_CHECK_LAUNCH("group_norm_stats");
     return 0;
@@ -849,6 +901,31 @@ namespace {
 // out[B][Hin][Win][Cin] = act(GN(frame)) of the virtual frame (or the plain concat/crop when no
 // prologue): one pass, 16-B loads/stores, GELU evaluated once per element instead of once per
 // consuming conv tile.
+__device__ __forceinline__ f32x4 prologue4(const nps_conv2d_t& a, const float2* tab, int cpg, int c, f32x4 v) {
+    if (a.gn_stats != nullptr) {
+        if ((cpg & 3) == 0 && c + 4 <= a.Cin && (a.Cin & 3) == 0) {
+            const float2 mr = tab[c / cpg];
+            const f32x4 ga = *reinterpret_cast<const f32x4*>(a.gn_gamma + c);
+            const f32x4 be = *reinterpret_cast<const f32x4*>(a.gn_beta + c);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = (v[e] - mr.x) * mr.y * ga[e] + be[e];
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                if (c + e < a.Cin) {
+                    const float2 mr = tab[(c + e) / cpg];
+                    v[e] = (v[e] - mr.x) * mr.y * a.gn_gamma[c + e] + a.gn_beta[c + e];
+                }
+            }
+        }
+    }
+    if (a.pre_act == 1) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = nps::gelu_erf(v[e]);
+    }
+    return v;
+}
+
 __global__ void frame_pack_kernel(nps_conv2d_t a, float* __restrict__ out) {
     __shared__ float2 tab[16];
     const int b = blockIdx.y;
@@ -863,25 +940,27 @@ __global__ void frame_pack_kernel(nps_conv2d_t a, float* __restrict__ out) {
     }
     __syncthreads();
     const int cpg = a.gn_stats ? a.Cin / a.gn_groups : 1;
-    const int C4 = (a.Cin + 3) / 4;
-    const long n = (long)a.Hin * a.Win * C4;
-    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-        const long pix = i / C4;
-        const int c = (int)(i - pix * C4) * 4;
-        const int y = (int)(pix / a.Win), x = (int)(pix % a.Win);
-        f32x4 v = fetch4(a, b, y, x, c);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            if (c + e < a.Cin) {
-                float t = v[e];
-                if (a.gn_stats != nullptr) {
-                    const float2 mr = tab[(c + e) / cpg];
-                    t = (t - mr.x) * mr.y * a.gn_gamma[c + e] + a.gn_beta[c + e];
-                }
-                if (a.pre_act == 1) t = nps::gelu_erf(t);
-                v[e] = t;
-            }
+    const int stride = gridDim.x * blockDim.x;
+    const nps_src_t S0 = a.src[0];
+    if (a.nsrc == 1 && S0.off_y == 0 && S0.off_x == 0 && S0.H == a.Hin && S0.W == a.Win && (a.Cin & 3) == 0) {
+        // one source covering the frame: a flat contiguous sweep
+        const int C4 = a.Cin >> 2;
+        const int n = a.Hin * a.Win * C4;
+        const f32x4* src = reinterpret_cast<const f32x4*>(S0.ptr + (size_t)b * a.Hin * a.Win * a.Cin);
+        f32x4* dst = reinterpret_cast<f32x4*>(out + (size_t)b * a.Hin * a.Win * a.Cin);
+        for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+            const int c = (i % C4) * 4;
+            dst[i] = prologue4(a, tab, cpg, c, src[i]);
         }
+        return;
+    }
+    const int C4 = (a.Cin + 3) / 4;
+    const int n = a.Hin * a.Win * C4;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const int pix = i / C4;
+        const int c = (i - pix * C4) * 4;
+        const int y = pix / a.Win, x = pix - y * a.Win;
+        f32x4 v = prologue4(a, tab, cpg, c, fetch4(a, b, y, x, c));
         float* dst = out + ((size_t)(b * a.Hin + y) * a.Win + x) * a.Cin + c;
         if ((a.Cin & 3) == 0) {
             *reinterpret_cast<f32x4*>(dst) = v;

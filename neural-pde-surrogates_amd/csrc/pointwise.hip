@@ -139,38 +139,65 @@ __global__ __launch_bounds__(256) void timeconv_fast_kernel(const float* __restr
         xs[i] = q < np ? src[(size_t)r * HW + q] : 0.f;
     }
     __syncthreads();
-    // conv1 (stride 2) + GELU: C2*L1 outputs per pixel, split over the 4 slots
-    for (int j = slot; j < C2 * L1; j += 4) {
-        const int o = j / L1, t1 = j - o * L1;
-        float acc = b1[o];
+    // conv1 (stride 2) + GELU: each work item = one output channel x R1 consecutive positions, the
+    // input window held in registers (R1*KA FMAs per 2*R1+KA-2 LDS reads)
+    constexpr int R1 = 8;
+    static_assert(L1 % R1 == 0, "conv1 run length");
+    for (int j = slot; j < C2 * (L1 / R1); j += 4) {
+        const int o = j / (L1 / R1), t0 = (j - o * (L1 / R1)) * R1;
+        float acc[R1];
+#pragma unroll
+        for (int r = 0; r < R1; ++r) acc[r] = b1[o];
 #pragma unroll
         for (int ci = 0; ci < NC; ++ci) {
-            const float* xr = xs + (ci * L + 2 * t1) * 64 + p;
+            float xw[2 * (R1 - 1) + KA];
+            const float* xr = xs + (ci * L + 2 * t0) * 64 + p;
+#pragma unroll
+            for (int k = 0; k < 2 * (R1 - 1) + KA; ++k) xw[k] = xr[k * 64];
             const float* wr = w1 + (o * NC + ci) * KA;
 #pragma unroll
-            for (int k = 0; k < KA; ++k) acc = fmaf(wr[k], xr[k * 64], acc);
+            for (int k = 0; k < KA; ++k) {
+                const float wk = wr[k];
+#pragma unroll
+                for (int r = 0; r < R1; ++r) acc[r] = fmaf(wk, xw[2 * r + k], acc[r]);
+            }
         }
-        d1[(o * L1 + t1) * 64 + p] = nps::gelu_erf(acc);
+#pragma unroll
+        for (int r = 0; r < R1; ++r) d1[(o * L1 + t0 + r) * 64 + p] = nps::gelu_erf(acc[r]);
     }
     __syncthreads();
     if (p >= np) return;
     const int pix = p0 + p;
     const float m = mask ? mask[((size_t)b * mask_S + mask_ch) * HW + pix] : 0.f;
-    for (int j = slot; j < NC * TW; j += 4) {
-        const int o2 = j / TW, t2 = j - o2 * TW;
-        float acc = b2[o2];
+    constexpr int R2 = 5;
+    static_assert(TW % R2 == 0, "conv2 run length");
+    for (int j = slot; j < NC * (TW / R2); j += 4) {
+        const int o2 = j / (TW / R2), t0 = (j - o2 * (TW / R2)) * R2;
+        float acc[R2];
+#pragma unroll
+        for (int r = 0; r < R2; ++r) acc[r] = b2[o2];
 #pragma unroll
         for (int o = 0; o < C2; ++o) {
-            const float* dr = d1 + (o * L1 + t2) * 64 + p;
+            float dw[R2 - 1 + KB];
+            const float* dr = d1 + (o * L1 + t0) * 64 + p;
+#pragma unroll
+            for (int k = 0; k < R2 - 1 + KB; ++k) dw[k] = dr[k * 64];
             const float* wr = w2 + (o2 * C2 + o) * KB;
 #pragma unroll
-            for (int k = 0; k < KB; ++k) acc = fmaf(wr[k], dr[k * 64], acc);
+            for (int k = 0; k < KB; ++k) {
+                const float wk = wr[k];
+#pragma unroll
+                for (int r = 0; r < R2; ++r) acc[r] = fmaf(wk, dw[r + k], acc[r]);
+            }
         }
         const float ulast = u[(((size_t)b * NC + o2) * TW + (TW - 1)) * HW + pix];
-        float v = ulast + dtcum[t2] * acc;
-        if (act_tanh) v = tanhf(v);
-        if (mask) v = v - m * v;
-        out[(((size_t)b * NC + o2) * TW + t2) * HW + pix] = v;
+#pragma unroll
+        for (int r = 0; r < R2; ++r) {
+            float v = ulast + dtcum[t0 + r] * acc[r];
+            if (act_tanh) v = tanhf(v);
+            if (mask) v = v - m * v;
+            out[(((size_t)b * NC + o2) * TW + t0 + r) * HW + pix] = v;
+        }
     }
 }
 
