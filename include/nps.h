@@ -91,9 +91,15 @@ size_t nps_conv2d_packed_size(int Cout, int Cin, int ntaps);
  * MFMA-fragment-native layout.  `transposed_phase` >= 0 packs the
  * stride-2 4x4 transposed-conv weight w[Cin][Cout][4][4]
  * (nn.ConvTranspose2d layout) as the 2x2 conv of output phase
- * (py, px) = (phase>>1, phase&1); KH = KW = 2 then. */
+ * (py, px) = (phase>>1, phase&1); KH = KW = 2 then.  transposed_phase == -2 packs a 3x3 stride-2
+ * weight w[Cout][Cin/4][3][3] for the space-to-depth 2x2 form (KH = KW = 2, Cin = 4C). */
 int nps_conv2d_pack_weights(const float* w, float* wpack, int Cout, int Cin, int KH, int KW,
                             int transposed_phase, void* stream);
+/* Stride-2 3x3 convs (U-Net Downsample, proc_unet_modern.py:445-455) run as 2x2 stride-1 convs
+ * over a space-to-depth copy: out[B][Hq][Wq][4C], channel (dy*2+dx)*C + c = x[2y+dy-pad][2x+dx-pad][c]
+ * (zero outside); pack the weight with transposed_phase = -2 (Cin = 4C).  C % 4 == 0. */
+int nps_space_to_depth(const float* x, float* out, int B, int H, int W, int C, int pad, int Hq, int Wq,
+                       void* stream);
 /* Fill TH/TW/lattice/waves of `a` for its shape; returns the LDS bytes used. */
 int nps_conv2d_plan(nps_conv2d_t* a);
 int nps_conv2d_fwd(const nps_conv2d_t* a, void* stream);

@@ -593,7 +593,13 @@ __global__ void pack_weights_kernel(const float* __restrict__ w, float* __restri
     float v = 0.f;
     if (co < Cout && ci < Cin) {
         const int ky = tap / KW, kx = tap % KW;
-        if (tphase < 0) {
+        if (tphase == -2) {
+            // 3x3 / stride-2 conv as a 2x2 conv over the space-to-depth input: channel
+            // ci = (dy*2 + dx)*C + c, tap (ky, kx) -> kernel element (2ky + dy, 2kx + dx) of w[Cout][C][3][3]
+            const int C = Cin / 4, par = ci / C, c = ci - par * C;
+            const int kyy = 2 * ky + (par >> 1), kxx = 2 * kx + (par & 1);
+            if (kyy < 3 && kxx < 3) v = w[(((size_t)co * C + c) * 3 + kyy) * 3 + kxx];
+        } else if (tphase < 0) {
             v = w[(((size_t)co * Cin + ci) * KH + ky) * KW + kx];
         } else {
             // 4x4 / stride-2 transposed conv, output phase (py, px): tap (ty, tx) uses
@@ -646,8 +652,9 @@ extern "C" size_t nps_conv2d_packed_size(int Cout, int Cin, int ntaps) { return 
 extern "C" int nps_conv2d_pack_weights(const float* w, float* wpack, int Cout, int Cin, int KH, int KW,
                                        int transposed_phase, void* stream) {
     NPS_CHECK_ARG(w && wpack && Cout > 0 && Cin > 0 && KH > 0 && KW > 0, "conv2d_pack_weights: bad args");
-    NPS_CHECK_ARG(transposed_phase < 0 || (KH == 2 && KW == 2 && transposed_phase < 4),
-                  "conv2d_pack_weights: transposed phase packing needs KH=KW=2");
+    NPS_CHECK_ARG(transposed_phase == -1 || ((transposed_phase == -2 || (transposed_phase >= 0 && transposed_phase < 4)) &&
+                                             KH == 2 && KW == 2 && (transposed_phase != -2 || Cin % 4 == 0)),
+                  "conv2d_pack_weights: phase / space-to-depth packing needs KH=KW=2");
     const size_t total = packed_size(Cout, Cin, KH * KW);
     const int bs = 256;
     pack_weights_kernel<<<(unsigned)((total + bs - 1) / bs), bs, 0, (hipStream_t)stream>>>(w, wpack, Cout, Cin, KH, KW,
@@ -988,5 +995,37 @@ extern "C" int nps_frame_pack(const nps_conv2d_t* ap, float* out, void* stream) 
     nb = nb > 2048 ? 2048 : nb;
     frame_pack_kernel<<<dim3(nb, a.B), 256, 0, (hipStream_t)stream>>>(a, out);
     NPS_CHECK_LAUNCH("frame_pack");
+    return 0;
+}
+
+// ------------------------------------------------------------------ space-to-depth
+namespace {
+__global__ void space_to_depth_kernel(const float* __restrict__ x, float* __restrict__ out, int H, int W, int C, int pad,
+                                      int Hq, int Wq) {
+    const int b = blockIdx.y;
+    const int C4 = (4 * C) / 4;  // float4 groups of the 4C output channels (C % 4 == 0)
+    const int n = Hq * Wq * C4;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int pix = i / C4, g = i - pix * C4;
+        const int yq = pix / Wq, xq = pix - yq * Wq;
+        const int cc = g * 4, par = cc / C, c = cc - par * C;
+        const int y = 2 * yq + (par >> 1) - pad, xx = 2 * xq + (par & 1) - pad;
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if (y >= 0 && y < H && xx >= 0 && xx < W)
+            v = *reinterpret_cast<const f32x4*>(x + ((size_t)(b * H + y) * W + xx) * C + c);
+        *reinterpret_cast<f32x4*>(out + ((size_t)b * Hq * Wq + pix) * 4 * C + cc) = v;
+    }
+}
+}  // namespace
+
+extern "C" int nps_space_to_depth(const float* x, float* out, int B, int H, int W, int C, int pad, int Hq, int Wq,
+                                  void* stream) {
+    NPS_CHECK_ARG(x && out && B > 0 && H > 0 && W > 0 && C > 0 && (C & 3) == 0 && Hq > 0 && Wq > 0,
+                  "space_to_depth: bad args (C %% 4 must be 0)");
+    const long n = (long)Hq * Wq * C;
+    int nb = (int)((n + 255) / 256);
+    nb = nb > 2048 ? 2048 : nb;
+    space_to_depth_kernel<<<dim3(nb, B), 256, 0, (hipStream_t)stream>>>(x, out, H, W, C, pad, Hq, Wq);
+    NPS_CHECK_LAUNCH("space_to_depth");
     return 0;
 }

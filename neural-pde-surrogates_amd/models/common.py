@@ -94,6 +94,23 @@ class Conv2d(_PackedMixin, nn.Conv2d):
 
     def run(self, srcs, frame_hw, **kw):
         KH, KW, s, d, lo, hi, circ = self.geometry()
+        x = srcs[0].t
+        if (s == 2 and KH == 3 and KW == 3 and d == 1 and circ == 0 and lo == hi and lo[0] == lo[1]
+                and len(srcs) == 1 and srcs[0].off_y == 0 and srcs[0].off_x == 0
+                and tuple(x.shape[1:3]) == tuple(frame_hw) and x.shape[3] % 4 == 0
+                and "gn" not in kw and not kw.get("pre_act")):
+            # U-Net Downsample: 3x3/s2 as a 2x2 stride-1 conv over a space-to-depth copy
+            p = lo[0]
+            Ho = (frame_hw[0] + 2 * p - 3) // 2 + 1
+            Wo = (frame_hw[1] + 2 * p - 3) // 2 + 1
+            xq = ops.space_to_depth(x, p, Ho + 1, Wo + 1)
+            wk = self.weight
+            key = ("s2d", wk.data_ptr(), wk._version, str(wk.device))
+            if getattr(self, "_pk2_key", None) != key:
+                self._pk2 = ops.pack_conv_weight_s2d(wk)
+                self._pk2_key = key
+            return ops.conv2d([ops.Src(xq)], (Ho + 1, Wo + 1), self._pk2, self.bias, self.out_channels, 2, 2,
+                              out_hw=(Ho, Wo), **kw)
         return ops.conv2d(srcs, frame_hw, self._packed(ops.pack_conv_weight), self.bias, self.out_channels, KH, KW,
                           stride=s, dil=d, pad=lo, pad_bottom=hi, circ=circ, **kw)
 

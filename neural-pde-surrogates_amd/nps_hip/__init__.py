@@ -56,6 +56,7 @@ _SIGS = {
     "nps_conv2d_plan": (_i, [ctypes.POINTER(Conv2dArgs)]),
     "nps_conv2d_fwd": (_i, [ctypes.POINTER(Conv2dArgs), _vp]),
     "nps_frame_pack": (_i, [ctypes.POINTER(Conv2dArgs), _vp, _vp]),
+    "nps_space_to_depth": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp]),
     "nps_group_norm_stats": (_i, [ctypes.POINTER(Src), _i, _i, _i, _i, _i, _i, _vp, _i, _vp]),
     "nps_spectral_dft_w": (_i, [ctypes.POINTER(Src), _i, _i, _i, _i, _i, _i, _vp, _vp]),
     "nps_spectral_dft_h": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp]),

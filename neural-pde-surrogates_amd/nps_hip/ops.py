@@ -58,6 +58,23 @@ def pack_conv_weight(w: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def pack_conv_weight_s2d(w: torch.Tensor) -> torch.Tensor:
+    """3x3 stride-2 weight (Cout, C, 3, 3) -> packed 2x2 conv over the space-to-depth input (4C channels)."""
+    w = w.detach().contiguous()
+    Cout, C = w.shape[0], w.shape[1]
+    n = lib.nps_conv2d_packed_size(Cout, 4 * C, 4)
+    out = torch.empty(n, dtype=torch.float32, device=w.device)
+    check(lib.nps_conv2d_pack_weights(ptr(w), ptr(out), Cout, 4 * C, 2, 2, -2, stream_ptr()), "pack s2d")
+    return out
+
+
+def space_to_depth(x: torch.Tensor, pad: int, Hq: int, Wq: int) -> torch.Tensor:
+    B, H, W, C = x.shape
+    out = torch.empty((B, Hq, Wq, 4 * C), dtype=torch.float32, device=x.device)
+    check(lib.nps_space_to_depth(ptr(x), ptr(out), B, H, W, C, pad, Hq, Wq, stream_ptr()), "space_to_depth")
+    return out
+
+
 def pack_convT_phases(w: torch.Tensor) -> List[torch.Tensor]:
     """nn.ConvTranspose2d(k=4, s=2) weight (Cin, Cout, 4, 4) -> 4 packed 2x2 phase convs."""
     w = w.detach().contiguous()
