@@ -120,7 +120,12 @@ def main():
     ap.add_argument("--global-batch", type=int, default=16)
     ap.add_argument("--fno-modes", type=int, default=None)
     ap.add_argument("--cpu-calls", type=int, default=2, help="CPU-baseline sample size (model calls, 0 = skip)")
+    ap.add_argument("--mode", default="rollout", choices=["rollout", "train"],
+                    help="rollout = the headline metric; train = pushforward train_step + backward + RCCL "
+                         "all-reduce + Adam (samples/s)")
     args = ap.parse_args()
+    if args.mode == "train":
+        return run_train(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -197,6 +202,75 @@ def main():
             "loss_last_window": float(losses[-1].item()),
         }
         print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+def run_train(args):
+    """Training throughput: trainers/base.py:472-507 steps of the pushforward train_step (unroll 0, the
+    epoch-0 case) on a fixed global batch sharded over the ranks; gradients all-reduced over RCCL
+    (trainers.distributed.GradAllReducer, overlapped with backward), Adam(lr=1e-4) as in the cfgs."""
+    import types
+    from common.interfaces import D
+    from trainers.autoregressivepushforwardtrainer import AutoregressivePushforwardTrainer
+    from trainers.synthetic import twophase_batch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    sync = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+    if args.global_batch % world != 0:
+        raise SystemExit(f"global batch {args.global_batch} not divisible by {world} ranks")
+    B = args.global_batch // world
+    tw = 25
+    model, _, _ = build_model(args.model, args.res, args.num_c, dev, fno_modes=args.fno_modes)
+    model.train()
+    if world > 1:
+        from trainers.distributed import GradAllReducer
+        sync = GradAllReducer(model.parameters())
+        sync.broadcast_parameters(0)
+    u, cond, pos, sc = twophase_batch(B, args.num_c, 2 * tw, args.res, args.res, seed=1234 + rank,
+                                      obstacle="disc", device=dev)
+    batch = (u[:, :, :1], u, pos, cond, torch.empty(0, device=dev), sc)
+    cfg = types.SimpleNamespace(time_window=tw, base_resolution=(2 * tw, args.res, args.res), device=dev,
+                                batch_size=B, lr_step_interval=25, unrolling=0)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4)
+    tr = AutoregressivePushforwardTrainer(model=model, data=types.SimpleNamespace(pde=model.pde,
+                                                                                  data_interface=D.sim2d),
+                                          criterion=nn.MSELoss(reduction="sum"), optimizer=opt, config=cfg,
+                                          grad_sync=sync)
+    for _ in range(max(1, args.warmup)):
+        tr.train_one_epoch([batch], epoch=0)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    t0 = time.perf_counter()
+    loss = None
+    for _ in range(args.steps):
+        loss = tr.train_one_epoch([batch], epoch=0)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = t.item()
+    if rank == 0:
+        print(json.dumps({
+            "metric": "pushforward training samples/sec (train_step + backward + all-reduce + Adam)",
+            "value": round(args.global_batch * args.steps / elapsed, 3), "unit": "samples/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic",
+            "config": {"workload": f"{args.model.upper()} twophase cfg train_step, {args.res}x{args.res}, "
+                                   f"{args.num_c} fields, tw=25", "global_batch": args.global_batch,
+                       "per_gpu_batch": B, "parallelism": f"dp{world} (RCCL gradient all-reduce)"},
+            "loss_last": float(loss)}), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
 

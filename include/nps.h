@@ -97,7 +97,7 @@ int nps_conv2d_pack_weights(const float* w, float* wpack, int Cout, int Cin, int
                             int transposed_phase, void* stream);
 /* Stride-2 3x3 convs (U-Net Downsample, proc_unet_modern.py:445-455) run as 2x2 stride-1 convs
  * over a space-to-depth copy: out[B][Hq][Wq][4C], channel (dy*2+dx)*C + c = x[2y+dy-pad][2x+dx-pad][c]
- * (zero outside); pack the weight with transposed_phase = -2 (Cin = 4C).  C % 4 == 0. */
+ * (zero outside); pack the weight with transposed_phase = -2 (Cin = 4C). */
 int nps_space_to_depth(const float* x, float* out, int B, int H, int W, int C, int pad, int Hq, int Wq,
                        void* stream);
 /* Fill TH/TW/lattice/waves of `a` for its shape; returns the LDS bytes used. */
@@ -167,6 +167,78 @@ int nps_sq_err_sum(const float* a, const float* b, long n, double* out, void* st
 /* layout transforms at module boundaries */
 int nps_nchw_to_nhwc(const float* in, float* out, int B, int C, int H, int W, void* stream);
 int nps_nhwc_to_nchw(const float* in, float* out, int B, int C, int H, int W, void* stream);
+
+/* ==== backward (training) ================================================
+ * The pushforward train_step (trainers/autoregressivepushforwardtrainer.py:43-163) and
+ * trainers/base.py:492 `loss.backward()` differentiate every op above.  Input gradients of a
+ * conv are forward convs of dy (nps_conv2d_fwd) with flipped / transposed / phase-split weights;
+ * the entries below provide the rest. */
+
+/* Weight gradient of a stride-1 (optionally dilated, zero- or circularly-padded) conv on fp32
+ * MFMA: g[m][n][ky*KW + kx] += sum_{b,py,px} a[b][py][px][m] * X[b][y][x][n] with
+ * (y, x) = (py + ky*dil - pad_y, px + kx*dil - pad_x) in the frame extended circularly by
+ * `circ` (outside it reads 0) — the same geometry as nps_conv2d_t.  For a conv, a = dy and
+ * X = its input, so g is the nn.Conv2d weight grad [Cout][Cin][KH][KW]; stride-2 and transposed
+ * convs are issued in their space-to-depth / phase form.  Replaces aten
+ * convolution_backward's weight output for models/common.py:37-47, 93-120. */
+typedef struct {
+    const float* a;                 /* [B][Ha][Wa][M] (NHWC) */
+    int B, Ha, Wa, M;
+    const float* x;                 /* [B][Hx][Wx][N] (NHWC) */
+    int Hx, Wx, N;
+    int KH, KW, dil, pad_y, pad_x, circ;
+    float* g;                       /* [M][N][KH*KW], accumulated with += */
+} nps_wgrad_t;
+size_t nps_wgrad_lds_bytes(int KH, int KW);
+int nps_conv2d_wgrad(const nps_wgrad_t* p, void* stream);
+/* out[c] += sum over `rows` rows of x[row][c] (conv bias gradients; parameter-partial reductions) */
+int nps_channel_sums(const float* x, long rows, int C, float* out, void* stream);
+
+/* Backward of nps_frame_pack: torch.cat + crop_Nd + GroupNorm + GELU (proc_unet_modern.py:245-247,
+ * :194, common.py:20-34) given gy = dL/d(frame).  dsrc[i] (shape of source i, or NULL) receives the
+ * gradient of each source (0 where the source lies outside the frame); dgamma/dbeta [Cin] are written
+ * when the prologue has a GroupNorm; work = [B][2][Cin] fp64 scratch. */
+int nps_frame_pack_bwd(const nps_conv2d_t* a, const float* gy, float* const* dsrc, float* dgamma, float* dbeta,
+                       double* work, void* stream);
+
+/* element-wise pieces of the differentiated graph */
+int nps_gelu(const float* x, float* y, long n, void* stream);                                /* nn.GELU() */
+int nps_gelu_bwd(const float* x, const float* gy, float* gx, long n, void* stream);
+/* out[b][y+off_y][x+off_x][c] += src[b][y][x][c] (crop_Nd(h) + shortcut, proc_unet_modern.py:250) */
+int nps_add_at(float* out, const float* src, int B, int Ho, int Wo, int Hs, int Ws, int C, int off_y, int off_x,
+               void* stream);
+/* circular_pad_2d (models/common.py:61-90) on NHWC and its adjoint (wrap-sum) */
+int nps_circular_pad(const float* x, float* out, int B, int H, int W, int C, int pad, void* stream);
+int nps_circular_fold(const float* gp, float* gx, int B, int H, int W, int C, int pad, void* stream);
+/* out = (*scale) * (a - b): gradient of sqrt(MSELoss(sum)) (autoregressivepushforwardtrainer.py:158-162) */
+int nps_scaled_diff(const float* a, const float* b, const double* scale, float* out, long n, void* stream);
+
+/* SpectralConv2d backward (proc_fno.py:257-288 under torch.fft autograd):
+ *  gZ  = (c_k / (H W)) DFT_W(gy)  on the m2 kept bins (c_k = 1 for DC/Nyquist, else 2)  idft_w_bwd
+ *  gY  = nps_spectral_dft_h(gZ);   gX2, gwpack = mix_bwd(X2, wpack, gY)
+ *  gX1 = nps_spectral_idft_h(gX2); gx[w] = sum_k Re(gX1[k] e^{+2 pi i k w / W})           dft_w_bwd
+ *  gweights1/2 = unpack_grad(gwpack)  (PyTorch's complex-gradient convention, conj(x) * g) */
+int nps_spectral_idft_w_bwd(const float* gy, float* gZ, int B, int H, int W, int m2, int Cout, void* stream);
+int nps_spectral_dft_w_bwd(const float* gX1, float* gx, int B, int H, int W, int m2, int Cin, void* stream);
+int nps_spectral_mix_bwd(const float* X2, const float* wpack, const float* gY, float* gX2, float* gwpack, int B,
+                         int R, int m2, int Cin, int Cout, void* stream);
+int nps_spectral_unpack_grad(const float* gwpack, float* gw1, float* gw2, int Cin, int Cout, int H, int m1, int m2,
+                             void* stream);
+
+/* TimeConvDense + add_delta + tanh + mask backward (dec_grid.py:126-146, :8-31): gpre is planar like
+ * `pre`; ws[blocks][params] receives per-block partials of [w1 | b1 | w2 | b2] (blocks = B*ceil(H*W/64),
+ * params = 2c*c*ka + 2c + c*2c*kb + c), reduced with nps_channel_sums. */
+int nps_timeconv_decode_bwd(const float* pre, const float* u, const float* w1, const float* b1, const float* w2,
+                            const float* b2, const float* dtcum, const float* mask, int mask_S, int mask_ch,
+                            const float* gout, float* gpre, float* ws, int B, int num_c, int tw, int H, int W,
+                            int act_tanh, void* stream);
+/* 'individual_static' volume rescale backward (activation_wrapper.py:80-105):
+ * D[plane] = sum g (1 - m) u_in (nps_plane_dot), then gu_in (nps_volume_rescale_bwd). */
+int nps_plane_dot(const float* g, const float* u, const float* mask, int mask_S, int mask_ch, int B, int nct, int H,
+                  int W, double* D, void* stream);
+int nps_volume_rescale_bwd(const float* g, const double* new_tot, const double* prev_tot, const float* mpdcum,
+                           const float* mask, int mask_S, int mask_ch, const double* D, float* gu, int B, int num_c,
+                           int tw, int H, int W, void* stream);
 
 const char* nps_last_error(void);
 const char* nps_version(void);

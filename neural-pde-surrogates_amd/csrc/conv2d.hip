@@ -1003,26 +1003,37 @@ namespace {
 __global__ void space_to_depth_kernel(const float* __restrict__ x, float* __restrict__ out, int H, int W, int C, int pad,
                                       int Hq, int Wq) {
     const int b = blockIdx.y;
-    const int C4 = (4 * C) / 4;  // float4 groups of the 4C output channels (C % 4 == 0)
-    const int n = Hq * Wq * C4;
+    if ((C & 3) == 0) {
+        const int C4 = (4 * C) / 4;  // float4 groups of the 4C output channels
+        const int n = Hq * Wq * C4;
+        for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+            const int pix = i / C4, g = i - pix * C4;
+            const int yq = pix / Wq, xq = pix - yq * Wq;
+            const int cc = g * 4, par = cc / C, c = cc - par * C;
+            const int y = 2 * yq + (par >> 1) - pad, xx = 2 * xq + (par & 1) - pad;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if (y >= 0 && y < H && xx >= 0 && xx < W)
+                v = *reinterpret_cast<const f32x4*>(x + ((size_t)(b * H + y) * W + xx) * C + c);
+            *reinterpret_cast<f32x4*>(out + ((size_t)b * Hq * Wq + pix) * 4 * C + cc) = v;
+        }
+        return;
+    }
+    const int n = Hq * Wq * 4 * C;  // channel counts that are not a multiple of 4: one float per thread
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const int pix = i / C4, g = i - pix * C4;
+        const int pix = i / (4 * C), cc = i - pix * 4 * C;
         const int yq = pix / Wq, xq = pix - yq * Wq;
-        const int cc = g * 4, par = cc / C, c = cc - par * C;
+        const int par = cc / C, c = cc - par * C;
         const int y = 2 * yq + (par >> 1) - pad, xx = 2 * xq + (par & 1) - pad;
-        f32x4 v = {0.f, 0.f, 0.f, 0.f};
-        if (y >= 0 && y < H && xx >= 0 && xx < W)
-            v = *reinterpret_cast<const f32x4*>(x + ((size_t)(b * H + y) * W + xx) * C + c);
-        *reinterpret_cast<f32x4*>(out + ((size_t)b * Hq * Wq + pix) * 4 * C + cc) = v;
+        out[(size_t)b * Hq * Wq * 4 * C + i] =
+            (y >= 0 && y < H && xx >= 0 && xx < W) ? x[((size_t)(b * H + y) * W + xx) * C + c] : 0.f;
     }
 }
 }  // namespace
 
 extern "C" int nps_space_to_depth(const float* x, float* out, int B, int H, int W, int C, int pad, int Hq, int Wq,
                                   void* stream) {
-    NPS_CHECK_ARG(x && out && B > 0 && H > 0 && W > 0 && C > 0 && (C & 3) == 0 && Hq > 0 && Wq > 0,
-                  "space_to_depth: bad args (C %% 4 must be 0)");
-    const long n = (long)Hq * Wq * C;
+    NPS_CHECK_ARG(x && out && B > 0 && H > 0 && W > 0 && C > 0 && Hq > 0 && Wq > 0, "space_to_depth: bad args");
+    const long n = (long)Hq * Wq * C * ((C & 3) ? 4 : 1);
     int nb = (int)((n + 255) / 256);
     nb = nb > 2048 ? 2048 : nb;
     space_to_depth_kernel<<<dim3(nb, B), 256, 0, (hipStream_t)stream>>>(x, out, H, W, C, pad, Hq, Wq);

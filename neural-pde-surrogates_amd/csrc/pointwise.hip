@@ -266,6 +266,161 @@ __global__ void transpose_kernel(const float* __restrict__ in, float* __restrict
     }
 }
 
+
+// ---------------------------------------------------------------- TimeConvDense backward
+// One wave = 64 pixels, one pixel per lane; the forward chain is recomputed per pixel
+// (dec_grid.py:126-146 + add_delta :8-31 + tanh + mask), then back-propagated:
+//   gpre[b][ci*L + j][pix]  (planar, like the forward's pre-decoder output)
+//   ws[block][w1 | b1 | w2 | b2]  per-block parameter-gradient partials (summed by nps_channel_sums).
+__global__ __launch_bounds__(64) void timeconv_bwd_kernel(
+    const float* __restrict__ pre, const float* __restrict__ u, const float* __restrict__ w1,
+    const float* __restrict__ b1, const float* __restrict__ w2, const float* __restrict__ b2,
+    const float* __restrict__ dtcum, const float* __restrict__ mask, int mask_S, int mask_ch,
+    const float* __restrict__ gout, float* __restrict__ gpre, float* __restrict__ ws, int nc, int tw, int HW, int ka,
+    int kb, int L1, int act_tanh, int nparams) {
+    extern __shared__ float lds[];
+    const int C2 = 2 * nc, L = 3 * tw;
+    float* d1 = lds;                       // [C2*L1][64]  GELU(conv1)
+    float* gd = lds + C2 * L1 * 64;        // [C2*L1][64]  GELU'(conv1) -> grad of conv1 pre-activation
+    float* gd2 = gd + C2 * L1 * 64;        // [nc*tw][64]  grad of conv2 output
+    const int b = blockIdx.y, p = threadIdx.x;
+    const int pix = blockIdx.x * 64 + p;
+    const bool valid = pix < HW;
+    const int pc = valid ? pix : 0;
+    const float* xb = pre + (size_t)b * nc * L * HW + pc;
+    const size_t blk = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+    // 1. conv1 (stride 2) pre-activation
+    for (int o = 0; o < C2; ++o)
+        for (int t1 = 0; t1 < L1; ++t1) {
+            float acc = b1[o];
+            for (int ci = 0; ci < nc; ++ci)
+                for (int k = 0; k < ka; ++k) acc = fmaf(w1[(o * nc + ci) * ka + k], xb[(size_t)(ci * L + 2 * t1 + k) * HW], acc);
+            const float z = acc;
+            d1[(o * L1 + t1) * 64 + p] = nps::gelu_erf(z);
+            gd[(o * L1 + t1) * 64 + p] = 0.5f * (1.0f + erff(z * 0.70710678118654752440f)) +
+                                         z * 0.39894228040143267794f * expf(-0.5f * z * z);
+        }
+    // 2. conv2, add_delta, tanh, mask -> gradient of conv2's output
+    const float m = (mask && valid) ? mask[((size_t)b * mask_S + mask_ch) * HW + pix] : 0.f;
+    for (int o2 = 0; o2 < nc; ++o2) {
+        const float ulast = u[(((size_t)b * nc + o2) * tw + (tw - 1)) * HW + pc];
+        for (int t = 0; t < tw; ++t) {
+            float acc = b2[o2];
+            for (int o = 0; o < C2; ++o)
+                for (int k = 0; k < kb; ++k) acc = fmaf(w2[(o2 * C2 + o) * kb + k], d1[(o * L1 + t + k) * 64 + p], acc);
+            float g = valid ? gout[(((size_t)b * nc + o2) * tw + t) * HW + pix] : 0.f;
+            if (mask) g = g - m * g;
+            if (act_tanh) {
+                const float y = tanhf(ulast + dtcum[t] * acc);
+                g *= 1.f - y * y;
+            }
+            gd2[(o2 * tw + t) * 64 + p] = g * dtcum[t];
+        }
+    }
+    // 3. parameter partials of conv2: w2[o2][o][k], b2[o2]
+    const int ow1 = 0, ob1 = C2 * nc * ka, ow2 = ob1 + C2, ob2 = ow2 + nc * C2 * kb;
+    for (int o2 = 0; o2 < nc; ++o2) {
+        float sb = 0.f;
+        for (int t = 0; t < tw; ++t) sb += gd2[(o2 * tw + t) * 64 + p];
+        sb = nps::wave_sum((double)sb);
+        if (p == 0) ws[blk * nparams + ob2 + o2] = sb;
+        for (int o = 0; o < C2; ++o)
+            for (int k = 0; k < kb; ++k) {
+                float s2 = 0.f;
+                for (int t = 0; t < tw; ++t) s2 = fmaf(gd2[(o2 * tw + t) * 64 + p], d1[(o * L1 + t + k) * 64 + p], s2);
+                s2 = (float)nps::wave_sum((double)s2);
+                if (p == 0) ws[blk * nparams + ow2 + (o2 * C2 + o) * kb + k] = s2;
+            }
+    }
+    // 4. gradient of conv1's pre-activation (in place over GELU')
+    for (int o = 0; o < C2; ++o)
+        for (int t1 = 0; t1 < L1; ++t1) {
+            float g = 0.f;
+            for (int o2 = 0; o2 < nc; ++o2)
+                for (int k = 0; k < kb; ++k) {
+                    const int t = t1 - k;
+                    if (t >= 0 && t < tw) g = fmaf(gd2[(o2 * tw + t) * 64 + p], w2[(o2 * C2 + o) * kb + k], g);
+                }
+            gd[(o * L1 + t1) * 64 + p] *= g;
+        }
+    // 5. parameter partials of conv1: w1[o][ci][k], b1[o]
+    for (int o = 0; o < C2; ++o) {
+        float sb = 0.f;
+        for (int t1 = 0; t1 < L1; ++t1) sb += gd[(o * L1 + t1) * 64 + p];
+        sb = (float)nps::wave_sum((double)sb);
+        if (p == 0) ws[blk * nparams + ob1 + o] = sb;
+        for (int ci = 0; ci < nc; ++ci)
+            for (int k = 0; k < ka; ++k) {
+                float s1 = 0.f;
+                for (int t1 = 0; t1 < L1; ++t1)
+                    s1 = fmaf(gd[(o * L1 + t1) * 64 + p], xb[(size_t)(ci * L + 2 * t1 + k) * HW], s1);
+                s1 = (float)nps::wave_sum((double)s1);
+                if (p == 0) ws[blk * nparams + ow1 + (o * nc + ci) * ka + k] = s1;
+            }
+    }
+    // 6. gradient of the pre-decoder output
+    if (!valid) return;
+    float* gb = gpre + (size_t)b * nc * L * HW + pix;
+    for (int ci = 0; ci < nc; ++ci)
+        for (int j = 0; j < L; ++j) {
+            float g = 0.f;
+            for (int k = (j & 1); k < ka; k += 2) {   // 2 t1 + k = j
+                const int t1 = (j - k) >> 1;
+                if (j - k < 0 || t1 >= L1) continue;
+                for (int o = 0; o < C2; ++o) g = fmaf(gd[(o * L1 + t1) * 64 + p], w1[(o * nc + ci) * ka + k], g);
+            }
+            gb[(size_t)(ci * L + j) * HW] = g;
+        }
+}
+
+// D[plane] = sum_hw g*(1-m) * u   (planes (b, c, t); m = spatial-cond mask of sample b or none)
+__global__ void plane_dot_kernel(const float* __restrict__ g, const float* __restrict__ u,
+                                 const float* __restrict__ mask, int mask_S, int mask_ch, int nct, int HW,
+                                 double* __restrict__ D) {
+    __shared__ double red[16];
+    const int plane = blockIdx.y;
+    const int b = plane / nct;
+    const float* gp = g + (size_t)plane * HW;
+    const float* up = u + (size_t)plane * HW;
+    const float* mk = mask ? mask + ((size_t)b * mask_S + mask_ch) * HW : nullptr;
+    double s = 0.0;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < HW; i += gridDim.x * blockDim.x) {
+        float gg = gp[i];
+        if (mk) gg = gg - mk[i] * gg;
+        s += (double)(gg * up[i]);
+    }
+    s = nps::block_sum(s, red);
+    if (threadIdx.x == 0) atomicAdd(&D[plane], s);
+}
+
+// backward of volume_rescale_kernel (activation_wrapper.py:80-105):
+//   v = (u / s) * f(s), f = resc(s) * prev;  df/ds = 1 - tanh^2;  out = v - m v
+//   gu = g1 f / s + D ((1 - tanh^2) / s - f / s^2),   g1 = g (1 - m),  D = sum_plane g1 u
+__global__ void volume_rescale_bwd_kernel(const float* __restrict__ g,
+                                          const double* __restrict__ new_tot, const double* __restrict__ prev_tot,
+                                          const float* __restrict__ mpdcum, const float* __restrict__ mask,
+                                          int mask_S, int mask_ch, const double* __restrict__ D, int nc, int tw,
+                                          int HW, float* __restrict__ gu) {
+    const int plane = blockIdx.y;
+    const int t = plane % tw;
+    const int bc = plane / tw;
+    const int b = bc / nc;
+    const float newt = (float)new_tot[plane];
+    const float prev = (float)prev_tot[bc];
+    const float mpd = mpdcum[t];
+    const float th = tanhf((1.f - newt / prev) * 100.f / mpd);
+    const float f = (1.f - th / 100.f * mpd) * prev;
+    const float coef = (float)D[plane] * ((1.f - th * th) / newt - f / (newt * newt));
+    const float* gp = g + (size_t)plane * HW;
+    float* op = gu + (size_t)plane * HW;
+    const float* mk = mask ? mask + ((size_t)b * mask_S + mask_ch) * HW : nullptr;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < HW; i += gridDim.x * blockDim.x) {
+        float gg = gp[i];
+        if (mk) gg = gg - mk[i] * gg;
+        op[i] = gg * f / newt + coef;
+    }
+}
+
 }  // namespace
 
 extern "C" int nps_pack_grid_input(const float* u, const float* pos, const float* cond, const float* sc, float* xin,
@@ -383,5 +538,64 @@ extern "C" int nps_nhwc_to_nchw(const float* in, float* out, int B, int C, int H
     const int R = H * W, Cc = C;
     transpose_kernel<<<dim3((R + 31) / 32, (Cc + 31) / 32, B), dim3(32, 8), 0, (hipStream_t)stream>>>(in, out, R, Cc);
     NPS_CHECK_LAUNCH("nhwc_to_nchw");
+    return 0;
+}
+
+extern "C" int nps_timeconv_decode_bwd(const float* pre, const float* u, const float* w1, const float* b1,
+                                       const float* w2, const float* b2, const float* dtcum, const float* mask,
+                                       int mask_S, int mask_ch, const float* gout, float* gpre, float* ws, int B,
+                                       int num_c, int tw, int H, int W, int act_tanh, void* stream) {
+    NPS_CHECK_ARG(pre && u && w1 && b1 && w2 && b2 && dtcum && gout && gpre && ws && B > 0 && num_c > 0 && tw > 0 &&
+                      H > 0 && W > 0,
+                  "timeconv_decode_bwd: bad args");
+    const int ka = (tw + 1) / 2;
+    const int kb = (tw + 3) / 4 + 1 + (tw % 4 == 0 ? 1 : 0);
+    const int L1 = (3 * tw - ka) / 2 + 1;
+    NPS_CHECK_ARG(L1 - kb + 1 == tw, "timeconv_decode_bwd: kernel sizes do not reproduce tw=%d", tw);
+    const int nparams = 2 * num_c * num_c * ka + 2 * num_c + num_c * 2 * num_c * kb + num_c;
+    const size_t lds = sizeof(float) * 64 * (2 * 2 * num_c * L1 + num_c * tw);
+    NPS_CHECK_ARG(lds <= 160 * 1024, "timeconv_decode_bwd: num_c=%d tw=%d too large", num_c, tw);
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)timeconv_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        attr_set = true;
+    }
+    const int HW = H * W;
+    timeconv_bwd_kernel<<<dim3((HW + 63) / 64, B), 64, lds, (hipStream_t)stream>>>(
+        pre, u, w1, b1, w2, b2, dtcum, mask, mask_S, mask_ch, gout, gpre, ws, num_c, tw, HW, ka, kb, L1, act_tanh,
+        nparams);
+    NPS_CHECK_LAUNCH("timeconv_decode_bwd");
+    return 0;
+}
+
+extern "C" int nps_plane_dot(const float* g, const float* u, const float* mask, int mask_S, int mask_ch, int B,
+                             int nct, int H, int W, double* D, void* stream) {
+    NPS_CHECK_ARG(g && u && D && B > 0 && nct > 0 && H > 0 && W > 0, "plane_dot: bad args");
+    hipStream_t s = (hipStream_t)stream;
+    if (hipMemsetAsync(D, 0, sizeof(double) * B * nct, s) != hipSuccess) {
+        nps::set_error("plane_dot: memset failed");
+        return -2;
+    }
+    const int HW = H * W;
+    int nb = (HW + 256 * 8 - 1) / (256 * 8);
+    nb = nb < 1 ? 1 : (nb > 64 ? 64 : nb);
+    plane_dot_kernel<<<dim3(nb, B * nct), 256, 0, s>>>(g, u, mask, mask_S, mask_ch, nct, HW, D);
+    NPS_CHECK_LAUNCH("plane_dot");
+    return 0;
+}
+
+extern "C" int nps_volume_rescale_bwd(const float* g, const double* new_tot, const double* prev_tot,
+                                      const float* mpdcum, const float* mask, int mask_S, int mask_ch,
+                                      const double* D, float* gu, int B, int num_c, int tw, int H, int W,
+                                      void* stream) {
+    NPS_CHECK_ARG(g && new_tot && prev_tot && mpdcum && D && gu && B > 0 && num_c > 0 && tw > 0,
+                  "volume_rescale_bwd: bad args");
+    const int HW = H * W;
+    int nb = (HW + 256 * 4 - 1) / (256 * 4);
+    nb = nb < 1 ? 1 : (nb > 64 ? 64 : nb);
+    volume_rescale_bwd_kernel<<<dim3(nb, B * num_c * tw), 256, 0, (hipStream_t)stream>>>(
+        g, new_tot, prev_tot, mpdcum, mask, mask_S, mask_ch, D, num_c, tw, HW, gu);
+    NPS_CHECK_LAUNCH("volume_rescale_bwd");
     return 0;
 }

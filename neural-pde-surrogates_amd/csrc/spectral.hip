@@ -28,7 +28,9 @@ __device__ __forceinline__ float2 twiddle(int k, int n, int N) {
 }
 
 // X1[b][h][k2][c] = sum_w x[b][h][w][c] e^{-2 pi i k2 w / W}
-__global__ void dft_w_kernel(nps_conv2d_t a, int m2, float2* __restrict__ X1) {
+// With c2r_adj != 0 this is the adjoint of the c2r synthesis (backward of idft_w): every bin is scaled
+// by `scale` and, except DC / Nyquist, doubled (torch irfft backward: rfft(g)/N, columns 1..W-(W//2+1) x2).
+__global__ void dft_w_kernel(nps_conv2d_t a, int m2, float2* __restrict__ X1, float scale, int c2r_adj) {
     extern __shared__ float2 tw[];  // [KW_CHUNK][W]
     const int h = blockIdx.x, b = blockIdx.y;
     const int W = a.Win, H = a.Hin, C = a.Cin;
@@ -66,8 +68,14 @@ __global__ void dft_w_kernel(nps_conv2d_t a, int m2, float2* __restrict__ X1) {
                 }
             }
 #pragma unroll
-            for (int k = 0; k < KW_CHUNK; ++k)
-                if (k < nk) X1[((size_t)(b * H + h) * m2 + kb + k) * C + c] = make_float2(re[k], im[k]);
+            for (int k = 0; k < KW_CHUNK; ++k) {
+                if (k < nk) {
+                    float f = scale;
+                    const int kk = kb + k;
+                    if (c2r_adj && !((kk == 0) || (2 * kk == W))) f *= 2.f;
+                    X1[((size_t)(b * H + h) * m2 + kk) * C + c] = make_float2(re[k] * f, im[k] * f);
+                }
+            }
         }
     }
 }
@@ -184,13 +192,16 @@ __global__ void idft_h_kernel(const float2* __restrict__ Y, float2* __restrict__
 }
 
 // out[b][h][w][o] (=|+=) act( sum_k c_k Re(Z[b][h][k][o] e^{2 pi i k w / W}) / (H W) [+ addend] )
+// doubling = 0, scale = 1 is the adjoint of the truncated real-input DFT (backward of dft_w):
+// gx[w] = sum_k Re(gX[k] e^{+2 pi i k w / W}).
 __global__ void idft_w_kernel(const float2* __restrict__ Z, float* __restrict__ out, int H, int W, int m2, int Cout,
-                              int accumulate, const float* __restrict__ addend, int act) {
+                              int accumulate, const float* __restrict__ addend, int act, float scale_arg,
+                              int doubling) {
     extern __shared__ float2 tw[];  // [m2][W]
     const int h = blockIdx.x, b = blockIdx.y;
     for (int i = threadIdx.x; i < m2 * W; i += blockDim.x) tw[i] = twiddle(i / W, i % W, W);
     __syncthreads();
-    const float scale = 1.0f / ((float)H * (float)W);
+    const float scale = scale_arg;
     for (int o = threadIdx.x; o < Cout; o += blockDim.x) {
         float zr[KW_CHUNK], zi[KW_CHUNK];
         for (int kb = 0; kb < m2; kb += KW_CHUNK) {
@@ -203,7 +214,7 @@ __global__ void idft_w_kernel(const float2* __restrict__ Z, float* __restrict__ 
                     z = Z[((size_t)(b * H + h) * m2 + kk) * Cout + o];
                     // one-sided c2r: DC and (even W) Nyquist count once, with Im discarded
                     const bool self_conj = (kk == 0) || (2 * kk == W);
-                    const float cm = self_conj ? 1.f : 2.f;
+                    const float cm = (self_conj || !doubling) ? 1.f : 2.f;
                     z.x *= cm;
                     z.y = self_conj ? 0.f : z.y * cm;
                 }
@@ -236,6 +247,86 @@ __global__ void idft_w_kernel(const float2* __restrict__ Z, float* __restrict__ 
     }
 }
 
+
+// Backward of mix_kernel for one mode per block (weights streamed once):
+//   gX2[b][mode][i] = sum_o gY[b][mode][o] * conj(wp[mode][i][o])
+//   gwp[mode][i][o] = sum_b conj(X2[b][mode][i]) * gY[b][mode][o]
+// One wave per input channel row i: lanes sweep o (coalesced), the gX2 sums are wave reductions.
+__global__ void mix_bwd_kernel(const float2* __restrict__ X2, const float2* __restrict__ wp,
+                               const float2* __restrict__ gY, float2* __restrict__ gX2, float2* __restrict__ gwp,
+                               int B, int nmodes, int Cin, int Cout) {
+    extern __shared__ float2 gys[];  // [B][Cout]
+    const int mode = blockIdx.x;
+    for (int i = threadIdx.x; i < B * Cout; i += blockDim.x)
+        gys[i] = gY[((size_t)(i / Cout) * nmodes + mode) * Cout + i % Cout];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int i = blockIdx.y * nw + wave; i < Cin; i += gridDim.y * nw) {
+        for (int b0 = 0; b0 < B; b0 += MAXB) {
+            const int nb = min(MAXB, B - b0);
+            float2 xv[MAXB];
+#pragma unroll
+            for (int bb = 0; bb < MAXB; ++bb)
+                xv[bb] = bb < nb ? X2[((size_t)(b0 + bb) * nmodes + mode) * Cin + i] : make_float2(0.f, 0.f);
+            float2 gx[MAXB];
+#pragma unroll
+            for (int bb = 0; bb < MAXB; ++bb) gx[bb] = make_float2(0.f, 0.f);
+            for (int o = lane; o < Cout; o += 64) {
+                const size_t wi = ((size_t)mode * Cin + i) * Cout + o;
+                const float2 w = wp[wi];
+                float2 gw = b0 == 0 ? make_float2(0.f, 0.f) : gwp[wi];
+#pragma unroll
+                for (int bb = 0; bb < MAXB; ++bb) {
+                    if (bb < nb) {
+                        const float2 g = gys[(b0 + bb) * Cout + o];
+                        // g * conj(w)
+                        gx[bb].x = fmaf(g.x, w.x, fmaf(g.y, w.y, gx[bb].x));
+                        gx[bb].y = fmaf(g.y, w.x, fmaf(-g.x, w.y, gx[bb].y));
+                        // conj(x) * g
+                        gw.x = fmaf(xv[bb].x, g.x, fmaf(xv[bb].y, g.y, gw.x));
+                        gw.y = fmaf(xv[bb].x, g.y, fmaf(-xv[bb].y, g.x, gw.y));
+                    }
+                }
+                gwp[wi] = gw;
+            }
+#pragma unroll
+            for (int bb = 0; bb < MAXB; ++bb) {
+                if (bb < nb) {
+                    float re = gx[bb].x, im = gx[bb].y;
+#pragma unroll
+                    for (int off = 32; off > 0; off >>= 1) {
+                        re += __shfl_xor(re, off, 64);
+                        im += __shfl_xor(im, off, 64);
+                    }
+                    if (lane == 0) gX2[((size_t)(b0 + bb) * nmodes + mode) * Cin + i] = make_float2(re, im);
+                }
+            }
+        }
+    }
+}
+
+// gw1/gw2 [Cin][Cout][m1][m2] from gwp[r][k2][i][o] (adjoint of spec_pack_kernel: a weights1 row that
+// the weights2 corner overwrites in the forward gets zero gradient)
+__global__ void spec_unpack_grad_kernel(const float2* __restrict__ gwp, float2* __restrict__ gw1,
+                                        float2* __restrict__ gw2, int Cin, int Cout, int H, int R, int m1, int m2) {
+    const size_t n = (size_t)Cin * Cout * m1 * m2;
+    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= n) return;
+    const int k2 = idx % m2;
+    size_t t = idx / m2;
+    const int j = t % m1;
+    t /= m1;
+    const int o = t % Cout;
+    const int ci = (int)(t / Cout);
+    auto row_of = [&](int k1) { return k1 < m1 ? k1 : k1 - (H - R); };
+    // weights1 row j -> frequency k1 = j, unless the [-m1:] corner covers it
+    float2 g1 = make_float2(0.f, 0.f);
+    if (j < H - m1) g1 = gwp[(((size_t)row_of(j) * m2 + k2) * Cin + ci) * Cout + o];
+    gw1[idx] = g1;
+    const int k1b = H - m1 + j;
+    gw2[idx] = gwp[(((size_t)row_of(k1b) * m2 + k2) * Cin + ci) * Cout + o];
+}
+
 }  // namespace
 
 extern "C" int nps_spectral_dft_w(const nps_src_t* src, int nsrc, int B, int H, int W, int C, int m2, float* X1,
@@ -259,7 +350,7 @@ extern "C" int nps_spectral_dft_w(const nps_src_t* src, int nsrc, int B, int H, 
     const size_t lds = sizeof(float2) * KW_CHUNK * W;
     NPS_CHECK_ARG(lds <= 64 * 1024, "spectral_dft_w: W=%d too large", W);
     const int bs = C >= 256 ? 256 : ((C + 63) / 64) * 64;
-    dft_w_kernel<<<dim3(H, B), bs, lds, (hipStream_t)stream>>>(a, m2, reinterpret_cast<float2*>(X1));
+    dft_w_kernel<<<dim3(H, B), bs, lds, (hipStream_t)stream>>>(a, m2, reinterpret_cast<float2*>(X1), 1.f, 0);
     NPS_CHECK_LAUNCH("spectral_dft_w");
     return 0;
 }
@@ -335,7 +426,77 @@ extern "C" int nps_spectral_idft_w(const float* Z, float* out, int B, int H, int
         attr_set = true;
     }
     idft_w_kernel<<<dim3(H, B), bs, lds, (hipStream_t)stream>>>(reinterpret_cast<const float2*>(Z), out, H, W, m2,
-                                                                Cout, accumulate, addend, act);
+                                                                Cout, accumulate, addend, act,
+                                                                1.0f / ((float)H * (float)W), 1);
     NPS_CHECK_LAUNCH("spectral_idft_w");
+    return 0;
+}
+
+// ---- SpectralConv2d backward (autograd conventions of torch.fft) ----------------
+extern "C" int nps_spectral_idft_w_bwd(const float* gy, float* gZ, int B, int H, int W, int m2, int Cout,
+                                       void* stream) {
+    NPS_CHECK_ARG(gy && gZ && B > 0 && H > 0 && W > 0 && m2 > 0 && m2 <= W / 2 + 1 && Cout > 0,
+                  "spectral_idft_w_bwd: bad args");
+    nps_conv2d_t a = {};
+    a.nsrc = 1;
+    a.src[0].ptr = gy;
+    a.src[0].C = Cout;
+    a.src[0].H = H;
+    a.src[0].W = W;
+    a.Hin = H;
+    a.Win = W;
+    a.Cin = Cout;
+    const size_t lds = sizeof(float2) * KW_CHUNK * W;
+    NPS_CHECK_ARG(lds <= 64 * 1024, "spectral_idft_w_bwd: W=%d too large", W);
+    const int bs = Cout >= 256 ? 256 : ((Cout + 63) / 64) * 64;
+    dft_w_kernel<<<dim3(H, B), bs, lds, (hipStream_t)stream>>>(a, m2, reinterpret_cast<float2*>(gZ),
+                                                               1.0f / ((float)H * (float)W), 1);
+    NPS_CHECK_LAUNCH("spectral_idft_w_bwd");
+    return 0;
+}
+
+extern "C" int nps_spectral_dft_w_bwd(const float* gX1, float* gx, int B, int H, int W, int m2, int Cin,
+                                      void* stream) {
+    NPS_CHECK_ARG(gX1 && gx && B > 0 && H > 0 && W > 0 && m2 > 0 && m2 <= W / 2 + 1 && Cin > 0,
+                  "spectral_dft_w_bwd: bad args");
+    const size_t lds = sizeof(float2) * m2 * W;
+    NPS_CHECK_ARG(lds <= 96 * 1024, "spectral_dft_w_bwd: m2*W too large");
+    const int bs = Cin >= 256 ? 256 : ((Cin + 63) / 64) * 64;
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)idft_w_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+        attr_set = true;
+    }
+    idft_w_kernel<<<dim3(H, B), bs, lds, (hipStream_t)stream>>>(reinterpret_cast<const float2*>(gX1), gx, H, W, m2,
+                                                                Cin, 0, nullptr, 0, 1.0f, 0);
+    NPS_CHECK_LAUNCH("spectral_dft_w_bwd");
+    return 0;
+}
+
+extern "C" int nps_spectral_mix_bwd(const float* X2, const float* wpack, const float* gY, float* gX2, float* gwpack,
+                                    int B, int R, int m2, int Cin, int Cout, void* stream) {
+    NPS_CHECK_ARG(X2 && wpack && gY && gX2 && gwpack && B > 0 && R > 0 && m2 > 0 && Cin > 0 && Cout > 0,
+                  "spectral_mix_bwd: bad args");
+    const size_t lds = sizeof(float2) * B * Cout;
+    NPS_CHECK_ARG(lds <= 64 * 1024, "spectral_mix_bwd: B*Cout=%d too large", B * Cout);
+    const int ychunks = (Cin + 31) / 32;
+    mix_bwd_kernel<<<dim3(R * m2, ychunks), 256, lds, (hipStream_t)stream>>>(
+        reinterpret_cast<const float2*>(X2), reinterpret_cast<const float2*>(wpack),
+        reinterpret_cast<const float2*>(gY), reinterpret_cast<float2*>(gX2), reinterpret_cast<float2*>(gwpack), B,
+        R * m2, Cin, Cout);
+    NPS_CHECK_LAUNCH("spectral_mix_bwd");
+    return 0;
+}
+
+extern "C" int nps_spectral_unpack_grad(const float* gwpack, float* gw1, float* gw2, int Cin, int Cout, int H, int m1,
+                                        int m2, void* stream) {
+    NPS_CHECK_ARG(gwpack && gw1 && gw2 && Cin > 0 && Cout > 0 && m1 > 0 && m1 <= H && m2 > 0,
+                  "spectral_unpack_grad: bad args");
+    const int R = H < 2 * m1 ? H : 2 * m1;
+    const size_t n = (size_t)Cin * Cout * m1 * m2;
+    spec_unpack_grad_kernel<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+        reinterpret_cast<const float2*>(gwpack), reinterpret_cast<float2*>(gw1), reinterpret_cast<float2*>(gw2), Cin,
+        Cout, H, R, m1, m2);
+    NPS_CHECK_LAUNCH("spectral_unpack_grad");
     return 0;
 }

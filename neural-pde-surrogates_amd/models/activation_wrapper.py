@@ -11,6 +11,7 @@ from torch import nn
 
 import models
 from nps_hip import ops
+from nps_hip import autograd as ad
 from utils.attr import getattr_nested
 
 
@@ -50,14 +51,16 @@ def activation_wrapper(model_class: str, activation_final: nn.Module, enforce_sp
                     f"approx_volume_preserve_mode '{approx_volume_preserve_mode}' is not on the MI355X path "
                     "(twophase cfgs use 'individual_static')")
             B, c, tw, H, W = u.shape
-            xc = x.contiguous()
-            new_tot = ops.plane_sums(u, 0, H * W, H * W, B * c * tw)                        # :81
-            prev_tot = ops.plane_sums(xc, (xc.shape[2] - 1) * H * W, xc.shape[2] * H * W, H * W, B * c)  # :84
             key = (float(max_pct_dif), tw, str(u.device))
             if getattr(self, "_mpd_key", None) != key:
                 self._mpd_tab = torch.from_numpy(_mpd_cumsum(max_pct_dif, tw)).to(u.device)
                 self._mpd_key = key
             mask = sc.float().contiguous() if enforce_spatial_cond else None
+            if u.requires_grad:
+                return ad.VolumeRescaleFn.apply(spatial_cond_channel, u, x.detach(), self._mpd_tab, mask)
+            xc = x.contiguous()
+            new_tot = ops.plane_sums(u, 0, H * W, H * W, B * c * tw)                        # :81
+            prev_tot = ops.plane_sums(xc, (xc.shape[2] - 1) * H * W, xc.shape[2] * H * W, H * W, B * c)  # :84
             ops.volume_rescale(u, new_tot, prev_tot, self._mpd_tab, mask, spatial_cond_channel)
         return u
 

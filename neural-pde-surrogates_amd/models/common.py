@@ -11,6 +11,13 @@ import torch
 from torch import nn
 
 from nps_hip import ops
+from nps_hip import autograd as ad
+
+
+def use_autograd(module) -> bool:
+    """True when this forward must be differentiable (training): grad mode on and trainable parameters.
+    The differentiable path runs the same HIP kernels unfused plus their backward kernels (nps_hip.autograd)."""
+    return torch.is_grad_enabled() and any(p.requires_grad for p in module.parameters())
 
 
 class Swish(nn.Module):
@@ -115,6 +122,8 @@ class Conv2d(_PackedMixin, nn.Conv2d):
                           stride=s, dil=d, pad=lo, pad_bottom=hi, circ=circ, **kw)
 
     def forward(self, x):
+        if use_autograd(self):
+            return ad.to_nchw(ad.conv2d(self, ad.to_nhwc(x)))
         x = ops.nchw_to_nhwc(x)
         y = self.run([ops.Src(x)], x.shape[1:3])
         return ops.nhwc_to_nchw(y)
@@ -147,6 +156,8 @@ class ConvTranspose2d(_PackedMixin, nn.ConvTranspose2d):
         return out
 
     def forward(self, x):
+        if use_autograd(self):
+            return ad.to_nchw(ad.conv_transpose2d(self, ad.to_nhwc(x)))
         return ops.nhwc_to_nchw(self.run(ops.nchw_to_nhwc(x)))
 
 

@@ -14,6 +14,7 @@ from torch import nn
 
 from models.base import ModelInterface
 from nps_hip import ops
+from nps_hip import autograd as ad
 from pdes import PDE
 from utils.attr import getattr_nested
 
@@ -104,13 +105,20 @@ class EncProcDec(ModelInterface):
         n_in = self.encoder.n_in
         Cp = ((n_in + 3) // 4) * 4
         xin, vb = ops.pack_grid_input(u, pos.float().contiguous(), variables, sc, Cp)
+        mask = sc if mask_channel is not None else None
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            # training: the same kernels unfused, each with its HIP backward (nps_hip.autograd)
+            h = self.encoder.run_packed_ad(xin)
+            for i, p in enumerate(self.processor):
+                h_next = p.run_ad(h, vb)
+                h = ad.add_at(h_next, h) if (self.processor_residual and i > 0) else h_next
+            return self.decoder.run_ad(h, u, final_tanh=final_tanh, mask=mask, mask_ch=mask_channel or 0)
         h = self.encoder.run_packed(xin)
         for i, p in enumerate(self.processor):
             h_next = p.run(h, vb)
             if self.processor_residual and i > 0:
                 h_next = h_next + h
             h = h_next
-        mask = sc if mask_channel is not None else None
         return self.decoder.run(h, u, final_tanh=final_tanh, mask=mask, mask_ch=mask_channel or 0)
 
     def forward(self, x, cond=None, bc=None, pos=None, t_cond=None, spatial_cond=None):

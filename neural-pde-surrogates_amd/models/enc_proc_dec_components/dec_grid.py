@@ -11,8 +11,9 @@ import numpy as np
 import torch
 from torch import nn
 
-from models.common import get_conv_with_right_spatial_dim, Swish, activation_code
+from models.common import get_conv_with_right_spatial_dim, Swish, activation_code, use_autograd
 from nps_hip import ops
+from nps_hip import autograd as ad
 from pdes import PDE
 
 
@@ -70,7 +71,21 @@ class TimeConvDense(nn.Module):
                                    c2.weight.detach().contiguous(), c2.bias.detach(), self._dtcum(h.device), mask,
                                    mask_ch, final_tanh, self.num_c, self.time_window)
 
+    def run_ad(self, h, u, final_tanh=False, mask=None, mask_ch=0):
+        """Differentiable form of run(): pre-decoder conv, planar transpose, fused conv1d-chain kernel."""
+        if self.dec_delta_mode != 'per_step':
+            raise NotImplementedError("TimeConvDense: dec_delta_mode='per_step' only on the MI355X path")
+        if activation_code(self.decoder[1]) != ops.GELU:
+            raise NotImplementedError("TimeConvDense: GELU activation only")
+        pre = ad.to_nchw(ad.conv2d(self.pre_decoder, h))
+        c1, c2 = self.decoder[0], self.decoder[2]
+        return ad.TimeConvDecodeFn.apply((mask_ch, bool(final_tanh), self.num_c, self.time_window), pre,
+                                         u.contiguous(), c1.weight, c1.bias, c2.weight, c2.bias,
+                                         self._dtcum(h.device), mask)
+
     def forward(self, h: torch.Tensor, u: torch.Tensor, **kwargs):
+        if use_autograd(self):
+            return self.run_ad(ad.to_nhwc(h), u)
         return self.run(ops.nchw_to_nhwc(h), u)
 
 

@@ -2,8 +2,9 @@
 import torch
 from torch import nn
 
-from models.common import get_conv_with_right_spatial_dim, Swish, activation_code
+from models.common import get_conv_with_right_spatial_dim, Swish, activation_code, use_autograd
 from nps_hip import ops
+from nps_hip import autograd as ad
 from pdes import PDE
 
 
@@ -48,6 +49,12 @@ class ElementWise(nn.Module):
         h = c1.run([ops.Src(xin)], (H, W), act=act)
         return c2.run([ops.Src(h)], (H, W), act=act)
 
+    def run_packed_ad(self, xin):
+        """Differentiable form of run_packed (the packed input is data: no gradient flows into it)."""
+        act = activation_code(self.encoder[1])
+        h = ad.act(ad.conv2d(self.encoder[0], xin), act)
+        return ad.act(ad.conv2d(self.encoder[2], h), act)
+
     def forward(self, u: torch.Tensor, pos: torch.Tensor, variables_broadcast: torch.Tensor = None, **kwargs):
         if pos.dim() != 4:
             raise NotImplementedError("ElementWise: 2-D grids only on the MI355X path")
@@ -57,4 +64,6 @@ class ElementWise(nn.Module):
         Cp = ((self.n_in + 3) // 4) * 4
         # the broadcast conditioning is already a spatial field here: pass it as spatial channels
         xin, _ = ops.pack_grid_input(u.contiguous(), pos.contiguous(), None, vb.contiguous() if vb is not None else None, Cp)
+        if use_autograd(self):
+            return ad.to_nchw(self.run_packed_ad(xin))
         return ops.nhwc_to_nchw(self.run_packed(xin))

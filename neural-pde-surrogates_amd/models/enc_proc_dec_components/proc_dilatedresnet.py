@@ -9,8 +9,9 @@ import torch
 from torch import nn
 
 from common.interfaces import D, M
-from models.common import get_conv_with_right_spatial_dim, activation_code
+from models.common import get_conv_with_right_spatial_dim, activation_code, use_autograd
 from nps_hip import ops
+from nps_hip import autograd as ad
 from pdes import PDE
 
 
@@ -39,7 +40,16 @@ class DilatedResnet(nn.Module):
             h = block.run(srcs, residual=h)
         return h
 
+    def run_ad(self, h, vb):
+        for block in self.processor.children():
+            srcs = [ops.Src(h)] + ([ops.Src(vb)] if vb is not None else [])
+            h = ad.add_at(h, block.run_ad(ad.frame(srcs, h.shape[1:3])))
+        return h
+
     def forward(self, h: torch.Tensor, variables_broadcast: torch.Tensor = None, pos=None):
+        if use_autograd(self):
+            vb = ad.to_nhwc(variables_broadcast) if variables_broadcast is not None else None
+            return ad.to_nchw(self.run_ad(ad.to_nhwc(h), vb))
         vb = ops.nchw_to_nhwc(variables_broadcast) if variables_broadcast is not None else None
         return ops.nhwc_to_nchw(self.run(ops.nchw_to_nhwc(h), vb))
 
@@ -80,6 +90,14 @@ class DilatedResnetBlock(nn.Module):
             H, W = y.shape[1:3]
         return y
 
+    def run_ad(self, x):
+        act = activation_code(self.activation)
+        for conv in [m for m in self.layers if not isinstance(m, type(self.activation))]:
+            x = ad.act(ad.conv2d(conv, x), act)
+        return x
+
     def forward(self, x: torch.Tensor):
+        if use_autograd(self):
+            return ad.to_nchw(self.run_ad(ad.to_nhwc(x)))
         x = ops.nchw_to_nhwc(x)
         return ops.nhwc_to_nchw(self.run([ops.Src(x)]))

@@ -9,8 +9,9 @@ import torch
 from torch import nn
 
 from common.interfaces import D, M
-from models.common import get_conv_with_right_spatial_dim, activation_code
+from models.common import get_conv_with_right_spatial_dim, activation_code, use_autograd
 from nps_hip import ops
+from nps_hip import autograd as ad
 from pdes import PDE
 
 
@@ -52,8 +53,19 @@ class FNO(nn.Module):
             h = layer.run(srcs)
         return h
 
+    def run_ad(self, h, vb):
+        if self.cond_mode == "film":
+            raise NotImplementedError("FiLM conditioning is not on the MI355X path (twophase cfgs use concat)")
+        for layer in self.fno_layers:
+            srcs = [ops.Src(h)] + ([ops.Src(vb)] if (vb is not None and self.cond_mode == "concat") else [])
+            h = layer.run_ad(ad.frame(srcs, h.shape[1:3]))
+        return h
+
     def forward(self, h: torch.Tensor, variables: torch.Tensor = None, variables_broadcast: torch.Tensor = None,
                 pos=None):
+        if use_autograd(self):
+            vb = ad.to_nhwc(variables_broadcast) if variables_broadcast is not None else None
+            return ad.to_nchw(self.run_ad(ad.to_nhwc(h), vb))
         vb = ops.nchw_to_nhwc(variables_broadcast) if variables_broadcast is not None else None
         return ops.nhwc_to_nchw(self.run(ops.nchw_to_nhwc(h), vb))
 
@@ -113,7 +125,19 @@ class FNO_Layer(nn.Module):
             self.w2.run(srcs, (H, W), out=out, accumulate=True)
         return self.conv.run(srcs, out=out, accumulate=True, act=act)
 
+    def run_ad(self, x):
+        """Differentiable form: x (B,H,W,Cin) materialised frame."""
+        if self.num_spatial_dims != 2:
+            raise NotImplementedError("FNO_Layer: 2-D only on the MI355X path")
+        self._check_modes(x.shape[1:3])
+        y = ad.add_at(ad.spectral_conv2d(self.conv, x), ad.conv2d(self.w, x))
+        if self.conv_mode == "double":
+            y = ad.add_at(y, ad.conv2d(self.w2, x))
+        return ad.act(y, activation_code(self.act))
+
     def forward(self, x, p=None):
+        if use_autograd(self):
+            return ad.to_nchw(self.run_ad(ad.to_nhwc(x)))
         x = ops.nchw_to_nhwc(x)
         return ops.nhwc_to_nchw(self.run([ops.Src(x)]))
 
@@ -155,6 +179,14 @@ class SpectralConv2d(nn.Module):
                                    accumulate=accumulate, addend=addend, act=act)
 
     def forward(self, x, p=None):
+        if self.feature_transform:
+            raise NotImplementedError("FiLM spectral conditioning is not on the MI355X path")
+        if use_autograd(self):
+            x = ad.to_nhwc(x)
+            H, W = x.shape[1:3]
+            if not (self.modes1 <= H and self.modes2 <= W // 2 + 1):
+                raise AssertionError("modes should be at most the spatial dim (// 2 + 1 for the last spatial dimension)")
+            return ad.to_nchw(ad.spectral_conv2d(self, x))
         x = ops.nchw_to_nhwc(x)
         return ops.nhwc_to_nchw(self.run([ops.Src(x)]))
 

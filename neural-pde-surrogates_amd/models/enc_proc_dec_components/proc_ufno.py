@@ -11,10 +11,11 @@ import torch
 from torch import nn
 
 from common.interfaces import D, M
-from models.common import activation_code
+from models.common import activation_code, use_autograd
 from models.enc_proc_dec_components.proc_fno import FNO_Layer
 from models.enc_proc_dec_components.proc_unet_modern import UNetModern
 from nps_hip import ops
+from nps_hip import autograd as ad
 from pdes import PDE
 
 
@@ -67,7 +68,21 @@ class UFNO(nn.Module):
             h = unet.run(h, vb, addend=h_fno, act_after=act)
         return h
 
+    def run_ad(self, h, vb):
+        """Differentiable form of run() (training)."""
+        if self.cond_mode != "concat":
+            raise NotImplementedError("U-FNO: only cond_mode='concat' runs on the MI355X path")
+        act = activation_code(self.activation)
+        for fno, unet in zip(self.fno_layers, self.unet_layers):
+            srcs = [ops.Src(h)] + ([ops.Src(vb)] if vb is not None else [])
+            h_fno = fno.run_ad(ad.frame(srcs, h.shape[1:3]))
+            h = ad.act(ad.add_at(h_fno, unet.run_ad(h, vb)), act)
+        return h
+
     def forward(self, h: torch.Tensor, variables: torch.Tensor = None, variables_broadcast: torch.Tensor = None,
                 pos=None):
+        if use_autograd(self):
+            vb = ad.to_nhwc(variables_broadcast) if variables_broadcast is not None else None
+            return ad.to_nchw(self.run_ad(ad.to_nhwc(h), vb))
         vb = ops.nchw_to_nhwc(variables_broadcast) if variables_broadcast is not None else None
         return ops.nhwc_to_nchw(self.run(ops.nchw_to_nhwc(h), vb))

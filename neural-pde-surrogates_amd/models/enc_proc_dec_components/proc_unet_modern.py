@@ -17,8 +17,9 @@ from torch import nn
 
 from common.interfaces import D, M
 from models.common import (get_conv_with_right_spatial_dim, get_upconv_with_right_spatial_dim, crop_offsets,
-                           activation_code)
+                           activation_code, use_autograd)
 from nps_hip import ops
+from nps_hip import autograd as ad
 from pdes import PDE
 
 
@@ -131,6 +132,41 @@ class UNetModern(nn.Module):
                        out_off=(oy, ox), addends=[addend] if addend is not None else [], act=act_after)
         return out
 
+    def run_ad(self, h, vb):
+        """Differentiable NHWC forward (training): proc_unet_modern.py:169-196 as unfused HIP ops."""
+        if self.num_spatial_dims != 2:
+            raise NotImplementedError("UNetModern: 2-D only on the MI355X path")
+        if self.n_cond > 0 and vb is None:
+            raise ValueError("UNetModern with n_cond > 0 needs variables_broadcast")
+        if self.n_cond == 0:
+            vb = None
+        h_shape = h.shape
+        feats, vbs = [h], [vb]
+        for m in self.down:
+            if isinstance(m, Downsample):
+                h, vb = m.run_ad(h, vb)
+            else:
+                h = m.run_ad(h, vb)
+            feats.append(h)
+            vbs.append(vb)
+        h = self.middle.run_ad(h, vb)
+        for m in self.up:
+            if isinstance(m, Upsample):
+                h = ad.conv_transpose2d(m.conv, h)
+            else:
+                _check_no_attn(m)
+                s = feats.pop()
+                v = vbs.pop()
+                H, W = h.shape[1:3]
+                srcs = [ops.Src(h), ops.Src(s, *crop_offsets(s.shape[1:3], (H, W)))]
+                if v is not None:
+                    srcs.append(ops.Src(v, *crop_offsets(v.shape[1:3], (H, W))))
+                h = m.res.run_ad(srcs, (H, W))
+        H, W = h.shape[1:3]
+        norm = self.norm if isinstance(self.norm, nn.GroupNorm) else None
+        y = ad.conv2d(self.final, ad.frame([ops.Src(h)], (H, W), norm, activation_code(self.activation)))
+        return ad.crop(y, h_shape[1:3], crop_offsets(y.shape[1:3], h_shape[1:3]))
+
     def final_out_hw(self, H, W):
         KH, KW, s, d, lo, hi, circ = self.final.geometry()
         return ((H + 2 * circ + lo[0] + hi[0] - d * (KH - 1) - 1) // s + 1,
@@ -138,6 +174,9 @@ class UNetModern(nn.Module):
 
     def forward(self, h: torch.Tensor, variables_broadcast: torch.Tensor = None, pos=None):
         assert h.dim() == 2 + self.num_spatial_dims
+        if use_autograd(self):
+            vb = ad.to_nhwc(variables_broadcast) if variables_broadcast is not None else None
+            return ad.to_nchw(self.run_ad(ad.to_nhwc(h), vb))
         vb = ops.nchw_to_nhwc(variables_broadcast) if variables_broadcast is not None else None
         return ops.nhwc_to_nchw(self.run(ops.nchw_to_nhwc(h), vb))
 
@@ -191,7 +230,26 @@ class ResidualBlock(nn.Module):
         self.conv2.run([ops.Src(h1)], (H1, W1), gn=gn2, pre_act=act, out=out, out_off=(oy, ox), accumulate=True)
         return out
 
+    def run_ad(self, srcs, frame_hw):
+        """Differentiable form of run(): frame -> GN+GELU -> conv1 -> GN+GELU -> conv2, + shortcut."""
+        act = activation_code(self.activation)
+        H, W = frame_hw
+        n1 = self.norm1 if isinstance(self.norm1, nn.GroupNorm) else None
+        n2 = self.norm2 if isinstance(self.norm2, nn.GroupNorm) else None
+        h1 = ad.conv2d(self.conv1, ad.frame(srcs, (H, W), n1, act))
+        if isinstance(self.shortcut, nn.Identity):
+            if len(srcs) != 1 or srcs[0].off_y or srcs[0].off_x or tuple(srcs[0].t.shape[1:3]) != (H, W):
+                raise RuntimeError("identity shortcut on a concatenated input")
+            sc = srcs[0].t
+        else:
+            sc = ad.conv2d(self.shortcut, ad.frame(srcs, (H, W)))
+        h2 = ad.conv2d(self.conv2, ad.frame([ops.Src(h1)], h1.shape[1:3], n2, act))
+        return ad.add_at(sc, h2, crop_offsets(h2.shape[1:3], sc.shape[1:3]))
+
     def forward(self, x: torch.Tensor):
+        if use_autograd(self):
+            x = ad.to_nhwc(x)
+            return ad.to_nchw(self.run_ad([ops.Src(x)], x.shape[1:3]))
         x = ops.nchw_to_nhwc(x)
         return ops.nhwc_to_nchw(self.run([ops.Src(x)], x.shape[1:3]))
 
@@ -240,7 +298,15 @@ class DownBlock(nn.Module):
         srcs = [ops.Src(x)] + ([ops.Src(vb)] if vb is not None else [])
         return self.res.run(srcs, x.shape[1:3])
 
+    def run_ad(self, x, vb):
+        _check_no_attn(self)
+        srcs = [ops.Src(x)] + ([ops.Src(vb)] if vb is not None else [])
+        return self.res.run_ad(srcs, x.shape[1:3])
+
     def forward(self, x: torch.Tensor, variables_broadcast: torch.Tensor = None):
+        if use_autograd(self):
+            vb = ad.to_nhwc(variables_broadcast) if variables_broadcast is not None else None
+            return ad.to_nchw(self.run_ad(ad.to_nhwc(x), vb)), variables_broadcast
         vb = ops.nchw_to_nhwc(variables_broadcast) if variables_broadcast is not None else None
         return ops.nhwc_to_nchw(self.run(ops.nchw_to_nhwc(x), vb)), variables_broadcast
 
@@ -257,6 +323,9 @@ class UpBlock(nn.Module):
 
     def forward(self, x: torch.Tensor):
         _check_no_attn(self)
+        if use_autograd(self):
+            x = ad.to_nhwc(x)
+            return ad.to_nchw(self.res.run_ad([ops.Src(x)], x.shape[1:3]))
         x = ops.nchw_to_nhwc(x)
         return ops.nhwc_to_nchw(self.res.run([ops.Src(x)], x.shape[1:3]))
 
@@ -279,7 +348,16 @@ class MiddleBlock(nn.Module):
         h = self.res1.run(srcs, x.shape[1:3])
         return self.res2.run([ops.Src(h)], h.shape[1:3])
 
+    def run_ad(self, x, vb):
+        _check_no_attn(self)
+        srcs = [ops.Src(x)] + ([ops.Src(vb)] if vb is not None else [])
+        h = self.res1.run_ad(srcs, x.shape[1:3])
+        return self.res2.run_ad([ops.Src(h)], h.shape[1:3])
+
     def forward(self, x: torch.Tensor, variables_broadcast: torch.Tensor = None):
+        if use_autograd(self):
+            vb = ad.to_nhwc(variables_broadcast) if variables_broadcast is not None else None
+            return ad.to_nchw(self.run_ad(ad.to_nhwc(x), vb)), variables_broadcast
         vb = ops.nchw_to_nhwc(variables_broadcast) if variables_broadcast is not None else None
         return ops.nhwc_to_nchw(self.run(ops.nchw_to_nhwc(x), vb)), variables_broadcast
 
@@ -314,7 +392,18 @@ class Downsample(nn.Module):
             vb = self.conv_variables_broadcast.run([ops.Src(vb)], vb.shape[1:3])
         return h, vb
 
+    def run_ad(self, x, vb):
+        h = ad.conv2d(self.conv, x)
+        if vb is not None:
+            vb = ad.conv2d(self.conv_variables_broadcast, vb)
+        return h, vb
+
     def forward(self, x: torch.Tensor, variables_broadcast: torch.Tensor = None):
+        if use_autograd(self):
+            if variables_broadcast is not None:
+                h, v = self.run_ad(ad.to_nhwc(x), ad.to_nhwc(variables_broadcast))
+                return ad.to_nchw(h), ad.to_nchw(v)
+            return self.conv(x)
         if variables_broadcast is not None:
             h, v = self.run(ops.nchw_to_nhwc(x), ops.nchw_to_nhwc(variables_broadcast))
             return ops.nhwc_to_nchw(h), ops.nhwc_to_nchw(v)

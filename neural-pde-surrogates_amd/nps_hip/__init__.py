@@ -13,7 +13,7 @@ import os
 
 import torch
 
-__all__ = ["lib", "Src", "Conv2dArgs", "check", "stream_ptr", "ptr", "LIB_PATH"]
+__all__ = ["lib", "Src", "Conv2dArgs", "WgradArgs", "check", "stream_ptr", "ptr", "LIB_PATH"]
 
 LIB_PATH = os.environ.get("NPS_HIP_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "libnps_hip.so"))
 if not os.path.exists(LIB_PATH):
@@ -49,6 +49,15 @@ class Conv2dArgs(ctypes.Structure):
     ]
 
 
+class WgradArgs(ctypes.Structure):
+    _fields_ = [
+        ("a", ctypes.c_void_p), ("B", ctypes.c_int), ("Ha", ctypes.c_int), ("Wa", ctypes.c_int), ("M", ctypes.c_int),
+        ("x", ctypes.c_void_p), ("Hx", ctypes.c_int), ("Wx", ctypes.c_int), ("N", ctypes.c_int),
+        ("KH", ctypes.c_int), ("KW", ctypes.c_int), ("dil", ctypes.c_int), ("pad_y", ctypes.c_int),
+        ("pad_x", ctypes.c_int), ("circ", ctypes.c_int), ("g", ctypes.c_void_p),
+    ]
+
+
 _vp, _i, _l, _sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_size_t
 _SIGS = {
     "nps_conv2d_packed_size": (_sz, [_i, _i, _i]),
@@ -72,6 +81,25 @@ _SIGS = {
     "nps_sq_err_sum": (_i, [_vp, _vp, _l, _vp, _vp]),
     "nps_nchw_to_nhwc": (_i, [_vp, _vp, _i, _i, _i, _i, _vp]),
     "nps_nhwc_to_nchw": (_i, [_vp, _vp, _i, _i, _i, _i, _vp]),
+    # backward (training)
+    "nps_wgrad_lds_bytes": (_sz, [_i, _i]),
+    "nps_conv2d_wgrad": (_i, [ctypes.POINTER(WgradArgs), _vp]),
+    "nps_channel_sums": (_i, [_vp, _l, _i, _vp, _vp]),
+    "nps_frame_pack_bwd": (_i, [ctypes.POINTER(Conv2dArgs), _vp, ctypes.POINTER(ctypes.c_void_p), _vp, _vp, _vp, _vp]),
+    "nps_gelu": (_i, [_vp, _vp, _l, _vp]),
+    "nps_gelu_bwd": (_i, [_vp, _vp, _vp, _l, _vp]),
+    "nps_add_at": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp]),
+    "nps_circular_pad": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp]),
+    "nps_circular_fold": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp]),
+    "nps_scaled_diff": (_i, [_vp, _vp, _vp, _vp, _l, _vp]),
+    "nps_spectral_idft_w_bwd": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp]),
+    "nps_spectral_dft_w_bwd": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp]),
+    "nps_spectral_mix_bwd": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _vp]),
+    "nps_spectral_unpack_grad": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _vp]),
+    "nps_timeconv_decode_bwd": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp, _vp, _i, _i, _i, _i,
+                                     _i, _i, _vp]),
+    "nps_plane_dot": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp]),
+    "nps_volume_rescale_bwd": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp, _i, _i, _i, _i, _i, _vp]),
     "nps_last_error": (ctypes.c_char_p, []),
     "nps_version": (ctypes.c_char_p, []),
 }

@@ -3,10 +3,16 @@
 `simulate` keeps the reference's signature, loop bounds (:354-358), loss
 normalisation (:422, :433-434) and return conventions, with the trajectory
 resident on the device (windows are views, no per-step host copies) and the
-MSE_sum criterion computed by a HIP fp64 reduction.  Grid models only.
+MSE_sum criterion computed by a HIP fp64 reduction.  `train_step` /
+`train_one_epoch` are the pushforward training loop (:43-163,
+trainers/base.py:472-507) whose backward runs the HIP backward kernels
+(nps_hip.autograd); with a `grad_sync` (trainers.distributed.GradAllReducer)
+the gradients are all-reduced over RCCL between backward and optimizer step.
+Grid models only.
 """
 import argparse
 import math
+import random
 from typing import Tuple
 
 import torch
@@ -14,6 +20,7 @@ from torch import nn
 
 from common.interfaces import D, M
 from nps_hip import ops
+from nps_hip import autograd as ad
 
 
 class DataCreator:
@@ -56,8 +63,12 @@ class AutoregressivePushforwardTrainer:
     model_interface = [M.AR_TB, M.AR_TB_GNN]
 
     def __init__(self, model, data, criterion, optimizer=None, lr_scheduler=None, config: argparse.Namespace = None,
-                 save_path: str = "models/model.pt", **kwargs):
+                 save_path: str = "models/model.pt", max_train_batches=float("inf"), epoch_callback=None,
+                 grad_sync=None, **kwargs):
         self.model = model
+        self.max_train_batches = max_train_batches
+        self.epoch_callback = epoch_callback
+        self.grad_sync = grad_sync
         self.data = data
         self.config = config if config is not None else argparse.Namespace(**kwargs)
         self.config.save_path = save_path
@@ -76,6 +87,78 @@ class AutoregressivePushforwardTrainer:
         if isinstance(c, nn.MSELoss) and c.reduction == "sum":
             return ops.sq_err_sum(pred, labels)
         return c(pred, labels)
+
+    def _train_loss(self, pred, labels):
+        """torch.sqrt(criterion(pred, labels)) (:158-162); MSELoss(sum) runs as a HIP fp64 reduction with a
+        HIP backward."""
+        c = self.criterion
+        if isinstance(c, nn.MSELoss) and c.reduction == "sum":
+            return ad.sqrt_mse_sum(pred, labels)
+        return torch.sqrt(c(pred, labels))
+
+    def train_step(self, batch: Tuple, epoch, batch_idx, loader=None):
+        """Pushforward training step, autoregressivepushforwardtrainer.py:43-163 (grid models, static time):
+        a random unroll depth (<= min(epoch // lr_step_interval, unrolling)) of no-grad model calls from
+        random start steps per sample, then one model call with grad; loss = sqrt(MSE_sum)."""
+        batch_size = self.config.batch_size
+        device = self.config.device
+        if self.data.data_interface == D.sim1d_var_t:
+            raise NotImplementedError("variable-length time (sim1d_var_t) is not on the grid path")
+        if self.model.model_interface != M.AR_TB:
+            raise NotImplementedError("graph (GNN) models are not on the MI355X path")
+        u_base, u_super, x, conditioning, t_conditioning, spatial_conditioning = batch
+        t_res = self.data_creator.t_res
+        use_t_conditioning = torch.numel(t_conditioning) != 0
+        if torch.numel(spatial_conditioning) == 0:
+            spatial_conditioning = None
+        unrolling_epoch = epoch // self.config.lr_step_interval                       # :78-82
+        max_unrolling = min(unrolling_epoch, self.config.unrolling)
+        unrolled_graphs = random.choice(list(range(max_unrolling + 1)))
+        steps = [t for t in range(self.data_creator.tw,
+                                  t_res - self.data_creator.tw - (self.data_creator.tw * unrolled_graphs) + 1)]
+        random_steps = random.choices(steps, k=batch_size)                             # :95
+        data, labels = self.data_creator.create_data(u_super, random_steps)
+        data, labels = data.to(device), labels.to(device)
+        t_cond = self.data_creator.create_data(t_conditioning, random_steps, mode="labels") \
+            if use_t_conditioning else None
+        with torch.no_grad():                                                          # :115-144
+            for _ in range(unrolled_graphs):
+                data = self.model(data, cond=conditioning, bc=None, pos=x, t_cond=t_cond,
+                                  spatial_cond=spatial_conditioning)
+                random_steps = [rs + self.data_creator.tw for rs in random_steps]
+                _, labels = self.data_creator.create_data(u_super, random_steps)
+                labels = labels.to(device)
+                t_cond = self.data_creator.create_data(t_conditioning, random_steps, mode="labels") \
+                    if use_t_conditioning else None
+        pred = self.model(data, cond=conditioning, bc=None, pos=x, t_cond=t_cond,     # :150
+                          spatial_cond=spatial_conditioning)
+        loss = self._train_loss(pred, labels)
+        return loss, pred
+
+    def train_one_epoch(self, loader, epoch) -> float:
+        """trainers/base.py:472-507: zero_grad -> train_step -> backward -> [RCCL all-reduce] -> step."""
+        self.model.train()
+        device = self.config.device
+        total_loss = 0
+        n = 0
+        for batch_idx, batch in enumerate(loader):
+            batch_on_device = tuple(t.to(device) if isinstance(t, torch.Tensor) else t for t in batch)
+            self.optimizer.zero_grad()
+            loss, preds = self.train_step(batch_on_device, epoch, batch_idx, loader=loader)
+            loss.backward()
+            if self.grad_sync is not None:
+                self.grad_sync.finish()
+            self.optimizer.step()
+            total_loss += loss.detach() / batch_on_device[0].shape[0]
+            n += 1
+            if batch_idx >= self.max_train_batches:
+                break
+        total_loss = total_loss / max(1, n)
+        if self.epoch_callback is not None:
+            self.epoch_callback(self, loader, epoch)
+        if self.lr_scheduler is not None and (epoch + 1) % self.config.lr_step_interval == 0:
+            self.lr_scheduler.step()
+        return total_loss
 
     def simulate(self, u, conditioning, x, compute_loss, include_data, nr_gt_steps, t_res,
                  t_conditioning=torch.empty(0), spatial_conditioning=torch.empty(0), clip_min=True, use_bc=True,

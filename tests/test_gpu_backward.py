@@ -1,0 +1,326 @@
+"""GPU parity of the backward (training) path: HIP gradients vs autograd through the CPU oracle and the
+reference's own golden gradients.
+
+Every gradient here is produced by libnps_hip.so kernels (nps_hip.autograd): conv input gradients as
+forward convs of dy, weight gradients on the MFMA wgrad kernel, GroupNorm/GELU frame backward,
+spectral-conv backward, TimeConvDense / volume-rescale backward.  Tolerance: fp32 rel-L2 < 1e-5 per
+gradient tensor (BASELINE.json north star), measured 1e-7 ... 1e-6.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+import oracle
+from oracle import functional as Fo
+from conftest import load_golden, rel_l2
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+DEV = "cuda"
+
+
+def _grads_ok(named_ref, named_got, tol=TOL, tensor_tol=1e-4):
+    """All parameter gradients as one vector: rel-L2 < tol (1e-5).  Per tensor: rel-L2 < tensor_tol, or an
+    error below tol x the norm of the whole gradient — bias / GroupNorm-affine gradients are sums over every
+    pixel that largely cancel (fp32 noise of such a sum is ~eps x the cancellation factor, on the CPU
+    reference as much as here), and a bias feeding a per-channel GroupNorm (e.g. the last UpBlock's
+    shortcut bias before GroupNorm(8, 8)) has an analytically zero gradient that both sides only resolve
+    to rounding noise."""
+    keys = list(named_ref)
+    for k in keys:
+        assert named_got[k] is not None, f"no gradient for {k}"
+    ref = torch.cat([torch.view_as_real(named_ref[k]).reshape(-1) if named_ref[k].is_complex()
+                     else named_ref[k].reshape(-1) for k in keys]).double()
+    got = torch.cat([(torch.view_as_real(named_got[k]) if named_got[k].is_complex() else named_got[k])
+                     .reshape(-1).cpu() for k in keys]).double()
+    e_all = (torch.linalg.vector_norm(got - ref) / torch.linalg.vector_norm(ref)).item()
+    total = torch.linalg.vector_norm(ref).item()
+    bad = []
+    for k in keys:
+        r = named_ref[k].detach().cpu()
+        g = named_got[k].detach().cpu()
+        if r.is_complex():
+            r, g = torch.view_as_real(r), torch.view_as_real(g)
+        r, g = r.double(), g.double()
+        d = torch.linalg.vector_norm(g - r).item()
+        e = d / max(torch.linalg.vector_norm(r).item(), 1e-30)
+        if not (e < tensor_tol or d < tol * total):
+            bad.append((k, e, d / total))
+    assert e_all < tol and not bad, (e_all, bad)
+
+
+# ------------------------------------------------------------------ conv
+CONV_CASES = [
+    # (Cin, Cout, k, stride, dil, padding, padding_mode, H, W)
+    (16, 64, 3, 1, 1, 0, "zeros", 20, 20),          # valid 3x3 (U-Net)
+    (196, 192, 3, 1, 1, 0, "zeros", 33, 35),        # U-FNO shape, chunk tails
+    (7, 5, 3, 1, 1, 1, "zeros", 17, 13),            # 'ones' zero pad, odd channels
+    (12, 12, 3, 2, 1, 0, "zeros", 31, 29),          # Downsample s2 valid, odd size
+    (12, 40, 3, 2, 1, 1, "zeros", 16, 16),          # Downsample s2 pad 1
+    (2, 2, 3, 2, 1, 0, "zeros", 21, 22),            # vb Downsample, C % 4 != 0
+    (8, 8, 5, 1, 2, "same", "circular", 24, 24),    # DRN dilated circular
+    (8, 8, 5, 1, 8, "same", "circular", 20, 20),
+    (132, 128, 5, 1, 4, "same", "circular", 40, 36),
+    (81, 192, 1, 1, 1, 0, "zeros", 19, 23),         # encoder 1x1, Cin % 4 != 0
+    (192, 75, 1, 1, 1, 0, "zeros", 16, 16),         # pre-decoder 1x1
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv2d_backward_vs_torch(case):
+    from models.common import Conv2d
+    Cin, Cout, k, s, d, p, pm, H, W = case
+    torch.manual_seed(0)
+    m = Conv2d(Cin, Cout, k, stride=s, dilation=d, padding=p, padding_mode=pm)
+    x = torch.randn(2, Cin, H, W)
+    w = m.weight.detach().clone().requires_grad_(True)
+    b = m.bias.detach().clone().requires_grad_(True)
+    xr = x.clone().requires_grad_(True)
+    ref = Fo.conv2d_ref(xr, {"weight": w, "bias": b}, "", stride=s, padding=p, dilation=d, padding_mode=pm)
+    g = torch.randn_like(ref)
+    ref.backward(g)
+    m = m.to(DEV)
+    xd = x.to(DEV).requires_grad_(True)
+    y = m(xd)
+    assert y.shape == ref.shape
+    y.backward(g.to(DEV))
+    assert rel_l2(y, ref) < TOL
+    assert rel_l2(xd.grad, xr.grad) < TOL
+    assert rel_l2(m.weight.grad, w.grad) < TOL
+    assert rel_l2(m.bias.grad, b.grad) < TOL
+
+
+@pytest.mark.parametrize("circ", [True, False])
+def test_conv_transpose_backward_vs_torch(circ):
+    from models.common import ConvTranspose2d, ConvTranspose2d_padded
+    torch.manual_seed(0)
+    m = ConvTranspose2d_padded(1, 24, 20, kernel_size=4, stride=2) if circ else \
+        ConvTranspose2d(24, 20, kernel_size=4, stride=2, padding=1)
+    x = torch.randn(2, 24, 13, 11)
+    sd = {"weight": m.weight.detach().clone().requires_grad_(True),
+          "bias": m.bias.detach().clone().requires_grad_(True)}
+    xr = x.clone().requires_grad_(True)
+    ref = Fo.conv_transpose_ref(xr, sd, "", stride=2, padding=0 if circ else 1, circ_pre_pad=1 if circ else 0)
+    g = torch.randn_like(ref)
+    ref.backward(g)
+    m = m.to(DEV)
+    xd = x.to(DEV).requires_grad_(True)
+    y = m(xd)
+    y.backward(g.to(DEV))
+    assert rel_l2(y, ref) < TOL
+    assert rel_l2(xd.grad, xr.grad) < TOL
+    assert rel_l2(m.weight.grad, sd["weight"].grad) < TOL
+    assert rel_l2(m.bias.grad, sd["bias"].grad) < TOL
+
+
+def test_residual_block_backward_concat_crop_groupnorm():
+    """cat(h, crop(s), crop(vb)) -> GN(1)+GELU -> conv1 -> GN+GELU -> conv2, + crop-padded 1x1 shortcut."""
+    from models.enc_proc_dec_components.proc_unet_modern import ResidualBlock
+    from nps_hip import ops
+    from nps_hip import autograd as ad
+    torch.manual_seed(0)
+    rb = ResidualBlock(20 + 16 + 4, 16, activation=nn.GELU(), norm=True, num_spatial_dims=2,
+                       padding_kwargs=dict(padding_mode="circular"))
+    with torch.no_grad():
+        for n in (rb.norm1, rb.norm2):
+            n.weight.uniform_(0.5, 1.5)
+            n.bias.uniform_(-0.3, 0.3)
+    h, s, v = torch.randn(2, 20, 30, 30), torch.randn(2, 16, 27, 27), torch.rand(2, 4, 33, 33)
+    sd = {k: t.detach().clone().requires_grad_(True) for k, t in rb.state_dict().items()}
+    hr, sr, vr = (t.clone().requires_grad_(True) for t in (h, s, v))
+    x = torch.cat([hr, Fo.crop_nd(sr, h.shape), Fo.crop_nd(vr, h.shape)], dim=1)
+    ref = Fo.residual_block(sd, "", x, True, dict(padding_mode="circular"))
+    g = torch.randn_like(ref)
+    ref.backward(g)
+    rb = rb.to(DEV)
+    hd, sdd, vd = (ops.nchw_to_nhwc(t.to(DEV)).requires_grad_(True) for t in (h, s, v))
+    srcs = [ops.Src(hd), ops.Src(sdd, ops.crop_offset(27, 30), ops.crop_offset(27, 30)),
+            ops.Src(vd, ops.crop_offset(33, 30), ops.crop_offset(33, 30))]
+    y = rb.run_ad(srcs, (30, 30))
+    y.backward(ops.nchw_to_nhwc(g.to(DEV)))
+    assert rel_l2(ops.nhwc_to_nchw(y.detach()), ref) < TOL
+    for got, want in ((hd, hr), (sdd, sr), (vd, vr)):
+        assert rel_l2(ops.nhwc_to_nchw(got.grad), want.grad) < TOL
+    _grads_ok({k: t.grad for k, t in sd.items()}, dict((k, p.grad) for k, p in rb.named_parameters()))
+
+
+# ------------------------------------------------------------------ spectral
+@pytest.mark.parametrize("name", ["spectral2d_a", "spectral2d_overlap", "spectral2d_nyq"])
+def test_spectral2d_backward_golden(name):
+    """dx, dweights1, dweights2 vs the reference's own autograd (torch.fft + complex einsum)."""
+    from models.enc_proc_dec_components.proc_fno import SpectralConv2d
+    g = load_golden(name)
+    kw = g["kwargs"]
+    m = SpectralConv2d(kw["in_channels"], kw["out_channels"], tuple(kw["modes"]))
+    m.load_state_dict(g["state_dict"])
+    m = m.to(DEV)
+    x = g["x"].to(DEV).requires_grad_(True)
+    y = m(x)
+    y.backward(g["g"].to(DEV))
+    assert rel_l2(y, g["y"]) < TOL
+    assert rel_l2(x.grad, g["dx"]) < TOL
+    assert rel_l2(m.weights1.grad, g["dw1"]) < TOL
+    assert rel_l2(m.weights2.grad, g["dw2"]) < TOL
+
+
+@pytest.mark.parametrize("H,W,m", [(64, 64, 12), (96, 64, 10)])
+def test_spectral2d_backward_full_channels(H, W, m):
+    from models.enc_proc_dec_components.proc_fno import SpectralConv2d
+    torch.manual_seed(1)
+    sc = SpectralConv2d(196, 192, (m, m))
+    x = torch.randn(2, 196, H, W)
+    w1 = sc.weights1.detach().clone().requires_grad_(True)
+    w2 = sc.weights2.detach().clone().requires_grad_(True)
+    xr = x.clone().requires_grad_(True)
+    ref = Fo.spectral_conv2d(xr, w1, w2)
+    g = torch.randn_like(ref)
+    ref.backward(g)
+    sc = sc.to(DEV)
+    xd = x.to(DEV).requires_grad_(True)
+    sc(xd).backward(g.to(DEV))
+    assert rel_l2(xd.grad, xr.grad) < TOL
+    assert rel_l2(sc.weights1.grad, w1.grad) < TOL
+    assert rel_l2(sc.weights2.grad, w2.grad) < TOL
+
+
+# ------------------------------------------------------------------ processors
+def _proc(name):
+    from models.enc_proc_dec_components import UNetModern, DilatedResnet, UFNO, FNO
+    cls = {"unet_ufno_style": UNetModern, "unet_cfg": UNetModern, "unet_ones": UNetModern, "drn": DilatedResnet,
+           "ufno": UFNO, "fno": FNO}[name]
+    g = load_golden(name)
+    kw = dict(g["kwargs"])
+    if cls is not FNO:
+        kw["activation"] = nn.GELU()
+    m = cls(pde=None, **kw)
+    m.load_state_dict(g["state_dict"])
+    return m, g, cls
+
+
+_ORACLE_PROC = {"unet_ufno_style": Fo.unet_modern, "unet_cfg": Fo.unet_modern, "unet_ones": Fo.unet_modern,
+                "drn": Fo.dilated_resnet, "ufno": Fo.ufno, "fno": Fo.fno}
+
+
+@pytest.mark.parametrize("name", ["unet_ufno_style", "unet_cfg", "unet_ones", "drn", "ufno", "fno"])
+def test_processor_backward_vs_oracle(name):
+    m, g, _ = _proc(name)
+    sd = {k: t.detach().clone().requires_grad_(True) for k, t in m.state_dict().items()}
+    hr = g["h"].clone().requires_grad_(True)
+    vr = g["vb"].clone().requires_grad_(True)
+    cfg = dict(g["kwargs"])
+    ref = _ORACLE_PROC[name](sd, "", cfg, hr, vr)
+    torch.manual_seed(3)
+    gy = torch.randn_like(ref)
+    ref.backward(gy)
+    m = m.to(DEV)
+    hd = g["h"].to(DEV).requires_grad_(True)
+    vd = g["vb"].to(DEV).requires_grad_(True)
+    y = m(h=hd, variables_broadcast=vd)
+    y.backward(gy.to(DEV))
+    assert rel_l2(y, g["y"]) < TOL
+    assert rel_l2(hd.grad, hr.grad) < TOL
+    assert rel_l2(vd.grad, vr.grad) < TOL
+    _grads_ok({k: t.grad for k, t in sd.items() if t.grad is not None},
+              {k: p.grad for k, p in m.named_parameters()})
+
+
+# ------------------------------------------------------------------ full model training loss
+def _build_model(g):
+    import models
+    from pdes import PDE2D
+    cfg = dict(g["cfg"])
+    cfg.pop("object")
+    cfg["activation"] = nn.GELU()
+    cfg["activation_final"] = nn.Tanh()
+    p = g["pde"]
+    pde = PDE2D(tmin=p["tmin"], tmax=p["tmax"], nt=p["nt"], L1=1.0, L2=1.0, nx1=p["nx1"], nx2=p["nx2"], x=None,
+                name="twophase", n_cond_static=p["n_cond_static"], n_cond_spatial=p["n_cond_spatial"])
+    m = models.activation_wrapper(**cfg, pde=pde)
+    m.load_state_dict(g["state_dict"])
+    return m, pde
+
+
+@pytest.mark.parametrize("name", ["model_ufno", "model_unet", "model_drn", "model_ufno_fno"])
+def test_model_train_loss_grads_vs_oracle(name):
+    """loss = sqrt(MSE_sum(model(x), labels)) (autoregressivepushforwardtrainer.py:158-162) and every
+    parameter gradient, vs autograd through the oracle on the same state_dict."""
+    from nps_hip import autograd as ad
+    g = load_golden(name)
+    m, pde = _build_model(g)
+    tw = g["cfg"]["time_window"]
+    u, cond, pos, sc = g["u"], g["cond"], g["pos"], g["spatial_cond"]
+    x, labels = u[:, :, :tw], u[:, :, tw:2 * tw]
+    om = oracle.build_oracle_model({k: v for k, v in g["cfg"].items() if k != "object"}, g["pde"], g["state_dict"])
+    om.sd = {k: v.detach().clone().requires_grad_(True) for k, v in om.sd.items()}
+    ref_pred = om(x, cond=cond, pos=pos, spatial_cond=sc)
+    ref_loss = torch.sqrt(torch.sum((ref_pred - labels) ** 2))
+    ref_loss.backward()
+    m = m.to(DEV).train()
+    pred = m(x.to(DEV), cond=cond.to(DEV), bc=None, pos=pos.to(DEV), t_cond=None, spatial_cond=sc.to(DEV))
+    loss = ad.sqrt_mse_sum(pred, labels.to(DEV))
+    loss.backward()
+    assert rel_l2(pred, ref_pred) < TOL
+    assert abs(loss.item() - ref_loss.item()) / ref_loss.item() < TOL
+    _grads_ok({k: t.grad for k, t in om.sd.items() if t.grad is not None},
+              {k: p.grad for k, p in m.named_parameters()})
+
+
+def test_ufno_c3_full_size_train_grads():
+    """North-star config C3 (U-FNO twophase cfg: hidden 192, 3 blocks, modes 10, 256x256, 3 fields,
+    obstacle), B=1: sqrt(MSE_sum) training loss and every parameter gradient vs the CPU oracle."""
+    import __graft_entry__  # noqa: F401
+    from bench import build_model
+    from nps_hip import autograd as ad
+    from trainers.synthetic import twophase_batch
+    m, ocfg, opde = build_model("ufno", res=256, num_c=3, device=DEV)
+    m.train()
+    u, cond, pos, sc = twophase_batch(1, 3, 50, 256, 256, seed=7, obstacle="disc")
+    x, labels = u[:, :, :25], u[:, :, 25:50]
+    om = oracle.build_oracle_model(ocfg, opde, {k: v.cpu() for k, v in m.state_dict().items()})
+    om.sd = {k: v.detach().clone().requires_grad_(True) for k, v in om.sd.items()}
+    ref_loss = torch.sqrt(torch.sum((om(x, cond=cond, pos=pos, spatial_cond=sc) - labels) ** 2))
+    ref_loss.backward()
+    loss = ad.sqrt_mse_sum(m(x.to(DEV), cond=cond.to(DEV), bc=None, pos=pos.to(DEV), t_cond=None,
+                             spatial_cond=sc.to(DEV)), labels.to(DEV))
+    loss.backward()
+    assert abs(loss.item() - ref_loss.item()) / ref_loss.item() < TOL
+    _grads_ok({k: t.grad for k, t in om.sd.items() if t.grad is not None},
+              {k: p.grad for k, p in m.named_parameters()})
+
+
+def test_pushforward_train_one_epoch():
+    """trainers/base.py:472-507 loop with the pushforward train_step (:43-163) and Adam on the MI355X:
+    finite losses, every parameter updated, loss goes down over a few steps on a fixed batch."""
+    import argparse
+    import types
+    import random
+    from bench import build_model
+    from common.interfaces import D
+    from trainers.autoregressivepushforwardtrainer import AutoregressivePushforwardTrainer
+    from trainers.synthetic import twophase_batch
+    random.seed(0)
+    m, _, _ = build_model("ufno", res=32, num_c=1, device=DEV)
+    m.train()
+    # T = 50: the only valid window starts at step 25, so successive losses are comparable
+    u, cond, pos, sc = twophase_batch(2, 1, 50, 32, 32, seed=3, obstacle="random", device=DEV)
+    batch = (u[:, :, :1], u, pos, cond, torch.empty(0, device=DEV), sc)
+    cfg = argparse.Namespace(time_window=25, base_resolution=(50, 32, 32), device=DEV, batch_size=2,
+                             lr_step_interval=1, unrolling=2)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-4)
+    tr = AutoregressivePushforwardTrainer(model=m, data=types.SimpleNamespace(pde=m.pde, data_interface=D.sim2d),
+                                          criterion=nn.MSELoss(reduction="sum"), optimizer=opt, config=cfg)
+    before = {k: p.detach().clone() for k, p in m.named_parameters()}
+    losses = [float(tr.train_one_epoch([batch], epoch=0)) for _ in range(6)]
+    assert all(l == l and l < 1e6 for l in losses), losses
+    assert losses[-1] < losses[0], losses
+    for k, p in m.named_parameters():
+        assert not torch.equal(p.detach(), before[k]), f"{k} not updated"
+    # epoch >= lr_step_interval: random unroll depth (no-grad pushforward calls) before the grad call
+    u2, _, _, _ = twophase_batch(2, 1, 125, 32, 32, seed=4, obstacle="random", device=DEV)
+    cfg.base_resolution = (125, 32, 32)
+    tr2 = AutoregressivePushforwardTrainer(model=m, data=types.SimpleNamespace(pde=m.pde, data_interface=D.sim2d),
+                                           criterion=nn.MSELoss(reduction="sum"), optimizer=opt, config=cfg)
+    for _ in range(3):
+        l2 = float(tr2.train_one_epoch([(u2[:, :, :1], u2, pos, cond, torch.empty(0, device=DEV), sc)], epoch=3))
+        assert l2 == l2
