@@ -64,21 +64,66 @@ def build_model(kind, res, num_c, device, fno_modes=None, seed=42):
     return m, ocfg, dict(ORACLE_PDE, nx1=res, nx2=res)
 
 
+# dense MFMA peaks, MI355X_MICROARCH.md: f32 (v_mfma_f32_32x32x2_f32) 157.3 TF; f16 2.5 PF.  A split-fp16
+# conv spends 3 f16 MFMA products per algorithmic fp32 product, so its fp32-equivalent ceiling is 2.5 PF / 3.
+PEAK_TFLOPS = {"f32": FP32_MFMA_PEAK_TFLOPS, "x3f16": 2500.0 / 3.0}
+KERNEL_NAMES = {("x3f16", 9): "conv2d_pc_kernel<9,16,*,2,1,true> (3x3, split-fp16 MFMA)",
+                ("x3f16", 4): "conv2d_pc_kernel<4,16,*,2,1,true> (2x2 phase / space-to-depth, split-fp16 MFMA)",
+                ("f32", 1): "conv2d_pc_kernel<1,32,2,3,2,false> (1x1, f32 MFMA)"}
+
+
 def conv_roofline(model, x, cond, pos, sc):
-    """One model call with every conv launch bracketed by HIP events on its stream."""
+    """One model call with every conv launch bracketed by HIP events on its stream; the roofline is
+    reported for the conv class with the largest total time (the dominant kernel)."""
     from nps_hip import ops
     ops.conv_probe = []
     with torch.no_grad():
         model(x, cond=cond, bc=None, pos=pos, t_cond=None, spatial_cond=sc)
     torch.cuda.synchronize()
     probe, ops.conv_probe = ops.conv_probe, None
-    ms = sum(e0.elapsed_time(e1) for e0, e1, _ in probe)
-    flops = sum(f for _, _, f in probe)
+    groups = {}
+    for e0, e1, f, (prec, ntaps, waves), nb in probe:
+        g = groups.setdefault((prec, ntaps), [0.0, 0.0, 0, 0.0])
+        g[0] += e0.elapsed_time(e1)
+        g[1] += f
+        g[2] += 1
+        g[3] += nb
+    key = max(groups, key=lambda k: groups[k][0])
+    ms, flops, n, nbytes = groups[key]
     achieved = flops / (ms * 1e-3) / 1e12
-    return dict(bound="mfma", achieved=round(achieved, 3), peak=FP32_MFMA_PEAK_TFLOPS, unit="TFLOP/s",
-                frac=round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), traffic=None,
-                kernel="conv2d_fwd_kernel (nps_conv2d_fwd)", launches=len(probe),
-                avg_launch_ms=round(ms / max(1, len(probe)), 4), flops_per_call=flops)
+    peak = PEAK_TFLOPS[key[0]]
+    all_ms = sum(g[0] for g in groups.values())
+    classes = {f"{p}_{t}tap": dict(launches=c, ms=round(m, 3), tflops=round(fl / (m * 1e-3) / 1e12, 2))
+               for (p, t), (m, fl, c, _) in groups.items()}
+    return dict(bound="mfma", achieved=round(achieved, 3), peak=round(peak, 1), unit="TFLOP/s",
+                frac=round(achieved / peak, 4), traffic=None,
+                kernel=KERNEL_NAMES.get(key, f"conv {key}"), arithmetic=key[0], launches=n,
+                avg_launch_ms=round(ms / max(1, n), 4), flops_per_launch=flops / max(1, n),
+                algorithmic_bytes_per_launch=nbytes / max(1, n),
+                conv_ms_per_call=round(all_ms, 3), conv_classes=classes)
+
+
+def _dtype():
+    from nps_hip import ops
+    return "f32" if ops.CONV_PRECISION == ops.PREC_F32 else "f32 (2x2/3x3 convs: 3-pass split-fp16 MFMA)"
+
+
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+
+
+def attach_traffic(roof):
+    """roofline.traffic: HBM bytes per launch of the dominant kernel from the committed rocprofv3 --pmc
+    passes (tools/pmc_traffic.sh; FETCH_SIZE doubled per MI355X_MICROARCH.md § HBM, + WRITE_SIZE)."""
+    try:
+        with open(PMC_FILE) as f:
+            pmc = json.load(f)
+    except (OSError, ValueError):
+        return roof
+    for name, rec in pmc.get("kernels", {}).items():
+        if rec.get("class") == f"{roof['arithmetic']}_{roof['kernel'].split('<')[1].split(',')[0]}tap":
+            roof["traffic"] = rec["hbm_bytes_per_launch"]
+            roof["traffic_source"] = f"{os.path.relpath(PMC_FILE, ROOT)} ({pmc.get('command', '')})"
+    return roof
 
 
 def cpu_baseline(model, ocfg, opde, res, num_c, calls=2, B=2):
@@ -185,14 +230,14 @@ def main():
     value = args.global_batch * tw * args.steps / elapsed
 
     if rank == 0:
-        roof = conv_roofline(model, u_all[:, :, :tw], cond, pos, sc)
+        roof = attach_traffic(conv_roofline(model, u_all[:, :, :tw], cond, pos, sc))
         cpu = cpu_baseline(model, ocfg, opde, args.res, args.num_c, calls=args.cpu_calls) if (
             args.cpu_calls > 0 and world == 1) else None
         line = {
             "metric": "rollout timesteps/sec on 256x256 two-phase grid (sample-timesteps/s); rel-L2 vs CPU reference",
             "value": round(value, 3), "unit": "sample-timesteps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "scaling": "strong", "vs_baseline": None, "dtype": _dtype(), "data": "synthetic",
             "config": {"workload": f"{args.model.upper()} twophase cfg rollout (simulate), {args.res}x{args.res}, "
                                    f"{args.num_c} fields, obstacle mask, tw=25", "model": args.model,
                        "global_batch": args.global_batch, "per_gpu_batch": B, "res": args.res,
@@ -265,7 +310,7 @@ def run_train(args):
             "metric": "pushforward training samples/sec (train_step + backward + all-reduce + Adam)",
             "value": round(args.global_batch * args.steps / elapsed, 3), "unit": "samples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": _dtype(),
             "data": "synthetic",
             "config": {"workload": f"{args.model.upper()} twophase cfg train_step, {args.res}x{args.res}, "
                                    f"{args.num_c} fields, tw=25", "global_batch": args.global_batch,

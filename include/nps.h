@@ -82,7 +82,19 @@ typedef struct {
     int add_after_act;              /* 0: act(acc+bias+addends); 1: act(acc+bias)+addends */
     /* tiling, chosen by nps_conv2d_plan() */
     int TH, TW, lattice, waves;
+    /* arithmetic: NPS_PREC_F32 = exact fp32 MFMA (v_mfma_f32_32x32x2_f32); NPS_PREC_X3F16 = 3-pass
+     * split fp16 (x = hi + 2^-11 lo, products hi*hi + 2^-11 (hi*lo + lo*hi) on v_mfma_f32_32x32x16_f16,
+     * fp32 accumulate, ~2^-22 relative per product) — only where nps_conv2d_x3_eligible(), with the
+     * weight packed by nps_conv2d_pack_weights_x3 */
+    int precision;
+    /* NPS_PREC_X3F16 only: device pointer to max|input| (nps_absmax) or NULL; the input is scaled by an
+     * exact power of 2 into fp16's normal range before the split and the result scaled back
+     * (used for gradients, whose magnitude is arbitrary) */
+    const float* in_scale;
 } nps_conv2d_t;
+
+#define NPS_PREC_F32 0
+#define NPS_PREC_X3F16 1
 
 /* Floats of the packed weight buffer for a conv with the given shape
  * (ntaps = KH*KW). */
@@ -95,6 +107,14 @@ size_t nps_conv2d_packed_size(int Cout, int Cin, int ntaps);
  * weight w[Cout][Cin/4][3][3] for the space-to-depth 2x2 form (KH = KW = 2, Cin = 4C). */
 int nps_conv2d_pack_weights(const float* w, float* wpack, int Cout, int Cin, int KH, int KW,
                             int transposed_phase, void* stream);
+/* Same transforms, packed as [hi | lo * 2^11] fp16 MFMA fragments for precision = NPS_PREC_X3F16
+ * (same buffer size as nps_conv2d_packed_size). */
+int nps_conv2d_pack_weights_x3(const float* w, float* wpack, int Cout, int Cin, int KH, int KW,
+                               int transposed_phase, void* stream);
+/* 1 when a conv of this geometry runs on the split-fp16 kernel (stride-1, undilated 2x2 / 3x3). */
+int nps_conv2d_x3_eligible(int KH, int KW, int stride, int dil);
+/* *out = max |x[i]| (the input range a split-fp16 conv scales by, nps_conv2d_t.in_scale) */
+int nps_absmax(const float* x, long n, float* out, void* stream);
 /* Stride-2 3x3 convs (U-Net Downsample, proc_unet_modern.py:445-455) run as 2x2 stride-1 convs
  * over a space-to-depth copy: out[B][Hq][Wq][4C], channel (dy*2+dx)*C + c = x[2y+dy-pad][2x+dx-pad][c]
  * (zero outside); pack the weight with transposed_phase = -2 (Cin = 4C). */

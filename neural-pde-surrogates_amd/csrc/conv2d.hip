@@ -24,7 +24,12 @@
 
 namespace {
 
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+
 constexpr int CK = 16;          // input channels per K chunk
+constexpr float X3_SCALE = 2048.f;        // lo part of the fp16 split is stored scaled by 2^11 (stays normal)
+constexpr float X3_INV = 1.f / 2048.f;
 constexpr int PIXS = CK + 4;    // LDS floats per patch pixel (+4 pad: conflict-free ds_read_b128)
 constexpr int MAXL = 12;        // max float4 patch loads per thread per chunk
 
@@ -354,7 +359,36 @@ __host__ __device__ constexpr int pc_patch_px_max(int ntaps, int tile_px) {
     return ntaps == 1 ? tile_px : (tile_px == 256 ? (ntaps == 4 ? 297 : 340) : (ntaps == 4 ? 153 : 180));
 }
 
-template <int NTAPS, int CKB, int PB, int CBW, int WCO>
+// fp32 -> (hi, lo * 2^11) fp16 split of 4 values (round-toward-zero packing: |x - hi| < ulp(hi), and
+// the scaled residual is again exact to 11 bits, so hi + lo * 2^-11 carries ~22 bits of x)
+// Power-of-2 input scale of a split-fp16 conv: maps max|x| (a.in_scale = device pointer to it, from
+// nps_absmax) into [2^13, 2^14) so every element within 2^-27 of the maximum keeps both fp16 halves
+// normal (gradients can be ~1e-8 in magnitude); 1 when no range is given.
+__device__ __forceinline__ float in_scale_of(const nps_conv2d_t& a) {
+    if (a.in_scale == nullptr) return 1.f;
+    const float m = *a.in_scale;
+    if (!(m > 0.f) || !(m < 3.0e38f)) return 1.f;
+    return ldexpf(1.f, 13 - ilogbf(m));
+}
+
+typedef _Float16 h2f __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ h2f pkrtz(float a, float b) { return __builtin_bit_cast(h2f, __builtin_amdgcn_cvt_pkrtz(a, b)); }
+
+__device__ __forceinline__ void split4(const f32x4 v, f16x4& hi, f16x4& lo) {
+    const h2f h01 = pkrtz(v[0], v[1]);
+    const h2f h23 = pkrtz(v[2], v[3]);
+    const h2f l01 = pkrtz((v[0] - (float)h01[0]) * X3_SCALE, (v[1] - (float)h01[1]) * X3_SCALE);
+    const h2f l23 = pkrtz((v[2] - (float)h23[0]) * X3_SCALE, (v[3] - (float)h23[1]) * X3_SCALE);
+    hi = f16x4{h01[0], h01[1], h23[0], h23[1]};
+    lo = f16x4{l01[0], l01[1], l23[0], l23[1]};
+}
+
+// X3 = false: exact fp32 (v_mfma_f32_32x32x2_f32).  X3 = true: 3-pass split-fp16 products
+// (v_mfma_f32_32x32x16_f16: hi*hi into one accumulator, hi*lo + lo*hi into a second, combined as
+// acc_hh + 2^-11 acc_x in the epilogue) — ~2^-22 relative per product at 5.3x the f32 MFMA rate.
+// The LDS stage has the same bytes either way: per pixel and 16-channel sub-chunk, 16 fp32 or
+// [16 hi | 16 lo] fp16; the packed weights are fp32 fragments or [hi | lo] fp16 fragments.
+template <int NTAPS, int CKB, int PB, int CBW, int WCO, bool X3>
 __global__ __launch_bounds__(512) void conv2d_pc_kernel(const nps_conv2d_t a) {
     constexpr int KWT = NTAPS == 9 ? 3 : (NTAPS == 4 ? 2 : 1);
     constexpr int SUB = CKB / CK;                       // 16-channel sub-chunks per stage
@@ -403,7 +437,10 @@ __global__ __launch_bounds__(512) void conv2d_pc_kernel(const nps_conv2d_t a) {
             sy[k] = ok ? (a.circ ? nps::wrap_mod(ye - a.circ, a.Hin) : ye) : -1;
             sx[k] = ok ? (a.circ ? nps::wrap_mod(xe - a.circ, a.Win) : xe) : 0;
         }
-        auto issue = [&](int st) {  // global loads of stage st into registers
+        // two register sets: stage s is loaded into set s & 1, two stages ahead of its LDS commit, so
+        // every global load has two consumer stages of time to land (more bytes in flight per CU)
+        f32x4 ra1[NAP], rp1[MAXP];
+        auto issue = [&](int st, f32x4 (&ra)[NAP], f32x4 (&rp)[MAXP]) {  // global loads of stage st
 #pragma unroll
             for (int k = 0; k < NAP; ++k) {
                 const int e = k * 256 + ptid;
@@ -464,7 +501,8 @@ __global__ __launch_bounds__(512) void conv2d_pc_kernel(const nps_conv2d_t a) {
                 }
             }
         };
-        auto commit = [&](int buf) {  // LDS store of the staged stage
+        const float xs = X3 ? in_scale_of(a) : 1.f;  // exact power-of-2 range scaling of the input
+        auto commit = [&](int buf, const f32x4 (&ra)[NAP], const f32x4 (&rp)[MAXP]) {  // LDS store of a stage
             float* A = ring + buf * stage_fl;
             float* Pt = A + AFL;
 #pragma unroll
@@ -474,14 +512,24 @@ __global__ __launch_bounds__(512) void conv2d_pc_kernel(const nps_conv2d_t a) {
                 const int idx = ptid + k * 256;
                 if (idx < NG) {
                     const int p = idx / (CKB / 4), gq = idx - p * (CKB / 4);
-                    *reinterpret_cast<f32x4*>(Pt + p * PIXSB + gq * 4) = rp[k];
+                    if constexpr (X3) {
+                        // channel c = 4 gq: sub-chunk c / 16 at 16 floats (= 32 halves) per sub-chunk
+                        f16x4 hi, lo;
+                        split4(rp[k] * xs, hi, lo);
+                        _Float16* base = reinterpret_cast<_Float16*>(Pt + p * PIXSB + (gq >> 2) * 16) + (gq & 3) * 4;
+                        *reinterpret_cast<f16x4*>(base) = hi;
+                        *reinterpret_cast<f16x4*>(base + 16) = lo;
+                    } else {
+                        *reinterpret_cast<f32x4*>(Pt + p * PIXSB + gq * 4) = rp[k];
+                    }
                 }
             }
         };
 #ifndef NPS_ABLATE_PRODUCER
-        issue(0);
-        commit(0);
-        if (nstages > 1) issue(1);
+        issue(0, ra, rp);
+        commit(0, ra, rp);
+        if (nstages > 1) issue(1, ra1, rp1);
+        if (nstages > 2) issue(2, ra, rp);
 #endif
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         for (int st = 0; st < nstages; ++st) {
@@ -490,8 +538,13 @@ __global__ __launch_bounds__(512) void conv2d_pc_kernel(const nps_conv2d_t a) {
 #else
             if (st + 1 < nstages) {
 #endif
-                commit((st + 1) & 1);
-                if (st + 2 < nstages) issue(st + 2);
+                if ((st + 1) & 1) {
+                    commit(1, ra1, rp1);
+                    if (st + 3 < nstages) issue(st + 3, ra1, rp1);
+                } else {
+                    commit(0, ra, rp);
+                    if (st + 3 < nstages) issue(st + 3, ra, rp);
+                }
             }
             asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         }
@@ -508,17 +561,92 @@ __global__ __launch_bounds__(512) void conv2d_pc_kernel(const nps_conv2d_t a) {
         boff[pb] = (ti * g.PW + tj) * PIXSB + (lane >> 5) * 8;
     }
     f32x16 acc[CBW][PB];
+    f32x16 accx[X3 ? CBW : 1][X3 ? PB : 1];
 #pragma unroll
     for (int i = 0; i < CBW; ++i)
 #pragma unroll
         for (int j = 0; j < PB; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    if constexpr (X3) {
+#pragma unroll
+        for (int i = 0; i < CBW; ++i)
+#pragma unroll
+            for (int j = 0; j < PB; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) accx[i][j][r] = 0.f;
+    }
 
     // Operands of K-group gi = (sub, tap, q) are read one group ahead into a second register set,
     // so every group's 8*PB MFMAs (>= 512 cycles) cover the LDS latency of the next group's reads.
     constexpr int G = SUB * NTAPS * 2;
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if constexpr (X3) {
+        const float inv_xs = 1.f / in_scale_of(a);
+        // K-group = (sub, tap): 16 channels, lane half h holds channels 8h..8h+7 (one b128 per operand
+        // half); A fragment = 2 KiB [hi: 64 lanes x 16 B | lo: 64 lanes x 16 B]
+        constexpr int GX = SUB * NTAPS;
+        int boffx[PB];
+#pragma unroll
+        for (int pb = 0; pb < PB; ++pb) {
+            const int P = wpx * 32 * PB + pb * 32 + (lane & 31);
+            const int ti = P / a.TW, tj = P - (P / a.TW) * a.TW;
+            boffx[pb] = (ti * g.PW + tj) * PIXSB * 4 + (lane >> 5) * 16;  // bytes
+        }
+        for (int st = 0; st < nstages; ++st) {
+            const char* A = reinterpret_cast<const char*>(ring + (st & 1) * stage_fl);
+            const char* Pt = A + AFL * 4;
+            f16x8 ah[2][CBW], al[2][CBW], bh[2][PB], bl[2][PB];
+            auto load_group = [&](int gi, f16x8 (&adh)[CBW], f16x8 (&adl)[CBW], f16x8 (&bdh)[PB], f16x8 (&bdl)[PB]) {
+                const int sub = gi / NTAPS, tap = gi - sub * NTAPS;
+                const int ky = tap / KWT, kx = tap % KWT;
+                const int toff = (ky * g.PW + kx) * PIXSB * 4 + sub * 64;
+#pragma unroll
+                for (int cb = 0; cb < CBW; ++cb) {
+                    const char* ab = A + ((sub * NTAPS + tap) * NCBG + wco * CBW + cb) * 2048 + lane * 16;
+                    adh[cb] = *reinterpret_cast<const f16x8*>(ab);
+                    adl[cb] = *reinterpret_cast<const f16x8*>(ab + 1024);
+                }
+#pragma unroll
+                for (int pb = 0; pb < PB; ++pb) {
+                    bdh[pb] = *reinterpret_cast<const f16x8*>(Pt + boffx[pb] + toff);
+                    bdl[pb] = *reinterpret_cast<const f16x8*>(Pt + boffx[pb] + toff + 32);
+                }
+            };
+#ifndef NPS_ABLATE_CONSUMER
+            load_group(0, ah[0], al[0], bh[0], bl[0]);
+#pragma unroll
+            for (int gi = 0; gi < GX; ++gi) {
+                const int cur = gi & 1;
+                if (gi + 1 < GX) load_group(gi + 1, ah[cur ^ 1], al[cur ^ 1], bh[cur ^ 1], bl[cur ^ 1]);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int cb = 0; cb < CBW; ++cb)
+#pragma unroll
+                    for (int pb = 0; pb < PB; ++pb)
+                        acc[cb][pb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[cur][cb], bh[cur][pb], acc[cb][pb], 0, 0, 0);
+#pragma unroll
+                for (int cb = 0; cb < CBW; ++cb)
+#pragma unroll
+                    for (int pb = 0; pb < PB; ++pb)
+                        accx[cb][pb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[cur][cb], bl[cur][pb], accx[cb][pb], 0, 0, 0);
+#pragma unroll
+                for (int cb = 0; cb < CBW; ++cb)
+#pragma unroll
+                    for (int pb = 0; pb < PB; ++pb)
+                        accx[cb][pb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[cur][cb], bh[cur][pb], accx[cb][pb], 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+#endif
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+#pragma unroll
+        for (int i = 0; i < CBW; ++i)
+#pragma unroll
+            for (int j = 0; j < PB; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][j][r] = fmaf(accx[i][j][r], X3_INV, acc[i][j][r]) * inv_xs;
+    } else
     for (int st = 0; st < nstages; ++st) {
         const float* A = ring + (st & 1) * stage_fl;
         const float* Pt = A + AFL;
@@ -573,7 +701,27 @@ __global__ __launch_bounds__(512) void conv2d_pc_kernel(const nps_conv2d_t a) {
     }
 }
 
-// Packed layout: [chunk][tap][cb (32-co block, padded to a multiple of 2)][q (2)][lane (64)][4]
+// Weight element (co, ci, tap) of the conv being packed, from w in the layout the mode implies.
+__device__ __forceinline__ float weight_elem(const float* __restrict__ w, int Cout, int Cin, int KH, int KW, int tphase,
+                                             int co, int ci, int tap) {
+    if (co >= Cout || ci >= Cin) return 0.f;
+    const int ky = tap / KW, kx = tap % KW;
+    if (tphase == -2) {
+        // 3x3 / stride-2 conv as a 2x2 conv over the space-to-depth input: channel
+        // ci = (dy*2 + dx)*C + c, tap (ky, kx) -> kernel element (2ky + dy, 2kx + dx) of w[Cout][C][3][3]
+        const int C = Cin / 4, par = ci / C, c = ci - par * C;
+        const int kyy = 2 * ky + (par >> 1), kxx = 2 * kx + (par & 1);
+        return (kyy < 3 && kxx < 3) ? w[(((size_t)co * C + c) * 3 + kyy) * 3 + kxx] : 0.f;
+    }
+    if (tphase < 0) return w[(((size_t)co * Cin + ci) * KH + ky) * KW + kx];
+    // 4x4 / stride-2 transposed conv, output phase (py, px): tap (ty, tx) uses
+    // kernel element (py + 2(1-ty), px + 2(1-tx)) of w[Cin][Cout][4][4]
+    const int py = tphase >> 1, px = tphase & 1;
+    const int kyy = py + 2 * (1 - ky), kxx = px + 2 * (1 - kx);
+    return w[(((size_t)ci * Cout + co) * 4 + kyy) * 4 + kxx];
+}
+
+// Packed layout (fp32): [chunk][tap][cb (32-co block, padded to a multiple of 6)][q (2)][lane (64)][4]
 // element = w[co = cb*32 + (lane&31)][ci = chunk*16 + (lane>>5)*8 + q*4 + e][tap]
 __global__ void pack_weights_kernel(const float* __restrict__ w, float* __restrict__ wp, int Cout, int Cin, int KH,
                                     int KW, int tphase, size_t total) {
@@ -588,28 +736,32 @@ __global__ void pack_weights_kernel(const float* __restrict__ w, float* __restri
     const int cb = r % ncb; r /= ncb;
     const int tap = r % ntaps; r /= ntaps;
     const int chunk = (int)r;
-    const int co = cb * 32 + (lane & 31);
-    const int ci = chunk * CK + (lane >> 5) * 8 + q * 4 + e;
-    float v = 0.f;
-    if (co < Cout && ci < Cin) {
-        const int ky = tap / KW, kx = tap % KW;
-        if (tphase == -2) {
-            // 3x3 / stride-2 conv as a 2x2 conv over the space-to-depth input: channel
-            // ci = (dy*2 + dx)*C + c, tap (ky, kx) -> kernel element (2ky + dy, 2kx + dx) of w[Cout][C][3][3]
-            const int C = Cin / 4, par = ci / C, c = ci - par * C;
-            const int kyy = 2 * ky + (par >> 1), kxx = 2 * kx + (par & 1);
-            if (kyy < 3 && kxx < 3) v = w[(((size_t)co * C + c) * 3 + kyy) * 3 + kxx];
-        } else if (tphase < 0) {
-            v = w[(((size_t)co * Cin + ci) * KH + ky) * KW + kx];
-        } else {
-            // 4x4 / stride-2 transposed conv, output phase (py, px): tap (ty, tx) uses
-            // kernel element (py + 2(1-ty), px + 2(1-tx)) of w[Cin][Cout][4][4]
-            const int py = tphase >> 1, px = tphase & 1;
-            const int kyy = py + 2 * (1 - ky), kxx = px + 2 * (1 - kx);
-            v = w[(((size_t)ci * Cout + co) * 4 + kyy) * 4 + kxx];
-        }
-    }
-    wp[i] = v;
+    wp[i] = weight_elem(w, Cout, Cin, KH, KW, tphase, cb * 32 + (lane & 31), chunk * CK + (lane >> 5) * 8 + q * 4 + e,
+                        tap);
+}
+
+// Packed layout (3-pass split fp16, same bytes): [chunk][tap][cb][hl (2)][lane (64)][8 halves]
+// element j of lane = (hi | lo * 2^11) of w[co = cb*32 + (lane&31)][ci = chunk*16 + (lane>>5)*8 + j][tap]
+__global__ void pack_weights_x3_kernel(const float* __restrict__ w, _Float16* __restrict__ wp, int Cout, int Cin,
+                                       int KH, int KW, int tphase, size_t total_pairs) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // (hi, lo) pair index
+    if (i >= total_pairs) return;
+    const int ntaps = KH * KW;
+    const int ncb = packed_ncb(Cout);
+    const int j = i & 7;
+    size_t r = i >> 3;
+    const int lane = r & 63; r >>= 6;
+    const int cb = r % ncb; r /= ncb;
+    const int tap = r % ntaps; r /= ntaps;
+    const int chunk = (int)r;
+    const float v = weight_elem(w, Cout, Cin, KH, KW, tphase, cb * 32 + (lane & 31), chunk * CK + (lane >> 5) * 8 + j,
+                                tap);
+    const size_t frag = i >> 9;  // (chunk, tap, cb) fragment of 64 lanes x 8
+    const size_t o = frag * 1024 + (size_t)lane * 8 + j;
+    const h2f hv = pkrtz(v, 0.f);
+    const h2f lv = pkrtz((v - (float)hv[0]) * X3_SCALE, 0.f);
+    wp[o] = hv[0];
+    wp[o + 512] = lv[0];
 }
 
 size_t packed_size(int Cout, int Cin, int ntaps) {
@@ -622,6 +774,12 @@ bool pc_eligible(const nps_conv2d_t& a) {
     // the producer/consumer kernel does no prologue (callers materialise it with nps_frame_pack)
     return a.stride == 1 && a.dil == 1 && a.KH == a.KW && (nt == 1 || nt == 4 || nt == 9) && a.gn_stats == nullptr &&
            a.pre_act == 0;
+}
+
+// 3-pass split-fp16 variant: stride-1 2x2 / 3x3 producer/consumer convs (1x1s stay exact f32)
+bool x3_eligible(const nps_conv2d_t& a) {
+    const int nt = a.KH * a.KW;
+    return pc_eligible(a) && (nt == 4 || nt == 9);
 }
 
 // producer/consumer variant per tap count: 1x1 convs use 192-channel x 128-pixel work-groups
@@ -661,6 +819,29 @@ extern "C" int nps_conv2d_pack_weights(const float* w, float* wpack, int Cout, i
                                                                                         transposed_phase, total);
     NPS_CHECK_LAUNCH("conv2d_pack_weights");
     return 0;
+}
+
+extern "C" int nps_conv2d_pack_weights_x3(const float* w, float* wpack, int Cout, int Cin, int KH, int KW,
+                                          int transposed_phase, void* stream) {
+    NPS_CHECK_ARG(w && wpack && Cout > 0 && Cin > 0 && KH > 0 && KW > 0, "conv2d_pack_weights_x3: bad args");
+    NPS_CHECK_ARG(transposed_phase == -1 || ((transposed_phase == -2 || (transposed_phase >= 0 && transposed_phase < 4)) &&
+                                             KH == 2 && KW == 2 && (transposed_phase != -2 || Cin % 4 == 0)),
+                  "conv2d_pack_weights_x3: phase / space-to-depth packing needs KH=KW=2");
+    const size_t pairs = packed_size(Cout, Cin, KH * KW);  // one (hi, lo) pair per fp32 slot
+    const int bs = 256;
+    pack_weights_x3_kernel<<<(unsigned)((pairs + bs - 1) / bs), bs, 0, (hipStream_t)stream>>>(
+        w, reinterpret_cast<_Float16*>(wpack), Cout, Cin, KH, KW, transposed_phase, pairs);
+    NPS_CHECK_LAUNCH("conv2d_pack_weights_x3");
+    return 0;
+}
+
+extern "C" int nps_conv2d_x3_eligible(int KH, int KW, int stride, int dil) {
+    nps_conv2d_t t = {};
+    t.KH = KH;
+    t.KW = KW;
+    t.stride = stride;
+    t.dil = dil;
+    return x3_eligible(t) ? 1 : 0;
 }
 
 extern "C" int nps_conv2d_plan(nps_conv2d_t* a) {
@@ -734,28 +915,36 @@ extern "C" int nps_conv2d_plan(nps_conv2d_t* a) {
 }
 
 namespace {
-template <int NT, int CKB, int PB, int CBW, int WCO>
+template <int NT, int CKB, int PB, int CBW, int WCO, bool X3>
 void launch_pc_one(const nps_conv2d_t& a, dim3 grid, int lds, hipStream_t s) {
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)conv2d_pc_kernel<NT, CKB, PB, CBW, WCO>,
+        (void)hipFuncSetAttribute((const void*)conv2d_pc_kernel<NT, CKB, PB, CBW, WCO, X3>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_set = true;
     }
-    conv2d_pc_kernel<NT, CKB, PB, CBW, WCO><<<grid, 512, lds, s>>>(a);
+    conv2d_pc_kernel<NT, CKB, PB, CBW, WCO, X3><<<grid, 512, lds, s>>>(a);
+}
+
+template <bool X3>
+void launch_pc_taps(const nps_conv2d_t& a, dim3 grid, int lds, hipStream_t s, int nt, bool pb2) {
+    if (nt == 9) {
+        if (pb2) launch_pc_one<9, 16, 2, 2, 1, X3>(a, grid, lds, s); else launch_pc_one<9, 16, 1, 2, 1, X3>(a, grid, lds, s);
+    } else {
+        if (pb2) launch_pc_one<4, 16, 2, 2, 1, X3>(a, grid, lds, s); else launch_pc_one<4, 16, 1, 2, 1, X3>(a, grid, lds, s);
+    }
 }
 
 int launch_pc(const nps_conv2d_t& a, dim3 grid, int lds, hipStream_t s) {
     const int nt = a.KH * a.KW;
     const bool pb2 = a.TH * a.TW == 256;
     grid.y = (a.Cout + pc_ncbg(nt) * 32 - 1) / (pc_ncbg(nt) * 32);
-    if (nt == 9) {
-        if (pb2) launch_pc_one<9, 16, 2, 2, 1>(a, grid, lds, s); else launch_pc_one<9, 16, 1, 2, 1>(a, grid, lds, s);
-    } else if (nt == 4) {
-        if (pb2) launch_pc_one<4, 16, 2, 2, 1>(a, grid, lds, s); else launch_pc_one<4, 16, 1, 2, 1>(a, grid, lds, s);
-    } else {
-        launch_pc_one<1, 32, 2, 3, 2>(a, grid, lds, s);
-    }
+    if (nt == 1)
+        launch_pc_one<1, 32, 2, 3, 2, false>(a, grid, lds, s);
+    else if (a.precision == NPS_PREC_X3F16)
+        launch_pc_taps<true>(a, grid, lds, s, nt, pb2);
+    else
+        launch_pc_taps<false>(a, grid, lds, s, nt, pb2);
     NPS_CHECK_LAUNCH("conv2d_fwd (producer/consumer)");
     return 0;
 }
@@ -778,6 +967,9 @@ extern "C" int nps_conv2d_fwd(const nps_conv2d_t* ap, void* stream) {
                   "conv2d_fwd: bad GroupNorm prologue");
     NPS_CHECK_ARG(a.circ == 0 || (a.Hin > 0 && a.Win > 0), "conv2d_fwd: circular padding of empty frame");
     NPS_CHECK_ARG(a.waves == 1 || a.waves == 2 || a.waves == 4 || a.waves == 8, "conv2d_fwd: call nps_conv2d_plan first");
+    NPS_CHECK_ARG(a.precision == NPS_PREC_F32 || (a.precision == NPS_PREC_X3F16 && x3_eligible(a) && a.waves == 8),
+                  "conv2d_fwd: precision %d not available for this conv (KH=%d stride=%d dil=%d)", a.precision, a.KH,
+                  a.stride, a.dil);
     NPS_CHECK_ARG(a.waves == 8 ? (a.TH * a.TW == 256 || a.TH * a.TW == 128) && pc_eligible(a) &&
                                      (a.KH * a.KW != 1 || a.TH * a.TW == 128)
                                : a.TH * a.TW == 64 * a.waves,
@@ -995,6 +1187,32 @@ extern "C" int nps_frame_pack(const nps_conv2d_t* ap, float* out, void* stream) 
     nb = nb > 2048 ? 2048 : nb;
     frame_pack_kernel<<<dim3(nb, a.B), 256, 0, (hipStream_t)stream>>>(a, out);
     NPS_CHECK_LAUNCH("frame_pack");
+    return 0;
+}
+
+// ------------------------------------------------------------------ absmax (input range of split-fp16 convs)
+namespace {
+__global__ void absmax_kernel(const float* __restrict__ x, long n, unsigned int* __restrict__ out) {
+    float m = 0.f;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+        m = fmaxf(m, fabsf(x[i]));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));  // non-negative floats order as uints
+}
+}  // namespace
+
+extern "C" int nps_absmax(const float* x, long n, float* out, void* stream) {
+    NPS_CHECK_ARG(x && out && n > 0, "absmax: bad args");
+    hipStream_t s = (hipStream_t)stream;
+    if (hipMemsetAsync(out, 0, sizeof(float), s) != hipSuccess) {
+        nps::set_error("absmax: memset failed");
+        return -2;
+    }
+    long nb = (n + 256 * 16 - 1) / (256 * 16);
+    nb = nb < 1 ? 1 : (nb > 1024 ? 1024 : nb);
+    absmax_kernel<<<(unsigned)nb, 256, 0, s>>>(x, n, reinterpret_cast<unsigned int*>(out));
+    NPS_CHECK_LAUNCH("absmax");
     return 0;
 }
 

@@ -67,7 +67,7 @@ class _PackedMixin:
 
     def _packed(self, fn):
         w = self.weight
-        key = (w.data_ptr(), w._version, str(w.device))
+        key = (w.data_ptr(), w._version, str(w.device), ops.CONV_PRECISION)
         if getattr(self, "_pk_key", None) != key:
             self._pk = fn(w)
             self._pk_key = key
@@ -112,13 +112,14 @@ class Conv2d(_PackedMixin, nn.Conv2d):
             Wo = (frame_hw[1] + 2 * p - 3) // 2 + 1
             xq = ops.space_to_depth(x, p, Ho + 1, Wo + 1)
             wk = self.weight
-            key = ("s2d", wk.data_ptr(), wk._version, str(wk.device))
+            key = ("s2d", wk.data_ptr(), wk._version, str(wk.device), ops.CONV_PRECISION)
             if getattr(self, "_pk2_key", None) != key:
                 self._pk2 = ops.pack_conv_weight_s2d(wk)
                 self._pk2_key = key
             return ops.conv2d([ops.Src(xq)], (Ho + 1, Wo + 1), self._pk2, self.bias, self.out_channels, 2, 2,
                               out_hw=(Ho, Wo), **kw)
-        return ops.conv2d(srcs, frame_hw, self._packed(ops.pack_conv_weight), self.bias, self.out_channels, KH, KW,
+        return ops.conv2d(srcs, frame_hw, self._packed(lambda w: ops.pack_conv_weight(w, s, d)), self.bias,
+                          self.out_channels, KH, KW,
                           stride=s, dil=d, pad=lo, pad_bottom=hi, circ=circ, **kw)
 
     def forward(self, x):

@@ -46,6 +46,7 @@ class Conv2dArgs(ctypes.Structure):
         ("addend0", ctypes.c_void_p), ("addend1", ctypes.c_void_p),
         ("act", ctypes.c_int), ("add_after_act", ctypes.c_int),
         ("TH", ctypes.c_int), ("TW", ctypes.c_int), ("lattice", ctypes.c_int), ("waves", ctypes.c_int),
+        ("precision", ctypes.c_int), ("in_scale", ctypes.c_void_p),
     ]
 
 
@@ -62,6 +63,9 @@ _vp, _i, _l, _sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_size_t
 _SIGS = {
     "nps_conv2d_packed_size": (_sz, [_i, _i, _i]),
     "nps_conv2d_pack_weights": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp]),
+    "nps_conv2d_pack_weights_x3": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp]),
+    "nps_conv2d_x3_eligible": (_i, [_i, _i, _i, _i]),
+    "nps_absmax": (_i, [_vp, _l, _vp, _vp]),
     "nps_conv2d_plan": (_i, [ctypes.POINTER(Conv2dArgs)]),
     "nps_conv2d_fwd": (_i, [ctypes.POINTER(Conv2dArgs), _vp]),
     "nps_frame_pack": (_i, [ctypes.POINTER(Conv2dArgs), _vp, _vp]),

@@ -53,9 +53,9 @@ def channel_sums(x: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def _pack_plain(w):
-    """Pack a [Cout][Cin][KH][KW] conv weight (any derived tensor)."""
-    return ops.pack_conv_weight(w)
+def _pack_plain(w, dil=1):
+    """Pack a [Cout][Cin][KH][KW] stride-1 conv weight (any derived tensor)."""
+    return ops.pack_conv_weight(w, 1, dil)
 
 
 # ------------------------------------------------------------------------- frame (cat/crop/GN/GELU)
@@ -173,7 +173,7 @@ class Conv2dFn(torch.autograd.Function):
                            out_hw=(Ho, Wo))
             ctx.save_for_backward(xq, weight)
         elif s == 1:
-            y = ops.conv2d([Src(x)], (H, W), ops.pack_conv_weight(weight), bias, Cout, KH, KW, dil=d, pad=lo,
+            y = ops.conv2d([Src(x)], (H, W), ops.pack_conv_weight(weight, 1, d), bias, Cout, KH, KW, dil=d, pad=lo,
                            pad_bottom=hi, circ=circ)
             ctx.save_for_backward(x, weight)
         else:
@@ -191,14 +191,15 @@ class Conv2dFn(torch.autograd.Function):
         Cin = w.shape[1]
         dx = dw = db = None
         if ctx.needs_input_grad[1]:
+            rng = ops.absmax(gy) if ops.CONV_PRECISION == ops.PREC_X3F16 else None  # gradients: any magnitude
             if s == 1:
                 if circ:
-                    dx = ops.conv2d([Src(gy)], (Ho, Wo), _pack_plain(_dgrad_weight(w)), None, Cin, KH, KW, dil=d,
-                                    circ=circ, out_hw=(H, W))
+                    dx = ops.conv2d([Src(gy)], (Ho, Wo), _pack_plain(_dgrad_weight(w), d), None, Cin, KH, KW, dil=d,
+                                    circ=circ, out_hw=(H, W), in_scale=rng)
                 else:
                     pt = (d * (KH - 1) - lo[0], d * (KW - 1) - lo[1])
-                    dx = ops.conv2d([Src(gy)], (Ho, Wo), _pack_plain(_dgrad_weight(w)), None, Cin, KH, KW, dil=d,
-                                    pad=pt, out_hw=(H, W))
+                    dx = ops.conv2d([Src(gy)], (Ho, Wo), _pack_plain(_dgrad_weight(w), d), None, Cin, KH, KW, dil=d,
+                                    pad=pt, out_hw=(H, W), in_scale=rng)
             else:
                 p = lo[0]
                 dx = torch.empty((B, H, W, Cin), dtype=torch.float32, device=gy.device)
@@ -208,7 +209,8 @@ class Conv2dFn(torch.autograd.Function):
                         if hq <= 0 or wq <= 0:
                             continue
                         ops.conv2d([Src(gy)], (Ho, Wo), _pack_plain(_s2_phase_weight(w, ry, rx, p)), None, Cin, 2, 2,
-                                   pad=(1 - p, 1 - p), out_hw=(hq, wq), out=dx, out_os=2, out_off=(ry, rx))
+                                   pad=(1 - p, 1 - p), out_hw=(hq, wq), out=dx, out_os=2, out_off=(ry, rx),
+                                   in_scale=rng)
         if ctx.needs_input_grad[2]:
             if s == 1:
                 dw = wgrad(gy, xs, KH, KW, dil=d, pad=lo, circ=circ)
@@ -259,8 +261,9 @@ class ConvTranspose2dFn(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[1]:
             w2 = w.detach().view(Cin, Cout, 2, 2, 2, 2).permute(0, 3, 5, 1, 2, 4).reshape(Cin, 4 * Cout, 2, 2)
+            rng = ops.absmax(gout) if ops.CONV_PRECISION == ops.PREC_X3F16 else None
             dxp = ops.conv2d([Src(dq)], (Hp + 1, Wp + 1), _pack_plain(w2.contiguous()), None, Cin, 2, 2,
-                             out_hw=(Hp, Wp))
+                             out_hw=(Hp, Wp), in_scale=rng)
             if c:
                 dx = torch.empty_like(x)
                 check(lib.nps_circular_fold(ptr(dxp), ptr(dx), B, H, W, Cin, c, stream_ptr()), "circular_fold")

@@ -6,6 +6,7 @@ along channels, each placed at an offset of the frame (crop_Nd, cat), so no
 cat / pad / crop is ever materialised.
 """
 import math
+import os
 from typing import List, NamedTuple, Optional, Sequence
 
 import torch
@@ -13,6 +14,18 @@ import torch
 from . import Conv2dArgs, Src as _CSrc, check, lib, ptr, stream_ptr
 
 GELU = 1
+
+# Conv arithmetic (include/nps.h NPS_PREC_*): exact fp32 MFMA, or the 3-pass split-fp16 MFMA products
+# (~2^-22 relative per product, 5.3x the fp32 MFMA rate) for the stride-1 2x2 / 3x3 convs.
+PREC_F32, PREC_X3F16 = 0, 1
+CONV_PRECISION = PREC_F32 if os.environ.get("NPS_CONV_PRECISION", "x3f16") == "f32" else PREC_X3F16
+
+
+def conv_precision(KH, KW, stride=1, dil=1):
+    """Arithmetic a conv of this geometry runs in under the current CONV_PRECISION setting."""
+    if CONV_PRECISION == PREC_X3F16 and lib.nps_conv2d_x3_eligible(KH, KW, stride, dil):
+        return PREC_X3F16
+    return PREC_F32
 
 # Optional live probe of the conv kernel (bench.py): when a list, every conv2d launch appends
 # (start_event, end_event, algorithmic_flops) recorded on the launching stream.
@@ -48,24 +61,28 @@ def empty_nhwc(B, H, W, C, like: torch.Tensor):
 
 
 # ----------------------------------------------------------------- weights ----
-def pack_conv_weight(w: torch.Tensor) -> torch.Tensor:
-    """nn.Conv2d weight (Cout, Cin, KH, KW) -> MFMA-fragment-packed buffer."""
-    w = w.detach().contiguous()
-    Cout, Cin, KH, KW = w.shape
+def _pack(w, Cout, Cin, KH, KW, mode, precision):
     n = lib.nps_conv2d_packed_size(Cout, Cin, KH * KW)
     out = torch.empty(n, dtype=torch.float32, device=w.device)
-    check(lib.nps_conv2d_pack_weights(ptr(w), ptr(out), Cout, Cin, KH, KW, -1, stream_ptr()), "conv2d_pack_weights")
+    fn = lib.nps_conv2d_pack_weights_x3 if precision == PREC_X3F16 else lib.nps_conv2d_pack_weights
+    check(fn(ptr(w), ptr(out), Cout, Cin, KH, KW, mode, stream_ptr()), "conv2d_pack_weights")
+    out.nps_precision = precision   # read back by conv2d(): the kernel must match the packing
     return out
+
+
+def pack_conv_weight(w: torch.Tensor, stride=1, dil=1) -> torch.Tensor:
+    """nn.Conv2d weight (Cout, Cin, KH, KW) -> MFMA-fragment-packed buffer (fp32 or split-fp16 fragments,
+    whichever the conv of this geometry runs in)."""
+    w = w.detach().contiguous()
+    Cout, Cin, KH, KW = w.shape
+    return _pack(w, Cout, Cin, KH, KW, -1, conv_precision(KH, KW, stride, dil))
 
 
 def pack_conv_weight_s2d(w: torch.Tensor) -> torch.Tensor:
     """3x3 stride-2 weight (Cout, C, 3, 3) -> packed 2x2 conv over the space-to-depth input (4C channels)."""
     w = w.detach().contiguous()
     Cout, C = w.shape[0], w.shape[1]
-    n = lib.nps_conv2d_packed_size(Cout, 4 * C, 4)
-    out = torch.empty(n, dtype=torch.float32, device=w.device)
-    check(lib.nps_conv2d_pack_weights(ptr(w), ptr(out), Cout, 4 * C, 2, 2, -2, stream_ptr()), "pack s2d")
-    return out
+    return _pack(w, Cout, 4 * C, 2, 2, -2, conv_precision(2, 2))
 
 
 def space_to_depth(x: torch.Tensor, pad: int, Hq: int, Wq: int) -> torch.Tensor:
@@ -79,13 +96,7 @@ def pack_convT_phases(w: torch.Tensor) -> List[torch.Tensor]:
     """nn.ConvTranspose2d(k=4, s=2) weight (Cin, Cout, 4, 4) -> 4 packed 2x2 phase convs."""
     w = w.detach().contiguous()
     Cin, Cout = w.shape[0], w.shape[1]
-    n = lib.nps_conv2d_packed_size(Cout, Cin, 4)
-    outs = []
-    for ph in range(4):
-        out = torch.empty(n, dtype=torch.float32, device=w.device)
-        check(lib.nps_conv2d_pack_weights(ptr(w), ptr(out), Cout, Cin, 2, 2, ph, stream_ptr()), "pack convT")
-        outs.append(out)
-    return outs
+    return [_pack(w, Cout, Cin, 2, 2, ph, conv_precision(2, 2)) for ph in range(4)]
 
 
 def pack_spectral_weight(w1: torch.Tensor, w2: torch.Tensor, H: int) -> torch.Tensor:
@@ -122,7 +133,8 @@ def group_norm_stats(srcs: Sequence[Src], frame_hw, groups: int) -> torch.Tensor
 def conv2d(srcs: Sequence[Src], frame_hw, wpack: torch.Tensor, bias: Optional[torch.Tensor], Cout: int, KH: int,
            KW: int, stride=1, dil=1, pad=(0, 0), circ=0, out_hw=None, gn: Optional[GN] = None, pre_act=0,
            out: Optional[torch.Tensor] = None, out_nchw=False, out_os=1, out_off=(0, 0), accumulate=False,
-           addends: Sequence[torch.Tensor] = (), act=0, add_after_act=False, pad_bottom=None):
+           addends: Sequence[torch.Tensor] = (), act=0, add_after_act=False, pad_bottom=None,
+           in_scale: Optional[torch.Tensor] = None):
     """One fused conv launch.  `pad` = top/left zero padding (in the circularly
     extended frame), `pad_bottom` defaults to `pad`.  Returns `out`."""
     t0 = srcs[0].t
@@ -168,6 +180,9 @@ def conv2d(srcs: Sequence[Src], frame_hw, wpack: torch.Tensor, bias: Optional[to
     a.addend0 = ptr(ads[0]) if len(ads) > 0 else None
     a.addend1 = ptr(ads[1]) if len(ads) > 1 else None
     a.act, a.add_after_act = act, (1 if add_after_act else 0)
+    a.precision = getattr(wpack, "nps_precision", PREC_F32)
+    if in_scale is not None and a.precision == PREC_X3F16:
+        a.in_scale = ptr(in_scale)
     if lib.nps_conv2d_plan(ctypes_byref(a)) < 0:
         raise RuntimeError("conv2d_plan failed: " + lib.nps_last_error().decode())
     if conv_probe is not None:
@@ -175,9 +190,19 @@ def conv2d(srcs: Sequence[Src], frame_hw, wpack: torch.Tensor, bias: Optional[to
         e0.record()
         check(lib.nps_conv2d_fwd(ctypes_byref(a), stream_ptr()), "conv2d_fwd")
         e1.record()
-        conv_probe.append((e0, e1, 2.0 * B * Hout * Wout * Cout * Cin * KH * KW))
+        nbytes = 4.0 * (sum(s.t.numel() for s in srcs) + Cout * Cin * KH * KW + B * Hout * Wout * Cout)
+        conv_probe.append((e0, e1, 2.0 * B * Hout * Wout * Cout * Cin * KH * KW,
+                           ("x3f16" if a.precision == PREC_X3F16 else "f32", KH * KW, a.waves), nbytes))
     else:
         check(lib.nps_conv2d_fwd(ctypes_byref(a), stream_ptr()), "conv2d_fwd")
+    return out
+
+
+def absmax(x: torch.Tensor) -> torch.Tensor:
+    """(1,) fp32 device tensor max|x| — the input range for a split-fp16 conv (conv2d(in_scale=...))."""
+    x = x.contiguous()
+    out = torch.empty(1, dtype=torch.float32, device=x.device)
+    check(lib.nps_absmax(ptr(x), x.numel(), ptr(out), stream_ptr()), "absmax")
     return out
 
 

@@ -28,13 +28,15 @@ def main():
     ap.add_argument("--gn", type=int, default=1)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--check", action="store_true")
+    ap.add_argument("--prec", default="x3f16", choices=["x3f16", "f32"])
     a = ap.parse_args()
+    ops.CONV_PRECISION = ops.PREC_F32 if a.prec == "f32" else ops.PREC_X3F16
     dev = "cuda"
     torch.manual_seed(0)
     x = torch.randn(a.b, a.hw, a.hw, a.cin, device=dev)
     w = torch.randn(a.cout, a.cin, a.k, a.k, device=dev) * (1.0 / (a.cin * a.k * a.k) ** 0.5)
     bias = torch.randn(a.cout, device=dev)
-    wp = ops.pack_conv_weight(w)
+    wp = ops.pack_conv_weight(w, a.stride, a.dil)
     gn = None
     if a.gn:
         st = ops.group_norm_stats([ops.Src(x)], (a.hw, a.hw), 1)
@@ -51,7 +53,7 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / a.iters
-    print(f"conv cin={a.cin} cout={a.cout} k={a.k} d={a.dil} s={a.stride} hw={a.hw} B={a.b} gn={a.gn}: "
+    print(f"conv[{a.prec}] cin={a.cin} cout={a.cout} k={a.k} d={a.dil} s={a.stride} hw={a.hw} B={a.b} gn={a.gn}: "
           f"{ms:.3f} ms  {flops / ms / 1e9:.1f} TFLOP/s  ({flops / ms / 1e9 / 157.3 * 100:.1f}% of fp32 MFMA peak)")
     if a.check:
         import torch.nn.functional as F

@@ -7,6 +7,6 @@ for P in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INS
          "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD" \
          "TCC_HIT_sum TCC_MISS_sum" "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
-  timeout -k 10 120 rocprofv3 --pmc $P --output-format csv -d gpurun_out/pmc_$i -o run -- python tools/conv_bench.py --iters 2 $ARGS > gpurun_out/pmc_$i.log 2>&1 || { echo "pass $i failed"; exit 1; }
+  timeout -k 10 120 rocprofv3 --pmc $P --output-format csv -d gpurun_out/pmc_$i -o run -- python3 tools/conv_bench.py --iters 2 $ARGS > gpurun_out/pmc_$i.log 2>&1 || { echo "pass $i failed"; exit 1; }
 done
 echo pmc done
