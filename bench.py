@@ -67,9 +67,10 @@ def build_model(kind, res, num_c, device, fno_modes=None, seed=42):
 # dense MFMA peaks, MI355X_MICROARCH.md: f32 (v_mfma_f32_32x32x2_f32) 157.3 TF; f16 2.5 PF.  A split-fp16
 # conv spends 3 f16 MFMA products per algorithmic fp32 product, so its fp32-equivalent ceiling is 2.5 PF / 3.
 PEAK_TFLOPS = {"f32": FP32_MFMA_PEAK_TFLOPS, "x3f16": 2500.0 / 3.0}
-KERNEL_NAMES = {("x3f16", 9): "conv2d_pc_kernel<9,16,*,2,1,true> (3x3, split-fp16 MFMA)",
-                ("x3f16", 4): "conv2d_pc_kernel<4,16,*,2,1,true> (2x2 phase / space-to-depth, split-fp16 MFMA)",
-                ("f32", 1): "conv2d_pc_kernel<1,32,2,3,2,false> (1x1, f32 MFMA)"}
+KERNEL_NAMES = {("x3f16", 9): "conv2d_x3_kernel<9,*> (3x3, split-fp16 MFMA)",
+                ("x3f16", 4): "conv2d_x3_kernel<4,*> (2x2 phase / space-to-depth, split-fp16 MFMA)",
+                ("x3f16", 1): "conv2d_x3_kernel<1,*> (1x1, split-fp16 MFMA)",
+                ("f32", 1): "conv2d_pc_kernel<1,32,2,3,2> (1x1, f32 MFMA)"}
 
 
 def conv_roofline(model, x, cond, pos, sc):
@@ -119,10 +120,10 @@ def attach_traffic(roof):
             pmc = json.load(f)
     except (OSError, ValueError):
         return roof
-    for name, rec in pmc.get("kernels", {}).items():
-        if rec.get("class") == f"{roof['arithmetic']}_{roof['kernel'].split('<')[1].split(',')[0]}tap":
-            roof["traffic"] = rec["hbm_bytes_per_launch"]
-            roof["traffic_source"] = f"{os.path.relpath(PMC_FILE, ROOT)} ({pmc.get('command', '')})"
+    rec = pmc.get("classes", {}).get(f"{roof['arithmetic']}_{roof['kernel'].split('<')[1].split(',')[0]}tap")
+    if rec:
+        roof["traffic"] = rec["hbm_bytes_per_launch"]
+        roof["traffic_source"] = f"{os.path.relpath(PMC_FILE, ROOT)} ({pmc.get('command', '')})"
     return roof
 
 

@@ -83,9 +83,10 @@ typedef struct {
     /* tiling, chosen by nps_conv2d_plan() */
     int TH, TW, lattice, waves;
     /* arithmetic: NPS_PREC_F32 = exact fp32 MFMA (v_mfma_f32_32x32x2_f32); NPS_PREC_X3F16 = 3-pass
-     * split fp16 (x = hi + 2^-11 lo, products hi*hi + 2^-11 (hi*lo + lo*hi) on v_mfma_f32_32x32x16_f16,
-     * fp32 accumulate, ~2^-22 relative per product) — only where nps_conv2d_x3_eligible(), with the
-     * weight packed by nps_conv2d_pack_weights_x3 */
+     * split fp16 (x = hi + lo, products hi*hi + hi*lo + lo*hi on v_mfma_f32_32x32x16_f16, fp32
+     * accumulate, ~2^-21 relative per product; weights pre-scaled by an exact power of 2) — only where
+     * nps_conv2d_x3_eligible() and nps_conv2d_x3_sources_ok(), with the weight packed by
+     * nps_conv2d_pack_weights_x3 */
     int precision;
     /* NPS_PREC_X3F16 only: device pointer to max|input| (nps_absmax) or NULL; the input is scaled by an
      * exact power of 2 into fp16's normal range before the split and the result scaled back
@@ -111,8 +112,11 @@ int nps_conv2d_pack_weights(const float* w, float* wpack, int Cout, int Cin, int
  * (same buffer size as nps_conv2d_packed_size). */
 int nps_conv2d_pack_weights_x3(const float* w, float* wpack, int Cout, int Cin, int KH, int KW,
                                int transposed_phase, void* stream);
-/* 1 when a conv of this geometry runs on the split-fp16 kernel (stride-1, undilated 2x2 / 3x3). */
+/* 1 when a conv of this geometry runs on the split-fp16 kernel (stride-1, undilated 1x1 / 2x2 / 3x3). */
 int nps_conv2d_x3_eligible(int KH, int KW, int stride, int dil);
+/* 1 when the split-fp16 kernel can stage this virtual frame directly: every source boundary on a
+ * multiple of 16 channels, every source's C a multiple of 4 (otherwise nps_frame_pack it first). */
+int nps_conv2d_x3_sources_ok(const nps_src_t* src, int nsrc);
 /* *out = max |x[i]| (the input range a split-fp16 conv scales by, nps_conv2d_t.in_scale) */
 int nps_absmax(const float* x, long n, float* out, void* stream);
 /* Stride-2 3x3 convs (U-Net Downsample, proc_unet_modern.py:445-455) run as 2x2 stride-1 convs

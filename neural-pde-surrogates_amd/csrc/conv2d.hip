@@ -20,147 +20,10 @@
 //   * Dilated convs tile the output on the dilation lattice ("lattice" mode),
 //     so the LDS patch is (TH+KH-1) x (TW+KW-1) instead of growing with d.
 //   * Patch double-buffered in LDS; one barrier per 16-channel chunk.
-#include "nps_common.hpp"
+
+#include "conv2d_common.hpp"
 
 namespace {
-
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
-
-constexpr int CK = 16;          // input channels per K chunk
-constexpr float X3_SCALE = 2048.f;        // lo part of the fp16 split is stored scaled by 2^11 (stays normal)
-constexpr float X3_INV = 1.f / 2048.f;
-constexpr int PIXS = CK + 4;    // LDS floats per patch pixel (+4 pad: conflict-free ds_read_b128)
-constexpr int MAXL = 12;        // max float4 patch loads per thread per chunk
-
-// 32-channel output blocks in the packed weight layout: a multiple of 6 so both the 64-co (2-block)
-// and the 192-co (6-block) work-group tiles index inside the buffer
-__host__ __device__ inline int packed_ncb(int Cout) { return 6 * ((Cout + 191) / 192); }
-
-struct Geo {
-    int T, ri, rk, rstep, PH, PW, tiles_x, tiles_y;
-};
-
-__host__ __device__ inline Geo make_geo(const nps_conv2d_t& a) {
-    Geo g;
-    g.T = a.lattice ? a.dil : 1;
-    g.ri = a.lattice ? 1 : a.stride;
-    g.rk = a.lattice ? 1 : a.dil;
-    g.rstep = a.lattice ? a.dil : 1;
-    g.PH = (a.TH - 1) * g.ri + (a.KH - 1) * g.rk + 1;
-    g.PW = (a.TW - 1) * g.ri + (a.KW - 1) * g.rk + 1;
-    const int ny = (a.Hout + g.T - 1) / g.T, nx = (a.Wout + g.T - 1) / g.T;
-    g.tiles_y = g.T * ((ny + a.TH - 1) / a.TH);
-    g.tiles_x = g.T * ((nx + a.TW - 1) / a.TW);
-    return g;
-}
-
-// Fetch 4 consecutive virtual channels [c, c+4) at virtual-frame position (y, x) of sample b.
-// Written without loops over a.src[] (explicitly per source) so the kernarg struct is never indexed
-// dynamically — a dynamic index makes the compiler copy the whole struct to scratch.
-__device__ __forceinline__ bool fetch4_fast(const nps_src_t& S, int lo, int b, int y, int x, int c, f32x4& v) {
-    const int hi = lo + S.C;
-    if (c >= lo && c + 4 <= hi && ((c - lo) & 3) == 0 && (S.C & 3) == 0) {
-        const int yy = y - S.off_y, xx = x - S.off_x;
-        if (yy >= 0 && yy < S.H && xx >= 0 && xx < S.W)
-            v = *reinterpret_cast<const f32x4*>(S.ptr + ((size_t)(b * S.H + yy) * S.W + xx) * S.C + (c - lo));
-        return true;
-    }
-    return false;
-}
-
-__device__ __forceinline__ float fetch1(const nps_src_t& S, int lo, int b, int y, int x, int ce) {
-    if (ce >= lo && ce < lo + S.C) {
-        const int yy = y - S.off_y, xx = x - S.off_x;
-        if (yy >= 0 && yy < S.H && xx >= 0 && xx < S.W)
-            return S.ptr[((size_t)(b * S.H + yy) * S.W + xx) * S.C + (ce - lo)];
-    }
-    return 0.f;
-}
-
-__device__ __forceinline__ f32x4 fetch4(const nps_conv2d_t& a, int b, int y, int x, int c) {
-    f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    const int lo1 = a.src[0].C, lo2 = a.src[0].C + a.src[1].C;
-    if (fetch4_fast(a.src[0], 0, b, y, x, c, v)) return v;
-    if (a.nsrc > 1 && fetch4_fast(a.src[1], lo1, b, y, x, c, v)) return v;
-    if (a.nsrc > 2 && fetch4_fast(a.src[2], lo2, b, y, x, c, v)) return v;
-    // general path: per-channel gather (sources with C % 4 != 0, straddling chunks)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        const int ce = c + e;
-        float r = fetch1(a.src[0], 0, b, y, x, ce);
-        if (a.nsrc > 1 && ce >= lo1) r = fetch1(a.src[1], lo1, b, y, x, ce);
-        if (a.nsrc > 2 && ce >= lo2) r = fetch1(a.src[2], lo2, b, y, x, ce);
-        v[e] = r;
-    }
-    return v;
-}
-
-// Epilogue of one 32x32 accumulator tile for this lane's output pixel (dy, dx): the lane holds
-// co = co_base + 8m + 4h + e (m, e < 4).  NHWC outputs with 4-aligned channels take a
-// vectorised path: all loads of the tile (bias, addends, accumulate source) are issued before
-// any store, then 16-B stores.  Order of the float ops matches the reference:
-// act(acc + bias + addends) or act(acc + bias) + addends, then + out when accumulating.
-__device__ __forceinline__ void store_tile(const nps_conv2d_t& a, int b, int co_base, int h, const f32x16& acc,
-                                           int dy, int dx) {
-    if (!a.out_nchw && (a.out_C & 3) == 0 && (a.Cout & 3) == 0) {
-        const size_t base = (((size_t)b * a.out_H + dy) * a.out_W + dx) * a.out_C;
-        f32x4 bi[4], a0[4], a1[4], o[4];
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-            const int co0 = co_base + 8 * m + 4 * h;
-            const bool ok = co0 < a.Cout;
-            const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-            bi[m] = (ok && a.bias) ? *reinterpret_cast<const f32x4*>(a.bias + co0) : z;
-            a0[m] = (ok && a.addend0) ? *reinterpret_cast<const f32x4*>(a.addend0 + base + co0) : z;
-            a1[m] = (ok && a.addend1) ? *reinterpret_cast<const f32x4*>(a.addend1 + base + co0) : z;
-            o[m] = (ok && a.accumulate) ? *reinterpret_cast<const f32x4*>(a.out + base + co0) : z;
-        }
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-            const int co0 = co_base + 8 * m + 4 * h;
-            if (co0 >= a.Cout) continue;
-            f32x4 r;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                float v = acc[4 * m + e] + bi[m][e];
-                if (!a.add_after_act) v = v + a0[m][e] + a1[m][e];
-                if (a.act == 1) v = nps::gelu_erf(v);
-                if (a.add_after_act) v = v + a0[m][e] + a1[m][e];
-                if (a.accumulate) v += o[m][e];
-                r[e] = v;
-            }
-            *reinterpret_cast<f32x4*>(a.out + base + co0) = r;
-        }
-        return;
-    }
-    // generic path: element address linear in co (NHWC stride 1, NCHW stride H*W)
-    const size_t base = a.out_nchw ? (((size_t)b * a.out_C) * a.out_H + dy) * a.out_W + dx
-                                   : (((size_t)b * a.out_H + dy) * a.out_W + dx) * a.out_C;
-    const size_t cstride = a.out_nchw ? (size_t)a.out_H * a.out_W : 1;
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int co = co_base + 8 * m + 4 * h + e;
-            if (co >= a.Cout) continue;
-            const size_t di = base + (size_t)co * cstride;
-            float v = acc[4 * m + e];
-            if (a.bias) v += a.bias[co];
-            if (!a.add_after_act) {
-                if (a.addend0) v += a.addend0[di];
-                if (a.addend1) v += a.addend1[di];
-            }
-            if (a.act == 1) v = nps::gelu_erf(v);
-            if (a.add_after_act) {
-                if (a.addend0) v += a.addend0[di];
-                if (a.addend1) v += a.addend1[di];
-            }
-            if (a.accumulate) v += a.out[di];
-            a.out[di] = v;
-        }
-    }
-}
 
 template <int WAVES>
 __global__ __launch_bounds__(WAVES * 64) void conv2d_fwd_kernel(const nps_conv2d_t a) {
@@ -359,36 +222,9 @@ __host__ __device__ constexpr int pc_patch_px_max(int ntaps, int tile_px) {
     return ntaps == 1 ? tile_px : (tile_px == 256 ? (ntaps == 4 ? 297 : 340) : (ntaps == 4 ? 153 : 180));
 }
 
-// fp32 -> (hi, lo * 2^11) fp16 split of 4 values (round-toward-zero packing: |x - hi| < ulp(hi), and
-// the scaled residual is again exact to 11 bits, so hi + lo * 2^-11 carries ~22 bits of x)
-// Power-of-2 input scale of a split-fp16 conv: maps max|x| (a.in_scale = device pointer to it, from
-// nps_absmax) into [2^13, 2^14) so every element within 2^-27 of the maximum keeps both fp16 halves
-// normal (gradients can be ~1e-8 in magnitude); 1 when no range is given.
-__device__ __forceinline__ float in_scale_of(const nps_conv2d_t& a) {
-    if (a.in_scale == nullptr) return 1.f;
-    const float m = *a.in_scale;
-    if (!(m > 0.f) || !(m < 3.0e38f)) return 1.f;
-    return ldexpf(1.f, 13 - ilogbf(m));
-}
-
-typedef _Float16 h2f __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ h2f pkrtz(float a, float b) { return __builtin_bit_cast(h2f, __builtin_amdgcn_cvt_pkrtz(a, b)); }
-
-__device__ __forceinline__ void split4(const f32x4 v, f16x4& hi, f16x4& lo) {
-    const h2f h01 = pkrtz(v[0], v[1]);
-    const h2f h23 = pkrtz(v[2], v[3]);
-    const h2f l01 = pkrtz((v[0] - (float)h01[0]) * X3_SCALE, (v[1] - (float)h01[1]) * X3_SCALE);
-    const h2f l23 = pkrtz((v[2] - (float)h23[0]) * X3_SCALE, (v[3] - (float)h23[1]) * X3_SCALE);
-    hi = f16x4{h01[0], h01[1], h23[0], h23[1]};
-    lo = f16x4{l01[0], l01[1], l23[0], l23[1]};
-}
-
-// X3 = false: exact fp32 (v_mfma_f32_32x32x2_f32).  X3 = true: 3-pass split-fp16 products
-// (v_mfma_f32_32x32x16_f16: hi*hi into one accumulator, hi*lo + lo*hi into a second, combined as
-// acc_hh + 2^-11 acc_x in the epilogue) — ~2^-22 relative per product at 5.3x the f32 MFMA rate.
-// The LDS stage has the same bytes either way: per pixel and 16-channel sub-chunk, 16 fp32 or
-// [16 hi | 16 lo] fp16; the packed weights are fp32 fragments or [hi | lo] fp16 fragments.
-template <int NTAPS, int CKB, int PB, int CBW, int WCO, bool X3>
+// Exact-fp32 producer/consumer kernel (v_mfma_f32_32x32x2_f32): the 1x1 / 2x2 / 3x3 convs under
+// NPS_PREC_F32.
+template <int NTAPS, int CKB, int PB, int CBW, int WCO>
 __global__ __launch_bounds__(512) void conv2d_pc_kernel(const nps_conv2d_t a) {
     constexpr int KWT = NTAPS == 9 ? 3 : (NTAPS == 4 ? 2 : 1);
     constexpr int SUB = CKB / CK;                       // 16-channel sub-chunks per stage
@@ -501,7 +337,6 @@ __global__ __launch_bounds__(512) void conv2d_pc_kernel(const nps_conv2d_t a) {
                 }
             }
         };
-        const float xs = X3 ? in_scale_of(a) : 1.f;  // exact power-of-2 range scaling of the input
         auto commit = [&](int buf, const f32x4 (&ra)[NAP], const f32x4 (&rp)[MAXP]) {  // LDS store of a stage
             float* A = ring + buf * stage_fl;
             float* Pt = A + AFL;
@@ -512,32 +347,17 @@ __global__ __launch_bounds__(512) void conv2d_pc_kernel(const nps_conv2d_t a) {
                 const int idx = ptid + k * 256;
                 if (idx < NG) {
                     const int p = idx / (CKB / 4), gq = idx - p * (CKB / 4);
-                    if constexpr (X3) {
-                        // channel c = 4 gq: sub-chunk c / 16 at 16 floats (= 32 halves) per sub-chunk
-                        f16x4 hi, lo;
-                        split4(rp[k] * xs, hi, lo);
-                        _Float16* base = reinterpret_cast<_Float16*>(Pt + p * PIXSB + (gq >> 2) * 16) + (gq & 3) * 4;
-                        *reinterpret_cast<f16x4*>(base) = hi;
-                        *reinterpret_cast<f16x4*>(base + 16) = lo;
-                    } else {
-                        *reinterpret_cast<f32x4*>(Pt + p * PIXSB + gq * 4) = rp[k];
-                    }
+                    *reinterpret_cast<f32x4*>(Pt + p * PIXSB + gq * 4) = rp[k];
                 }
             }
         };
-#ifndef NPS_ABLATE_PRODUCER
         issue(0, ra, rp);
         commit(0, ra, rp);
         if (nstages > 1) issue(1, ra1, rp1);
         if (nstages > 2) issue(2, ra, rp);
-#endif
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         for (int st = 0; st < nstages; ++st) {
-#ifdef NPS_ABLATE_PRODUCER
-            if (false) {
-#else
             if (st + 1 < nstages) {
-#endif
                 if ((st + 1) & 1) {
                     commit(1, ra1, rp1);
                     if (st + 3 < nstages) issue(st + 3, ra1, rp1);
@@ -561,92 +381,16 @@ __global__ __launch_bounds__(512) void conv2d_pc_kernel(const nps_conv2d_t a) {
         boff[pb] = (ti * g.PW + tj) * PIXSB + (lane >> 5) * 8;
     }
     f32x16 acc[CBW][PB];
-    f32x16 accx[X3 ? CBW : 1][X3 ? PB : 1];
 #pragma unroll
     for (int i = 0; i < CBW; ++i)
 #pragma unroll
         for (int j = 0; j < PB; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    if constexpr (X3) {
-#pragma unroll
-        for (int i = 0; i < CBW; ++i)
-#pragma unroll
-            for (int j = 0; j < PB; ++j)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) accx[i][j][r] = 0.f;
-    }
-
     // Operands of K-group gi = (sub, tap, q) are read one group ahead into a second register set,
     // so every group's 8*PB MFMAs (>= 512 cycles) cover the LDS latency of the next group's reads.
     constexpr int G = SUB * NTAPS * 2;
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if constexpr (X3) {
-        const float inv_xs = 1.f / in_scale_of(a);
-        // K-group = (sub, tap): 16 channels, lane half h holds channels 8h..8h+7 (one b128 per operand
-        // half); A fragment = 2 KiB [hi: 64 lanes x 16 B | lo: 64 lanes x 16 B]
-        constexpr int GX = SUB * NTAPS;
-        int boffx[PB];
-#pragma unroll
-        for (int pb = 0; pb < PB; ++pb) {
-            const int P = wpx * 32 * PB + pb * 32 + (lane & 31);
-            const int ti = P / a.TW, tj = P - (P / a.TW) * a.TW;
-            boffx[pb] = (ti * g.PW + tj) * PIXSB * 4 + (lane >> 5) * 16;  // bytes
-        }
-        for (int st = 0; st < nstages; ++st) {
-            const char* A = reinterpret_cast<const char*>(ring + (st & 1) * stage_fl);
-            const char* Pt = A + AFL * 4;
-            f16x8 ah[2][CBW], al[2][CBW], bh[2][PB], bl[2][PB];
-            auto load_group = [&](int gi, f16x8 (&adh)[CBW], f16x8 (&adl)[CBW], f16x8 (&bdh)[PB], f16x8 (&bdl)[PB]) {
-                const int sub = gi / NTAPS, tap = gi - sub * NTAPS;
-                const int ky = tap / KWT, kx = tap % KWT;
-                const int toff = (ky * g.PW + kx) * PIXSB * 4 + sub * 64;
-#pragma unroll
-                for (int cb = 0; cb < CBW; ++cb) {
-                    const char* ab = A + ((sub * NTAPS + tap) * NCBG + wco * CBW + cb) * 2048 + lane * 16;
-                    adh[cb] = *reinterpret_cast<const f16x8*>(ab);
-                    adl[cb] = *reinterpret_cast<const f16x8*>(ab + 1024);
-                }
-#pragma unroll
-                for (int pb = 0; pb < PB; ++pb) {
-                    bdh[pb] = *reinterpret_cast<const f16x8*>(Pt + boffx[pb] + toff);
-                    bdl[pb] = *reinterpret_cast<const f16x8*>(Pt + boffx[pb] + toff + 32);
-                }
-            };
-#ifndef NPS_ABLATE_CONSUMER
-            load_group(0, ah[0], al[0], bh[0], bl[0]);
-#pragma unroll
-            for (int gi = 0; gi < GX; ++gi) {
-                const int cur = gi & 1;
-                if (gi + 1 < GX) load_group(gi + 1, ah[cur ^ 1], al[cur ^ 1], bh[cur ^ 1], bl[cur ^ 1]);
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int cb = 0; cb < CBW; ++cb)
-#pragma unroll
-                    for (int pb = 0; pb < PB; ++pb)
-                        acc[cb][pb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[cur][cb], bh[cur][pb], acc[cb][pb], 0, 0, 0);
-#pragma unroll
-                for (int cb = 0; cb < CBW; ++cb)
-#pragma unroll
-                    for (int pb = 0; pb < PB; ++pb)
-                        accx[cb][pb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[cur][cb], bl[cur][pb], accx[cb][pb], 0, 0, 0);
-#pragma unroll
-                for (int cb = 0; cb < CBW; ++cb)
-#pragma unroll
-                    for (int pb = 0; pb < PB; ++pb)
-                        accx[cb][pb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[cur][cb], bh[cur][pb], accx[cb][pb], 0, 0, 0);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-#endif
-            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        }
-#pragma unroll
-        for (int i = 0; i < CBW; ++i)
-#pragma unroll
-            for (int j = 0; j < PB; ++j)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) acc[i][j][r] = fmaf(accx[i][j][r], X3_INV, acc[i][j][r]) * inv_xs;
-    } else
     for (int st = 0; st < nstages; ++st) {
         const float* A = ring + (st & 1) * stage_fl;
         const float* Pt = A + AFL;
@@ -663,7 +407,6 @@ __global__ __launch_bounds__(512) void conv2d_pc_kernel(const nps_conv2d_t a) {
 #pragma unroll
             for (int pb = 0; pb < PB; ++pb) bd[pb] = *reinterpret_cast<const f32x4*>(Pt + boff[pb] + toff + q * 4);
         };
-#ifndef NPS_ABLATE_CONSUMER
         load_group(0, av[0], bv[0]);
 #pragma unroll
         for (int gi = 0; gi < G; ++gi) {
@@ -679,7 +422,6 @@ __global__ __launch_bounds__(512) void conv2d_pc_kernel(const nps_conv2d_t a) {
                         acc[cb][pb] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[cur][cb][e], bv[cur][pb][e], acc[cb][pb], 0, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
         }
-#endif
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
 
@@ -741,9 +483,10 @@ __global__ void pack_weights_kernel(const float* __restrict__ w, float* __restri
 }
 
 // Packed layout (3-pass split fp16, same bytes): [chunk][tap][cb][hl (2)][lane (64)][8 halves]
-// element j of lane = (hi | lo * 2^11) of w[co = cb*32 + (lane&31)][ci = chunk*16 + (lane>>5)*8 + j][tap]
+// element j of lane = (hi | lo) of s * w[co = cb*32 + (lane&31)][ci = chunk*16 + (lane>>5)*8 + j][tap],
+// s = pow2_scale_for(max|w|) (max|w| is in the buffer's trailer, written by nps_absmax beforehand)
 __global__ void pack_weights_x3_kernel(const float* __restrict__ w, _Float16* __restrict__ wp, int Cout, int Cin,
-                                       int KH, int KW, int tphase, size_t total_pairs) {
+                                       int KH, int KW, int tphase, size_t total_pairs, const float* __restrict__ wmax) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // (hi, lo) pair index
     if (i >= total_pairs) return;
     const int ntaps = KH * KW;
@@ -754,20 +497,17 @@ __global__ void pack_weights_x3_kernel(const float* __restrict__ w, _Float16* __
     const int cb = r % ncb; r /= ncb;
     const int tap = r % ntaps; r /= ntaps;
     const int chunk = (int)r;
-    const float v = weight_elem(w, Cout, Cin, KH, KW, tphase, cb * 32 + (lane & 31), chunk * CK + (lane >> 5) * 8 + j,
-                                tap);
+    const float v = pow2_scale_for(*wmax) *
+                    weight_elem(w, Cout, Cin, KH, KW, tphase, cb * 32 + (lane & 31), chunk * CK + (lane >> 5) * 8 + j, tap);
     const size_t frag = i >> 9;  // (chunk, tap, cb) fragment of 64 lanes x 8
     const size_t o = frag * 1024 + (size_t)lane * 8 + j;
     const h2f hv = pkrtz(v, 0.f);
-    const h2f lv = pkrtz((v - (float)hv[0]) * X3_SCALE, 0.f);
+    const h2f lv = pkrtz(v - (float)hv[0], 0.f);
     wp[o] = hv[0];
     wp[o + 512] = lv[0];
 }
 
-size_t packed_size(int Cout, int Cin, int ntaps) {
-    const size_t nchunks = (Cin + CK - 1) / CK, ncb = packed_ncb(Cout);
-    return nchunks * ntaps * ncb * 2 * 64 * 4;
-}
+size_t packed_size(int Cout, int Cin, int ntaps) { return packed_body(Cout, Cin, ntaps) + PACK_TRAILER; }
 
 bool pc_eligible(const nps_conv2d_t& a) {
     const int nt = a.KH * a.KW;
@@ -776,11 +516,9 @@ bool pc_eligible(const nps_conv2d_t& a) {
            a.pre_act == 0;
 }
 
-// 3-pass split-fp16 variant: stride-1 2x2 / 3x3 producer/consumer convs (1x1s stay exact f32)
-bool x3_eligible(const nps_conv2d_t& a) {
-    const int nt = a.KH * a.KW;
-    return pc_eligible(a) && (nt == 4 || nt == 9);
-}
+// 3-pass split-fp16 kernel: every stride-1 undilated 1x1 / 2x2 / 3x3 conv without a prologue
+bool x3_eligible(const nps_conv2d_t& a) { return pc_eligible(a); }
+
 
 // producer/consumer variant per tap count: 1x1 convs use 192-channel x 128-pixel work-groups
 // (the input is streamed once); 2x2 / 3x3 use 64 x 256 (or 64 x 128) so the weight tile of a
@@ -797,7 +535,7 @@ int pc_lds_bytes(const nps_conv2d_t& a) {
 }
 
 int lds_bytes(const nps_conv2d_t& a) {
-    if (a.waves == 8) return pc_lds_bytes(a);
+    if (a.waves == 8) return a.precision == NPS_PREC_X3F16 ? x3_lds_bytes(a) : pc_lds_bytes(a);
     const Geo g = make_geo(a);
     const int bufsz = ((g.PH * g.PW * PIXS + 3) & ~3);
     return (32 + 2 * bufsz) * 4;
@@ -813,7 +551,7 @@ extern "C" int nps_conv2d_pack_weights(const float* w, float* wpack, int Cout, i
     NPS_CHECK_ARG(transposed_phase == -1 || ((transposed_phase == -2 || (transposed_phase >= 0 && transposed_phase < 4)) &&
                                              KH == 2 && KW == 2 && (transposed_phase != -2 || Cin % 4 == 0)),
                   "conv2d_pack_weights: phase / space-to-depth packing needs KH=KW=2");
-    const size_t total = packed_size(Cout, Cin, KH * KW);
+    const size_t total = packed_body(Cout, Cin, KH * KW);
     const int bs = 256;
     pack_weights_kernel<<<(unsigned)((total + bs - 1) / bs), bs, 0, (hipStream_t)stream>>>(w, wpack, Cout, Cin, KH, KW,
                                                                                         transposed_phase, total);
@@ -827,12 +565,23 @@ extern "C" int nps_conv2d_pack_weights_x3(const float* w, float* wpack, int Cout
     NPS_CHECK_ARG(transposed_phase == -1 || ((transposed_phase == -2 || (transposed_phase >= 0 && transposed_phase < 4)) &&
                                              KH == 2 && KW == 2 && (transposed_phase != -2 || Cin % 4 == 0)),
                   "conv2d_pack_weights_x3: phase / space-to-depth packing needs KH=KW=2");
-    const size_t pairs = packed_size(Cout, Cin, KH * KW);  // one (hi, lo) pair per fp32 slot
+    const size_t pairs = packed_body(Cout, Cin, KH * KW);  // one (hi, lo) pair per fp32 slot
+    float* wmax = wpack + pairs;                             // trailer[0]
+    const long nw = transposed_phase == -1 ? (long)Cout * Cin * KH * KW
+                                           : (transposed_phase == -2 ? (long)Cout * (Cin / 4) * 9 : (long)Cout * Cin * 16);
+    if (nps_absmax(w, nw, wmax, stream) != 0) return -2;
     const int bs = 256;
     pack_weights_x3_kernel<<<(unsigned)((pairs + bs - 1) / bs), bs, 0, (hipStream_t)stream>>>(
-        w, reinterpret_cast<_Float16*>(wpack), Cout, Cin, KH, KW, transposed_phase, pairs);
+        w, reinterpret_cast<_Float16*>(wpack), Cout, Cin, KH, KW, transposed_phase, pairs, wmax);
     NPS_CHECK_LAUNCH("conv2d_pack_weights_x3");
     return 0;
+}
+
+extern "C" int nps_conv2d_x3_sources_ok(const nps_src_t* src, int nsrc) {
+    nps_conv2d_t t = {};
+    t.nsrc = nsrc;
+    for (int i = 0; i < nsrc && i < NPS_MAX_SRC; ++i) t.src[i] = src[i];
+    return nsrc >= 1 && nsrc <= NPS_MAX_SRC && x3_sources_aligned(t) ? 1 : 0;
 }
 
 extern "C" int nps_conv2d_x3_eligible(int KH, int KW, int stride, int dil) {
@@ -849,6 +598,36 @@ extern "C" int nps_conv2d_plan(nps_conv2d_t* a) {
     // dilated stride-1 convs tile on the dilation lattice (patch independent of d)
     a->lattice = (a->dil > 1 && a->stride == 1) ? 1 : 0;
     const long units_co = (a->Cout + 63) / 64;
+    if (a->precision == NPS_PREC_X3F16 && x3_eligible(*a)) {
+        // split-fp16 kernel: 512-pixel tiles (16x32, 32x16, 8x64) or 256-pixel ones (16x16, 8x32),
+        // scored by the useful fraction of the launched pixels x the fill of the last round of
+        // work-groups over the 256 CUs; 256-pixel tiles carry a 10 % penalty (half the reuse of
+        // each weight fragment per global load)
+        const int cand[5][2] = {{16, 32}, {32, 16}, {8, 64}, {16, 16}, {8, 32}};
+        int best = -1;
+        double best_eff = -1.0;
+        for (int i = 0; i < 5; ++i) {
+            nps_conv2d_t t = *a;
+            t.waves = 8;
+            t.TH = cand[i][0];
+            t.TW = cand[i][1];
+            if (x3_lds_bytes(t) > 160 * 1024) continue;
+            const Geo g = make_geo(t);
+            const long wgs = (long)g.tiles_x * g.tiles_y * a->B * units_co;
+            const double useful = (double)a->Hout * a->Wout * a->B * units_co / ((double)wgs * t.TH * t.TW);
+            const long rounds = (wgs + 255) / 256;
+            const double fill = (double)wgs / (double)(rounds * 256);
+            const double eff = useful * fill * (t.TH * t.TW == 512 ? 1.0 : 0.9);
+            if (eff > best_eff) {
+                best_eff = eff;
+                best = i;
+            }
+        }
+        a->waves = 8;
+        a->TH = cand[best][0];
+        a->TW = cand[best][1];
+        return x3_lds_bytes(*a);
+    }
     if (pc_eligible(*a)) {
         // producer/consumer kernel: 256-pixel tiles (16x16 or 8x32, whichever wastes less of the
         // output edge); 128-pixel 8x16 tiles only when the 256-pixel grid cannot give every CU a
@@ -915,23 +694,22 @@ extern "C" int nps_conv2d_plan(nps_conv2d_t* a) {
 }
 
 namespace {
-template <int NT, int CKB, int PB, int CBW, int WCO, bool X3>
+template <int NT, int CKB, int PB, int CBW, int WCO>
 void launch_pc_one(const nps_conv2d_t& a, dim3 grid, int lds, hipStream_t s) {
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)conv2d_pc_kernel<NT, CKB, PB, CBW, WCO, X3>,
+        (void)hipFuncSetAttribute((const void*)conv2d_pc_kernel<NT, CKB, PB, CBW, WCO>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_set = true;
     }
-    conv2d_pc_kernel<NT, CKB, PB, CBW, WCO, X3><<<grid, 512, lds, s>>>(a);
+    conv2d_pc_kernel<NT, CKB, PB, CBW, WCO><<<grid, 512, lds, s>>>(a);
 }
 
-template <bool X3>
 void launch_pc_taps(const nps_conv2d_t& a, dim3 grid, int lds, hipStream_t s, int nt, bool pb2) {
     if (nt == 9) {
-        if (pb2) launch_pc_one<9, 16, 2, 2, 1, X3>(a, grid, lds, s); else launch_pc_one<9, 16, 1, 2, 1, X3>(a, grid, lds, s);
+        if (pb2) launch_pc_one<9, 16, 2, 2, 1>(a, grid, lds, s); else launch_pc_one<9, 16, 1, 2, 1>(a, grid, lds, s);
     } else {
-        if (pb2) launch_pc_one<4, 16, 2, 2, 1, X3>(a, grid, lds, s); else launch_pc_one<4, 16, 1, 2, 1, X3>(a, grid, lds, s);
+        if (pb2) launch_pc_one<4, 16, 2, 2, 1>(a, grid, lds, s); else launch_pc_one<4, 16, 1, 2, 1>(a, grid, lds, s);
     }
 }
 
@@ -940,14 +718,13 @@ int launch_pc(const nps_conv2d_t& a, dim3 grid, int lds, hipStream_t s) {
     const bool pb2 = a.TH * a.TW == 256;
     grid.y = (a.Cout + pc_ncbg(nt) * 32 - 1) / (pc_ncbg(nt) * 32);
     if (nt == 1)
-        launch_pc_one<1, 32, 2, 3, 2, false>(a, grid, lds, s);
-    else if (a.precision == NPS_PREC_X3F16)
-        launch_pc_taps<true>(a, grid, lds, s, nt, pb2);
+        launch_pc_one<1, 32, 2, 3, 2>(a, grid, lds, s);
     else
-        launch_pc_taps<false>(a, grid, lds, s, nt, pb2);
+        launch_pc_taps(a, grid, lds, s, nt, pb2);
     NPS_CHECK_LAUNCH("conv2d_fwd (producer/consumer)");
     return 0;
 }
+
 }  // namespace
 
 extern "C" int nps_conv2d_fwd(const nps_conv2d_t* ap, void* stream) {
@@ -967,18 +744,23 @@ extern "C" int nps_conv2d_fwd(const nps_conv2d_t* ap, void* stream) {
                   "conv2d_fwd: bad GroupNorm prologue");
     NPS_CHECK_ARG(a.circ == 0 || (a.Hin > 0 && a.Win > 0), "conv2d_fwd: circular padding of empty frame");
     NPS_CHECK_ARG(a.waves == 1 || a.waves == 2 || a.waves == 4 || a.waves == 8, "conv2d_fwd: call nps_conv2d_plan first");
+    NPS_CHECK_ARG(a.precision == NPS_PREC_F32 || x3_sources_aligned(a),
+                  "conv2d_fwd: split-fp16 conv needs sources on 16-channel boundaries with C %% 4 == 0 (frame_pack first)");
     NPS_CHECK_ARG(a.precision == NPS_PREC_F32 || (a.precision == NPS_PREC_X3F16 && x3_eligible(a) && a.waves == 8),
                   "conv2d_fwd: precision %d not available for this conv (KH=%d stride=%d dil=%d)", a.precision, a.KH,
                   a.stride, a.dil);
-    NPS_CHECK_ARG(a.waves == 8 ? (a.TH * a.TW == 256 || a.TH * a.TW == 128) && pc_eligible(a) &&
-                                     (a.KH * a.KW != 1 || a.TH * a.TW == 128)
-                               : a.TH * a.TW == 64 * a.waves,
+    NPS_CHECK_ARG(a.precision == NPS_PREC_X3F16
+                      ? (a.TH * a.TW == 512 || a.TH * a.TW == 256) && (a.TW == 16 || a.TW == 32 || a.TW == 64)
+                      : (a.waves == 8 ? (a.TH * a.TW == 256 || a.TH * a.TW == 128) && pc_eligible(a) &&
+                                            (a.KH * a.KW != 1 || a.TH * a.TW == 128)
+                                      : a.TH * a.TW == 64 * a.waves),
                   "conv2d_fwd: tile %dx%d does not match waves=%d", a.TH, a.TW, a.waves);
     const Geo g = make_geo(a);
     const int lds = lds_bytes(a);
     NPS_CHECK_ARG(lds <= 160 * 1024, "conv2d_fwd: LDS %d B too large", lds);
     dim3 grid((unsigned)(g.tiles_x * g.tiles_y), (unsigned)((a.Cout + 63) / 64), (unsigned)a.B);
     hipStream_t s = (hipStream_t)stream;
+    if (a.precision == NPS_PREC_X3F16) return nps_launch_conv2d_x3(a, lds, s);
     if (a.waves == 8) return launch_pc(a, grid, lds, s);
     static bool attr_set = false;  // allow > 64 KiB dynamic LDS (gfx950 has 160 KiB per CU)
     if (!attr_set) {
@@ -1141,7 +923,8 @@ __global__ void frame_pack_kernel(nps_conv2d_t a, float* __restrict__ out) {
     const int cpg = a.gn_stats ? a.Cin / a.gn_groups : 1;
     const int stride = gridDim.x * blockDim.x;
     const nps_src_t S0 = a.src[0];
-    if (a.nsrc == 1 && S0.off_y == 0 && S0.off_x == 0 && S0.H == a.Hin && S0.W == a.Win && (a.Cin & 3) == 0) {
+    if (a.nsrc == 1 && S0.off_y == 0 && S0.off_x == 0 && S0.H == a.Hin && S0.W == a.Win && (a.Cin & 3) == 0 &&
+        a.out_C <= a.Cin) {
         // one source covering the frame: a flat contiguous sweep
         const int C4 = a.Cin >> 2;
         const int n = a.Hin * a.Win * C4;
@@ -1153,20 +936,26 @@ __global__ void frame_pack_kernel(nps_conv2d_t a, float* __restrict__ out) {
         }
         return;
     }
-    const int C4 = (a.Cin + 3) / 4;
+    // output channel stride oC >= Cin (a.out_C; channels [Cin, oC) are written as zeros)
+    const int oC = a.out_C > a.Cin ? a.out_C : a.Cin;
+    const int C4 = (oC + 3) / 4;
     const int n = a.Hin * a.Win * C4;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const int pix = i / C4;
         const int c = (i - pix * C4) * 4;
         const int y = pix / a.Win, x = pix - y * a.Win;
-        f32x4 v = prologue4(a, tab, cpg, c, fetch4(a, b, y, x, c));
-        float* dst = out + ((size_t)(b * a.Hin + y) * a.Win + x) * a.Cin + c;
-        if ((a.Cin & 3) == 0) {
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if (c < a.Cin) v = prologue4(a, tab, cpg, c, fetch4(a, b, y, x, c));
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            if (c + e >= a.Cin) v[e] = 0.f;
+        float* dst = out + ((size_t)(b * a.Hin + y) * a.Win + x) * oC + c;
+        if ((oC & 3) == 0) {
             *reinterpret_cast<f32x4*>(dst) = v;
         } else {
 #pragma unroll
             for (int e = 0; e < 4; ++e)
-                if (c + e < a.Cin) dst[e] = v[e];
+                if (c + e < oC) dst[e] = v[e];
         }
     }
 }
@@ -1182,7 +971,8 @@ extern "C" int nps_frame_pack(const nps_conv2d_t* ap, float* out, void* stream) 
     NPS_CHECK_ARG(csum == a.Cin, "frame_pack: Cin mismatch");
     NPS_CHECK_ARG(!a.gn_stats || (a.gn_groups > 0 && a.gn_groups <= 16 && a.Cin % a.gn_groups == 0),
                   "frame_pack: bad GroupNorm");
-    const long n = (long)a.Hin * a.Win * ((a.Cin + 3) / 4);
+    NPS_CHECK_ARG(a.out_C <= a.Cin || a.out_C < a.Cin + 4, "frame_pack: out_C pads at most 3 channels");
+    const long n = (long)a.Hin * a.Win * (((a.out_C > a.Cin ? a.out_C : a.Cin) + 3) / 4);
     int nb = (int)((n + 255) / 256);
     nb = nb > 2048 ? 2048 : nb;
     frame_pack_kernel<<<dim3(nb, a.B), 256, 0, (hipStream_t)stream>>>(a, out);

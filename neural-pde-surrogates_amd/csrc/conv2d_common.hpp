@@ -1,0 +1,212 @@
+// Shared device helpers of the implicit-GEMM conv kernels (conv2d.hip, conv2d_x3.hip).
+#pragma once
+#include "nps_common.hpp"
+
+namespace {
+
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+
+constexpr int CK = 16;          // input channels per K chunk
+constexpr int PIXS = CK + 4;    // LDS floats per patch pixel (+4 pad: conflict-free ds_read_b128)
+constexpr int MAXL = 12;        // max float4 patch loads per thread per chunk
+
+// 32-channel output blocks in the packed weight layout: a multiple of 6 so both the 64-co (2-block)
+// and the 192-co (6-block) work-group tiles index inside the buffer
+__host__ __device__ inline int packed_ncb(int Cout) { return 6 * ((Cout + 191) / 192); }
+
+// floats of the fragment body of a packed weight; the buffer carries PACK_TRAILER more floats
+// (trailer[0] = max|w| of a split-fp16 packing)
+__host__ __device__ inline size_t packed_body(int Cout, int Cin, int ntaps) {
+    const size_t nchunks = (Cin + CK - 1) / CK, ncb = packed_ncb(Cout);
+    return nchunks * ntaps * ncb * 2 * 64 * 4;
+}
+constexpr int PACK_TRAILER = 64;
+
+struct Geo {
+    int T, ri, rk, rstep, PH, PW, tiles_x, tiles_y;
+};
+
+__host__ __device__ inline Geo make_geo(const nps_conv2d_t& a) {
+    Geo g;
+    g.T = a.lattice ? a.dil : 1;
+    g.ri = a.lattice ? 1 : a.stride;
+    g.rk = a.lattice ? 1 : a.dil;
+    g.rstep = a.lattice ? a.dil : 1;
+    g.PH = (a.TH - 1) * g.ri + (a.KH - 1) * g.rk + 1;
+    g.PW = (a.TW - 1) * g.ri + (a.KW - 1) * g.rk + 1;
+    const int ny = (a.Hout + g.T - 1) / g.T, nx = (a.Wout + g.T - 1) / g.T;
+    g.tiles_y = g.T * ((ny + a.TH - 1) / a.TH);
+    g.tiles_x = g.T * ((nx + a.TW - 1) / a.TW);
+    return g;
+}
+
+// Fetch 4 consecutive virtual channels [c, c+4) at virtual-frame position (y, x) of sample b.
+// Written without loops over a.src[] (explicitly per source) so the kernarg struct is never indexed
+// dynamically — a dynamic index makes the compiler copy the whole struct to scratch.
+__device__ __forceinline__ bool fetch4_fast(const nps_src_t& S, int lo, int b, int y, int x, int c, f32x4& v) {
+    const int hi = lo + S.C;
+    if (c >= lo && c + 4 <= hi && ((c - lo) & 3) == 0 && (S.C & 3) == 0) {
+        const int yy = y - S.off_y, xx = x - S.off_x;
+        if (yy >= 0 && yy < S.H && xx >= 0 && xx < S.W)
+            v = *reinterpret_cast<const f32x4*>(S.ptr + ((size_t)(b * S.H + yy) * S.W + xx) * S.C + (c - lo));
+        return true;
+    }
+    return false;
+}
+
+__device__ __forceinline__ float fetch1(const nps_src_t& S, int lo, int b, int y, int x, int ce) {
+    if (ce >= lo && ce < lo + S.C) {
+        const int yy = y - S.off_y, xx = x - S.off_x;
+        if (yy >= 0 && yy < S.H && xx >= 0 && xx < S.W)
+            return S.ptr[((size_t)(b * S.H + yy) * S.W + xx) * S.C + (ce - lo)];
+    }
+    return 0.f;
+}
+
+__device__ __forceinline__ f32x4 fetch4(const nps_conv2d_t& a, int b, int y, int x, int c) {
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    const int lo1 = a.src[0].C, lo2 = a.src[0].C + a.src[1].C;
+    if (fetch4_fast(a.src[0], 0, b, y, x, c, v)) return v;
+    if (a.nsrc > 1 && fetch4_fast(a.src[1], lo1, b, y, x, c, v)) return v;
+    if (a.nsrc > 2 && fetch4_fast(a.src[2], lo2, b, y, x, c, v)) return v;
+    // general path: per-channel gather (sources with C % 4 != 0, straddling chunks)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int ce = c + e;
+        float r = fetch1(a.src[0], 0, b, y, x, ce);
+        if (a.nsrc > 1 && ce >= lo1) r = fetch1(a.src[1], lo1, b, y, x, ce);
+        if (a.nsrc > 2 && ce >= lo2) r = fetch1(a.src[2], lo2, b, y, x, ce);
+        v[e] = r;
+    }
+    return v;
+}
+
+// Epilogue of one 32x32 accumulator tile for this lane's output pixel (dy, dx): the lane holds
+// co = co_base + 8m + 4h + e (m, e < 4).  NHWC outputs with 4-aligned channels take a
+// vectorised path: all loads of the tile (bias, addends, accumulate source) are issued before
+// any store, then 16-B stores.  Order of the float ops matches the reference:
+// act(acc + bias + addends) or act(acc + bias) + addends, then + out when accumulating.
+__device__ __forceinline__ void store_tile(const nps_conv2d_t& a, int b, int co_base, int h, const f32x16& acc,
+                                           int dy, int dx) {
+    if (!a.out_nchw && (a.out_C & 3) == 0 && (a.Cout & 3) == 0) {
+        const size_t base = (((size_t)b * a.out_H + dy) * a.out_W + dx) * a.out_C;
+        f32x4 bi[4], a0[4], a1[4], o[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const int co0 = co_base + 8 * m + 4 * h;
+            const bool ok = co0 < a.Cout;
+            const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+            bi[m] = (ok && a.bias) ? *reinterpret_cast<const f32x4*>(a.bias + co0) : z;
+            a0[m] = (ok && a.addend0) ? *reinterpret_cast<const f32x4*>(a.addend0 + base + co0) : z;
+            a1[m] = (ok && a.addend1) ? *reinterpret_cast<const f32x4*>(a.addend1 + base + co0) : z;
+            o[m] = (ok && a.accumulate) ? *reinterpret_cast<const f32x4*>(a.out + base + co0) : z;
+        }
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const int co0 = co_base + 8 * m + 4 * h;
+            if (co0 >= a.Cout) continue;
+            f32x4 r;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float v = acc[4 * m + e] + bi[m][e];
+                if (!a.add_after_act) v = v + a0[m][e] + a1[m][e];
+                if (a.act == 1) v = nps::gelu_erf(v);
+                if (a.add_after_act) v = v + a0[m][e] + a1[m][e];
+                if (a.accumulate) v += o[m][e];
+                r[e] = v;
+            }
+            *reinterpret_cast<f32x4*>(a.out + base + co0) = r;
+        }
+        return;
+    }
+    // generic path: element address linear in co (NHWC stride 1, NCHW stride H*W)
+    const size_t base = a.out_nchw ? (((size_t)b * a.out_C) * a.out_H + dy) * a.out_W + dx
+                                   : (((size_t)b * a.out_H + dy) * a.out_W + dx) * a.out_C;
+    const size_t cstride = a.out_nchw ? (size_t)a.out_H * a.out_W : 1;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int co = co_base + 8 * m + 4 * h + e;
+            if (co >= a.Cout) continue;
+            const size_t di = base + (size_t)co * cstride;
+            float v = acc[4 * m + e];
+            if (a.bias) v += a.bias[co];
+            if (!a.add_after_act) {
+                if (a.addend0) v += a.addend0[di];
+                if (a.addend1) v += a.addend1[di];
+            }
+            if (a.act == 1) v = nps::gelu_erf(v);
+            if (a.add_after_act) {
+                if (a.addend0) v += a.addend0[di];
+                if (a.addend1) v += a.addend1[di];
+            }
+            if (a.accumulate) v += a.out[di];
+            a.out[di] = v;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// 3-pass split-fp16 arithmetic (NPS_PREC_X3F16).  Every fp32 operand x is carried as two fp16
+// halves x = hi + lo (hi = x rounded toward zero to fp16, lo = the fp32 residual x - hi rounded
+// toward zero, unscaled), and every product as hi_a*hi_b + hi_a*lo_b + lo_a*hi_b on
+// v_mfma_f32_32x32x16_f16 (fp32 accumulate, one accumulator): ~2^-21 relative per product, i.e. the
+// same error class as the reference's fp32 FMA chain, at 5.3x the fp32 MFMA rate.  Weights are
+// packed pre-scaled by an exact power of 2 (max |w| -> [2^13, 2^14)), so their residuals stay normal
+// fp16; activations are used as they are (a residual below 2^-14 turns subnormal, an absolute error
+// < 2^-25, far below the fp32 rounding of O(1) activations), gradients are range-scaled the same way
+// as weights (nps_conv2d_t.in_scale).  The epilogue multiplies the exact power-of-2 scales back out.
+
+// Power-of-2 scale mapping max |x| = m into [2^13, 2^14) (1 when m is 0 / not finite).
+__device__ __forceinline__ float pow2_scale_for(float m) {
+    if (!(m > 0.f) || !(m < 3.0e38f)) return 1.f;
+    return ldexpf(1.f, 13 - ilogbf(m));
+}
+// input scale of a split-fp16 conv: from a.in_scale (device pointer to max|x|, nps_absmax) or 1
+__device__ __forceinline__ float in_scale_of(const nps_conv2d_t& a) {
+    return a.in_scale == nullptr ? 1.f : pow2_scale_for(*a.in_scale);
+}
+
+typedef _Float16 h2f __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ h2f pkrtz(float a, float b) { return __builtin_bit_cast(h2f, __builtin_amdgcn_cvt_pkrtz(a, b)); }
+
+__device__ __forceinline__ void split4(const f32x4 v, f16x4& hi, f16x4& lo) {
+    const h2f h01 = pkrtz(v[0], v[1]);
+    const h2f h23 = pkrtz(v[2], v[3]);
+    const h2f l01 = pkrtz(v[0] - (float)h01[0], v[1] - (float)h01[1]);
+    const h2f l23 = pkrtz(v[2] - (float)h23[0], v[3] - (float)h23[1]);
+    hi = f16x4{h01[0], h01[1], h23[0], h23[1]};
+    lo = f16x4{l01[0], l01[1], l23[0], l23[1]};
+}
+
+constexpr int X3_NST = 3;     // LDS ring stages of the split-fp16 kernel
+constexpr int X3_PIXB = 80;   // LDS bytes per patch pixel of the split-fp16 kernel
+
+// The split-fp16 kernel stages 16 channels at a time from ONE source with 16-B loads: every source
+// boundary of the virtual frame on a multiple of 16 channels and every source's C a multiple of 4
+// (callers frame_pack other concatenations first).
+inline bool x3_sources_aligned(const nps_conv2d_t& a) {
+    int lo = 0;
+    for (int s = 0; s < a.nsrc; ++s) {
+        if ((a.src[s].C & 3) != 0 || (lo & 15) != 0) return false;
+        lo += a.src[s].C;
+    }
+    return true;
+}
+
+constexpr int X3_TPITCH = 68;  // floats per pixel of the LDS-staged output tile (64 channels + pad)
+
+inline int x3_lds_bytes(const nps_conv2d_t& a) {
+    const Geo g = make_geo(a);
+    const int ring = X3_NST * ((g.PH * g.PW * X3_PIXB + 15) & ~15);
+    const int tile = a.TH * a.TW * X3_TPITCH * 4;
+    return 128 + (ring > tile ? ring : tile);
+}
+
+}  // namespace
+
+// conv2d_x3.hip: launch of the split-fp16 kernel for a planned nps_conv2d_t
+int nps_launch_conv2d_x3(const nps_conv2d_t& a, int lds, hipStream_t s);

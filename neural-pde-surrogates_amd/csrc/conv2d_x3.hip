@@ -1,0 +1,394 @@
+// Split-fp16 (3-pass) implicit-GEMM 2-D convolution for gfx950 (MI355X), NHWC activations:
+// the NPS_PREC_X3F16 arithmetic of nps_conv2d_fwd (include/nps.h) for every stride-1, undilated
+// 1x1 / 2x2 / 3x3 conv of the reference's grid path (models/common.py:37-47, 93-120;
+// proc_unet_modern.py, proc_fno.py:114-117, enc_grid.py, dec_grid.py).
+#include "conv2d_common.hpp"
+
+#include <type_traits>
+
+namespace {
+
+// ---------------------------------------------------------------------------------------------
+// Split-fp16 producer/consumer conv (NPS_PREC_X3F16) for stride-1, undilated 1x1 / 2x2 / 3x3 convs.
+// 512 threads.  Work-group = 64 output channels x TILE_PX = 4*PB*32 output pixels (TH x TW) of one
+// sample; consumer wave w (0-3) owns 64 co x PB*32 px (2 x PB accumulators of 32x32, one per tile).
+//   * LDS holds only the input patch: a ring of NST = 3 stages of 16 channels, each pixel as
+//     [16 hi | 16 lo] fp16 + 16 B pad (80 B, conflict-free ds_read_b128).  Producer waves 4-7 fetch
+//     stage s+4 while stage s+2 is being committed (two register sets), so each global load has two
+//     consumer stages to land; one s_barrier per stage.
+//   * The weight fragments (2 KiB per (chunk, tap, 32-co block): [hi | lo] x 64 lanes x 16 B) are read
+//     by the consumer waves straight from global memory (L2/L1-resident: all 4 waves read the same
+//     bytes), two K-groups ahead in a 3-slot register ring, so LDS never carries the 9x-larger A tile.
+//   * K-group = (stage, tap): 24 v_mfma_f32_32x32x16_f16 per wave (2 co x PB px tiles x 3 passes),
+//     passes ordered hi*lo, hi*hi, lo*hi so the B registers are reloaded for the next group right
+//     after their last use (lo after pass 1, hi after pass 3) — one B register set.
+//   * Work-groups are numbered co-block fastest and remapped so consecutive numbers share an XCD
+//     (the 3 co-blocks of a tile and neighbouring tiles read the same patch bytes from one L2).
+__host__ __device__ constexpr int x3_patch_px_max(int ntaps, int tile_px) {
+    // largest (TH + k - 1) * (TW + k - 1) over the tile shapes nps_conv2d_plan uses for tile_px
+    return ntaps == 1 ? tile_px
+                      : (tile_px == 512 ? (ntaps == 4 ? 9 * 65 : 10 * 66) : (ntaps == 4 ? 9 * 33 : 10 * 34));
+}
+
+#ifdef NPS_X3_ABL_MFMA  // dev ablation: operands are loaded and consumed, no matrix instructions
+#define X3_MFMA(a_, b_, c_, ...) ((c_) + (float)((a_)[0] * (b_)[0]))
+#else
+#define X3_MFMA __builtin_amdgcn_mfma_f32_32x32x16_f16
+#endif
+
+#ifdef NPS_X3_STAMP  // dev diagnostic: per-work-group s_memtime stamps of consumer wave 0
+__device__ unsigned long long x3_stamps[1 << 20];
+#define X3_STAMP(i) \
+    if (wave == 0 && lane == 0 && blockIdx.x < (1 << 17)) x3_stamps[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memtime()
+#define X3_RSTAMP(i) \
+    if (wave == 0 && lane == 0 && blockIdx.x < (1 << 17)) x3_stamps[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime()
+#else
+#define X3_STAMP(i)
+#define X3_RSTAMP(i)
+#endif
+
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (N > 0) {
+        static_for<N - 1>(f);
+        f(std::integral_constant<int, N - 1>{});
+    }
+}
+
+// NHWC output with 4-aligned channels: the epilogue goes through LDS (x3_store_phase)
+__device__ __forceinline__ bool x3_lds_epilogue(const nps_conv2d_t& a) {
+    return !a.out_nchw && (a.out_C & 3) == 0 && (a.Cout & 3) == 0;
+}
+
+// All 512 threads store the work-group's 64-channel x TILE_PX tile from LDS (T[pixel][X3_TPITCH]):
+// 16 consecutive threads cover one pixel's 64 channels (256 contiguous bytes of the NHWC output), with
+// the fused bias / addends / GELU / accumulate of store_tile, in the same float order.
+template <int TILE_PX>
+__device__ __forceinline__ void x3_store_phase(const nps_conv2d_t& a, int b, int cob, int oy0, int ox0,
+                                               const float* T, int tid) {
+#pragma unroll 4
+    for (int i = tid; i < TILE_PX * 16; i += 512) {
+        const int P = i >> 4, q = i & 15;
+        const int co0 = cob * 64 + q * 4;
+        const int ti = P / a.TW, tj = P - (P / a.TW) * a.TW;
+        const int oy = oy0 + ti, ox = ox0 + tj;
+        const int dy = oy * a.out_os + a.out_off_y, dx = ox * a.out_os + a.out_off_x;
+        if (co0 >= a.Cout || oy >= a.Hout || ox >= a.Wout || dy < 0 || dy >= a.out_H || dx < 0 || dx >= a.out_W)
+            continue;
+        const f32x4 acc = *reinterpret_cast<const f32x4*>(T + P * X3_TPITCH + q * 4);
+        const size_t o = (((size_t)b * a.out_H + dy) * a.out_W + dx) * a.out_C + co0;
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        const f32x4 bi = a.bias ? *reinterpret_cast<const f32x4*>(a.bias + co0) : z;
+        const f32x4 a0 = a.addend0 ? *reinterpret_cast<const f32x4*>(a.addend0 + o) : z;
+        const f32x4 a1 = a.addend1 ? *reinterpret_cast<const f32x4*>(a.addend1 + o) : z;
+        const f32x4 ov = a.accumulate ? *reinterpret_cast<const f32x4*>(a.out + o) : z;
+        f32x4 r;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            float v = acc[e] + bi[e];
+            if (!a.add_after_act) v = v + a0[e] + a1[e];
+            if (a.act == 1) v = nps::gelu_erf(v);
+            if (a.add_after_act) v = v + a0[e] + a1[e];
+            if (a.accumulate) v += ov[e];
+            r[e] = v;
+        }
+        *reinterpret_cast<f32x4*>(a.out + o) = r;
+    }
+}
+
+template <int NTAPS, int PB>
+__global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
+    constexpr int KWT = NTAPS == 9 ? 3 : (NTAPS == 4 ? 2 : 1);
+    constexpr int CBW = 2;
+    constexpr int TILE_PX = 4 * PB * 32;
+    constexpr int MAXP = (x3_patch_px_max(NTAPS, TILE_PX) * 4 + 255) / 256;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const Geo g = make_geo(a);
+    const int ncob = (a.Cout + 63) / 64;
+    const int ntiles = g.tiles_x * g.tiles_y;
+    int L = blockIdx.x;
+    {
+        const int full = (int)(gridDim.x & ~7u);
+        if (L < full) L = (L & 7) * (full >> 3) + (L >> 3);
+    }
+    const int cob = L % ncob;
+    const int rest = L / ncob;
+    const int tile = rest % ntiles, b = rest / ntiles;
+    const int ty = tile / g.tiles_x, tx = tile - (tile / g.tiles_x) * g.tiles_x;
+    const int oy0 = ty * a.TH, ox0 = tx * a.TW;
+    const int npix = g.PH * g.PW;
+    const int NG = npix * 4;                              // float4 slots of a 16-channel patch stage
+    const int stage_b = (npix * X3_PIXB + 15) & ~15;
+    char* ring = reinterpret_cast<char*>(smem) + 128;
+    const int nstages = (a.Cin + CK - 1) / CK;
+
+    if (wave >= 4) {
+        // ------------------------------------------------------------------ producers: patch only
+        const int ptid = tid - 256;
+        const int ybase = oy0 - a.pad_y, xbase = ox0 - a.pad_x;
+        const int Hext = a.Hin + 2 * a.circ, Wext = a.Win + 2 * a.circ;
+        int sy[MAXP], sx[MAXP];
+#pragma unroll
+        for (int k = 0; k < MAXP; ++k) {
+            const int idx = ptid + k * 256;
+            const int p = idx >> 2;
+            const int pr = p / g.PW, pc = p - pr * g.PW;
+            const int ye = ybase + pr, xe = xbase + pc;
+            const bool ok = idx < NG && ye >= 0 && ye < Hext && xe >= 0 && xe < Wext;
+            sy[k] = ok ? (a.circ ? nps::wrap_mod(ye - a.circ, a.Hin) : ye) : -1;
+            sx[k] = ok ? (a.circ ? nps::wrap_mod(xe - a.circ, a.Win) : xe) : 0;
+        }
+        const float xs = in_scale_of(a);
+        f32x4 r0[MAXP];
+        // issue() returns the mask of slots holding in-frame data; commit() zeroes the others
+        auto issue = [&](int st, f32x4 (&rp)[MAXP]) -> unsigned {
+            unsigned okm = 0;
+            const int c0 = st * CK;
+            const int cend = min(c0 + CK, a.Cin);
+            int sidx = 0, cbase = 0;
+            {
+                int lo = 0;
+#pragma unroll
+                for (int si = 0; si < NPS_MAX_SRC; ++si) {  // unrolled: static kernarg indexing
+                    if (si < a.nsrc) {
+                        const int hi = lo + a.src[si].C;
+                        if (c0 >= lo && cend <= hi && (a.src[si].C & 3) == 0 && ((c0 - lo) & 3) == 0) {
+                            sidx = si;
+                            cbase = lo;
+                        }
+                        lo = hi;
+                    }
+                }
+            }
+            // host-checked (x3_sources_aligned): every 16-channel stage lies in one 4-aligned source
+            {
+                const nps_src_t S0 = a.src[0], S1 = a.src[1], S2 = a.src[2];
+                const float* sptr = sidx == 0 ? S0.ptr : (sidx == 1 ? S1.ptr : S2.ptr);
+                const int sC = sidx == 0 ? S0.C : (sidx == 1 ? S1.C : S2.C);
+                const int sH = sidx == 0 ? S0.H : (sidx == 1 ? S1.H : S2.H);
+                const int sW = sidx == 0 ? S0.W : (sidx == 1 ? S1.W : S2.W);
+                const int soy = sidx == 0 ? S0.off_y : (sidx == 1 ? S1.off_y : S2.off_y);
+                const int sox = sidx == 0 ? S0.off_x : (sidx == 1 ? S1.off_x : S2.off_x);
+                const int cs = c0 - cbase;
+                // every lane loads (padding lanes from the sample's first pixel) and then selects: no
+                // branch around the loads, so the in-order vmcnt accounting stays exact
+#pragma unroll
+                for (int k = 0; k < MAXP; ++k) {
+                    const int gq = (ptid + k * 256) & 3;
+                    const int yy = sy[k] - soy, xx = sx[k] - sox;
+                    const bool ok = sy[k] >= 0 && yy >= 0 && yy < sH && xx >= 0 && xx < sW && c0 + gq * 4 < cend;
+                    const size_t off = ok ? ((size_t)(b * sH + yy) * sW + xx) * sC + cs + gq * 4 : (size_t)b * sH * sW * sC;
+                    rp[k] = *reinterpret_cast<const f32x4*>(sptr + off);
+                    okm = ok ? (okm | (1u << k)) : okm;  // zeroed at commit: no use of a load before all are issued
+                }
+            }
+            return okm;
+        };
+        auto commit = [&](int st, const f32x4 (&rp)[MAXP], unsigned okm) {
+            char* Pt = ring + (st % X3_NST) * stage_b;
+#pragma unroll
+            for (int k = 0; k < MAXP; ++k) {
+                const int idx = ptid + k * 256;
+                if (idx < NG) {
+                    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+                    f16x4 hi, lo;
+                    split4(((okm >> k) & 1u) ? rp[k] * xs : z, hi, lo);
+                    char* base = Pt + (idx >> 2) * X3_PIXB + (idx & 3) * 8;
+                    *reinterpret_cast<f16x4*>(base) = hi;
+                    *reinterpret_cast<f16x4*>(base + 32) = lo;
+                }
+            }
+        };
+#ifdef NPS_X3_ABL_PROD  // dev ablation: producers only keep the barrier protocol
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        for (int st = 0; st < nstages; ++st) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        return;
+#endif
+        // Iteration st (while the consumers compute stage st): fetch stage st + 2, split it into the ring
+        // slot (st + 2) % 3 that the consumers released at the last barrier, barrier.  The fetch is
+        // waited for inside the iteration that issued it (a load carried across the loop's back edge
+        // makes the compiler drain every load at the latch), so its latency hides behind one consumer
+        // stage.  Barriers: 1 + nstages, as the consumers.
+        {
+            f32x4 r1[MAXP];
+            const unsigned m0 = issue(0, r0);
+            const unsigned m1 = issue(min(1, nstages - 1), r1);  // both prologue fetches in flight together
+            commit(0, r0, m0);
+            if (nstages > 1) commit(1, r1, m1);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        for (int st = 0; st < nstages; ++st) {
+            if (st + 2 < nstages) {
+                const unsigned m = issue(st + 2, r0);
+                commit(st + 2, r0, m);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+        if (!x3_lds_epilogue(a)) return;
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // consumers' tile is in LDS
+        x3_store_phase<TILE_PX>(a, b, cob, oy0, ox0, reinterpret_cast<const float*>(ring), tid);
+        return;
+    }
+
+    // ---------------------------------------------------------------------- consumers
+    int boff[PB];
+#pragma unroll
+    for (int pb = 0; pb < PB; ++pb) {
+        const int P = wave * 32 * PB + pb * 32 + (lane & 31);
+        const int ti = P / a.TW, tj = P - (P / a.TW) * a.TW;
+        boff[pb] = (ti * g.PW + tj) * X3_PIXB + (lane >> 5) * 16;
+    }
+    f32x16 acc[CBW][PB];
+#pragma unroll
+    for (int i = 0; i < CBW; ++i)
+#pragma unroll
+        for (int j = 0; j < PB; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int ncb = packed_ncb(a.Cout);
+    const char* wbase = reinterpret_cast<const char*>(a.wpack) + (size_t)cob * CBW * 2048 + lane * 16;
+    const size_t gstride = (size_t)ncb * 2048;  // bytes per K-group (chunk, tap) of the packed weight
+    const int G = nstages * NTAPS;
+    f16x8 Aw[2][CBW][2];
+    f16x8 Bh[2][PB], Bl[2][PB];
+    auto loadA = [&](int gg, f16x8 (&d)[CBW][2]) {
+        const char* p = wbase + (size_t)gg * gstride;
+#pragma unroll
+        for (int cb = 0; cb < CBW; ++cb) {
+#ifdef NPS_X3_ABL_A  // dev ablation: weights from LDS instead of global memory
+            d[cb][0] = *reinterpret_cast<const f16x8*>(ring + ((gg * 64 + cb * 2048) & 8191) + lane * 16);
+            d[cb][1] = *reinterpret_cast<const f16x8*>(ring + ((gg * 64 + cb * 2048 + 1024) & 8191) + lane * 16);
+#else
+            d[cb][0] = *reinterpret_cast<const f16x8*>(p + cb * 2048);
+            d[cb][1] = *reinterpret_cast<const f16x8*>(p + cb * 2048 + 1024);
+#endif
+        }
+    };
+    auto boffs = [&](int gg) {  // byte offset of K-group gg's patch window in the LDS ring
+        const int st = gg / NTAPS, tap = gg - (gg / NTAPS) * NTAPS;
+        return (st % X3_NST) * stage_b + ((tap / KWT) * g.PW + tap % KWT) * X3_PIXB;
+    };
+    auto loadB = [&](int gg, f16x8 (&d)[PB], int half) {
+        const char* p = ring + boffs(gg) + half * 32;
+#pragma unroll
+        for (int pb = 0; pb < PB; ++pb) d[pb] = *reinterpret_cast<const f16x8*>(p + boff[pb]);
+    };
+    // K-group gg uses weight slot gg & 1 and patch slot gg & 1; at its start the loads of group gg + 1
+    // (weights from global memory, patch from LDS) are issued into the other slots, so every load has
+    // the group's 8*PB MFMAs to land.  Loads are never skipped (index clamped to the last group): a
+    // skipped load on one path makes the compiler's in-order vmcnt wait drain the newest loads.
+    auto gclamp = [&](int x) { return x < G ? x : G - 1; };
+    auto group = [&](int gg, const int r) {
+        loadA(gclamp(gg + 1), Aw[r ^ 1]);
+        loadB(gclamp(gg + 1), Bh[r ^ 1], 0);
+        loadB(gclamp(gg + 1), Bl[r ^ 1], 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int cb = 0; cb < CBW; ++cb)
+#pragma unroll
+            for (int pb = 0; pb < PB; ++pb) acc[cb][pb] = X3_MFMA(Aw[r][cb][0], Bh[r][pb], acc[cb][pb], 0, 0, 0);
+#pragma unroll
+        for (int cb = 0; cb < CBW; ++cb)
+#pragma unroll
+            for (int pb = 0; pb < PB; ++pb) acc[cb][pb] = X3_MFMA(Aw[r][cb][0], Bl[r][pb], acc[cb][pb], 0, 0, 0);
+#pragma unroll
+        for (int cb = 0; cb < CBW; ++cb)
+#pragma unroll
+            for (int pb = 0; pb < PB; ++pb) acc[cb][pb] = X3_MFMA(Aw[r][cb][1], Bh[r][pb], acc[cb][pb], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if ((gg + 1) % NTAPS == 0) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    X3_STAMP(0);
+    X3_RSTAMP(4);
+    loadA(0, Aw[0]);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    loadB(0, Bh[0], 0);
+    loadB(0, Bl[0], 1);
+    X3_STAMP(1);
+    int g0 = 0;
+    for (; g0 + 2 <= G; g0 += 2) {
+        group(g0, 0);
+        group(g0 + 1, 1);
+    }
+    if (g0 < G) group(g0, 0);
+    X3_STAMP(2);
+
+    // epilogue: undo the exact power-of-2 scales of the weights and the input
+    const float inv = 1.f / (pow2_scale_for(a.wpack[packed_body(a.Cout, a.Cin, NTAPS)]) * in_scale_of(a));
+    const int h = lane >> 5;
+    if (x3_lds_epilogue(a)) {
+        // the ring is free (every read of it completed before the last stage barrier): the consumers
+        // drop the 64 x TILE_PX tile into LDS, then all 8 waves store it with coalesced 16-B accesses
+        float* T = reinterpret_cast<float*>(ring);
+#pragma unroll
+        for (int pb = 0; pb < PB; ++pb) {
+            const int P = wave * 32 * PB + pb * 32 + (lane & 31);
+#pragma unroll
+            for (int cb = 0; cb < CBW; ++cb)
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    const f32x4 v = {acc[cb][pb][4 * m] * inv, acc[cb][pb][4 * m + 1] * inv, acc[cb][pb][4 * m + 2] * inv,
+                                     acc[cb][pb][4 * m + 3] * inv};
+                    *reinterpret_cast<f32x4*>(T + P * X3_TPITCH + cb * 32 + 8 * m + 4 * h) = v;
+                }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        x3_store_phase<TILE_PX>(a, b, cob, oy0, ox0, T, tid);
+    } else {
+        static_for<PB>([&](auto pbc) {  // compile-time pb: acc stays in registers
+            constexpr int pb = decltype(pbc)::value;
+            const int P = wave * 32 * PB + pb * 32 + (lane & 31);
+            const int ti = P / a.TW, tj = P - (P / a.TW) * a.TW;
+            const int oy = oy0 + ti, ox = ox0 + tj;
+            if (oy >= a.Hout || ox >= a.Wout) return;
+            const int dy = oy * a.out_os + a.out_off_y, dx = ox * a.out_os + a.out_off_x;
+            if (dy < 0 || dy >= a.out_H || dx < 0 || dx >= a.out_W) return;
+#pragma unroll
+            for (int cb = 0; cb < CBW; ++cb) {
+                f32x16 v = acc[cb][pb];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) v[r] *= inv;
+                store_tile(a, b, cob * 64 + cb * 32, h, v, dy, dx);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        });
+    }
+    X3_STAMP(3);
+    X3_RSTAMP(5);
+}
+
+template <int NT, int PB>
+void launch_x3_one(const nps_conv2d_t& a, unsigned nwg, int lds, hipStream_t s) {
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)conv2d_x3_kernel<NT, PB>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        attr_set = true;
+    }
+    conv2d_x3_kernel<NT, PB><<<nwg, 512, lds, s>>>(a);
+}
+
+}  // namespace
+
+int nps_launch_conv2d_x3(const nps_conv2d_t& a, int lds, hipStream_t s) {
+    const Geo g = make_geo(a);
+    const long nwg = (long)g.tiles_x * g.tiles_y * a.B * ((a.Cout + 63) / 64);
+    NPS_CHECK_ARG(nwg < (1L << 31), "conv2d_fwd: grid too large");
+    const bool p512 = a.TH * a.TW == 512;
+    switch (a.KH * a.KW) {
+        case 9: p512 ? launch_x3_one<9, 4>(a, nwg, lds, s) : launch_x3_one<9, 2>(a, nwg, lds, s); break;
+        case 4: p512 ? launch_x3_one<4, 4>(a, nwg, lds, s) : launch_x3_one<4, 2>(a, nwg, lds, s); break;
+        default: p512 ? launch_x3_one<1, 4>(a, nwg, lds, s) : launch_x3_one<1, 2>(a, nwg, lds, s); break;
+    }
+    NPS_CHECK_LAUNCH("conv2d_fwd (split-fp16)");
+    return 0;
+}
+
+#ifdef NPS_X3_STAMP
+extern "C" int nps_x3_stamps(unsigned long long* host, int n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(x3_stamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -16,7 +16,7 @@ from . import Conv2dArgs, Src as _CSrc, check, lib, ptr, stream_ptr
 GELU = 1
 
 # Conv arithmetic (include/nps.h NPS_PREC_*): exact fp32 MFMA, or the 3-pass split-fp16 MFMA products
-# (~2^-22 relative per product, 5.3x the fp32 MFMA rate) for the stride-1 2x2 / 3x3 convs.
+# (~2^-21 relative per product, 5.3x the fp32 MFMA rate) for the stride-1 undilated 1x1 / 2x2 / 3x3 convs.
 PREC_F32, PREC_X3F16 = 0, 1
 CONV_PRECISION = PREC_F32 if os.environ.get("NPS_CONV_PRECISION", "x3f16") == "f32" else PREC_X3F16
 
@@ -141,10 +141,15 @@ def conv2d(srcs: Sequence[Src], frame_hw, wpack: torch.Tensor, bias: Optional[to
     B = t0.shape[0]
     Hin, Win = int(frame_hw[0]), int(frame_hw[1])
     Cin = sum(s.t.shape[3] for s in srcs)
-    if (gn is not None or pre_act) and stride == 1 and dil == 1 and KH == KW and KH in (1, 2, 3):
-        # the stride-1 producer/consumer conv stages raw bytes only: materialise act(GN(frame)) once
-        srcs = [Src(frame_pack(srcs, (Hin, Win), gn, pre_act))]
+    cin_alg = Cin  # algorithmic input channels (before any zero channel padding)
+    x3 = getattr(wpack, "nps_precision", PREC_F32) == PREC_X3F16
+    if ((gn is not None or pre_act) and stride == 1 and dil == 1 and KH == KW and KH in (1, 2, 3)) or (
+            x3 and not lib.nps_conv2d_x3_sources_ok(_c_src(srcs), len(srcs))):
+        # the stride-1 producer/consumer convs stage raw bytes only (the split-fp16 one from 16-channel
+        # aligned sources): materialise act(GN(frame)) / the concatenation once
+        srcs = [Src(frame_pack(srcs, (Hin, Win), gn, pre_act, pad4=x3))]
         gn, pre_act = None, 0
+        Cin = srcs[0].t.shape[3]  # (channel padding: the packed weight is zero for ci >= the true Cin)
     pb = pad if pad_bottom is None else pad_bottom
     if out_hw is None:
         Hout = (Hin + 2 * circ + pad[0] + pb[0] - dil * (KH - 1) - 1) // stride + 1
@@ -190,8 +195,8 @@ def conv2d(srcs: Sequence[Src], frame_hw, wpack: torch.Tensor, bias: Optional[to
         e0.record()
         check(lib.nps_conv2d_fwd(ctypes_byref(a), stream_ptr()), "conv2d_fwd")
         e1.record()
-        nbytes = 4.0 * (sum(s.t.numel() for s in srcs) + Cout * Cin * KH * KW + B * Hout * Wout * Cout)
-        conv_probe.append((e0, e1, 2.0 * B * Hout * Wout * Cout * Cin * KH * KW,
+        nbytes = 4.0 * (sum(s.t.numel() for s in srcs) + Cout * cin_alg * KH * KW + B * Hout * Wout * Cout)
+        conv_probe.append((e0, e1, 2.0 * B * Hout * Wout * Cout * cin_alg * KH * KW,
                            ("x3f16" if a.precision == PREC_X3F16 else "f32", KH * KW, a.waves), nbytes))
     else:
         check(lib.nps_conv2d_fwd(ctypes_byref(a), stream_ptr()), "conv2d_fwd")
@@ -206,8 +211,9 @@ def absmax(x: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def frame_pack(srcs: Sequence[Src], frame_hw, gn: Optional[GN] = None, pre_act=0) -> torch.Tensor:
-    """(B, Hin, Win, Cin) = act(GN(virtual frame)) — nps_frame_pack."""
+def frame_pack(srcs: Sequence[Src], frame_hw, gn: Optional[GN] = None, pre_act=0, pad4=False) -> torch.Tensor:
+    """(B, Hin, Win, Cin) = act(GN(virtual frame)) — nps_frame_pack; pad4: channels zero-padded to a
+    multiple of 4 (the split-fp16 conv stages 16-B channel groups)."""
     t0 = srcs[0].t
     B = t0.shape[0]
     Hin, Win = int(frame_hw[0]), int(frame_hw[1])
@@ -220,7 +226,8 @@ def frame_pack(srcs: Sequence[Src], frame_hw, gn: Optional[GN] = None, pre_act=0
         a.gn_stats, a.gn_gamma, a.gn_beta = ptr(gn.stats), ptr(gn.gamma), ptr(gn.beta)
         a.gn_groups, a.gn_eps = gn.groups, gn.eps
     a.pre_act = pre_act
-    out = empty_nhwc(B, Hin, Win, Cin, t0)
+    a.out_C = (Cin + 3) // 4 * 4 if pad4 else Cin
+    out = empty_nhwc(B, Hin, Win, a.out_C, t0)
     check(lib.nps_frame_pack(ctypes_byref(a), ptr(out), stream_ptr()), "frame_pack")
     return out
 

@@ -18,10 +18,12 @@ for s in $STEPS; do
     train) timeout -k 10 300 python -u bench.py --mode train --steps 5 --warmup 2 --global-batch 2 > gpurun_out/${TAG}_train.log 2>&1 || { echo "train bench failed"; tail -30 gpurun_out/${TAG}_train.log; exit 1; }; tail -1 gpurun_out/${TAG}_train.log ;;
     trainprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_tprof -o run -- python3 bench.py --mode train --steps 3 --warmup 1 --global-batch 2 \
              > gpurun_out/${TAG}_tprof.log 2>&1 || { echo "train prof failed"; tail -30 gpurun_out/${TAG}_tprof.log; exit 1; } ;;
-    convx3) for P in f32 x3f16; do
-              timeout -k 10 120 python -u tools/conv_bench.py --prec $P --cin 388 --cout 192 --k 3 --hw 260 --b 16 --gn 1 --check &&
-              timeout -k 10 120 python -u tools/conv_bench.py --prec $P --cin 192 --cout 192 --k 3 --hw 258 --b 16 --gn 1 &&
-              timeout -k 10 120 python -u tools/conv_bench.py --prec $P --cin 196 --cout 192 --k 3 --hw 127 --b 16 --gn 1 --check || exit 1
+    convx3) for A in "--cin 388 --cout 192 --k 3 --hw 260 --gn 1" "--cin 192 --cout 192 --k 3 --hw 258 --gn 0" \
+                     "--cin 196 --cout 192 --k 3 --hw 127 --gn 1" "--cin 388 --cout 192 --k 1 --hw 260 --gn 0" \
+                     "--cin 196 --cout 192 --k 1 --hw 256 --gn 0" "--cin 81 --cout 192 --k 1 --hw 256 --gn 0" \
+                     "--cin 192 --cout 75 --k 1 --hw 256 --gn 0" "--cin 768 --cout 192 --k 2 --hw 129 --gn 0" \
+                     "--cin 192 --cout 192 --k 1 --hw 132 --gn 1"; do
+              timeout -k 10 120 python -u tools/conv_bench.py --prec x3f16 --b 16 $A --check || exit 1
             done > gpurun_out/${TAG}_convx3.log 2>&1; cat gpurun_out/${TAG}_convx3.log | grep -v amdgpu.ids ;;
   esac
   echo "step $s ok"

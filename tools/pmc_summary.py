@@ -25,9 +25,12 @@ def load(d, counter):
 
 
 def klass(name):
-    m = re.search(r"conv2d_pc_kernel<(\d+), \d+, \d+, \d+, \d+, (true|false)>", name)
+    m = re.search(r"conv2d_x3_kernel<(\d+), \d+>", name)
     if m:
-        return f"{'x3f16' if m.group(2) == 'true' else 'f32'}_{m.group(1)}tap"
+        return f"x3f16_{m.group(1)}tap"
+    m = re.search(r"conv2d_pc_kernel<(\d+), \d+, \d+, \d+, \d+>", name)
+    if m:
+        return f"f32_{m.group(1)}tap"
     return None
 
 
@@ -46,6 +49,14 @@ def main():
         wb = 1024 * sum(wv) / len(wv)
         out["kernels"][name[:160]] = dict(launches=len(fv), fetch_bytes_per_launch=fb, write_bytes_per_launch=wb,
                                           hbm_bytes_per_launch=fb + wb, **({"class": klass(name)} if klass(name) else {}))
+    classes = {}
+    for rec in out["kernels"].values():
+        if "class" in rec:
+            c = classes.setdefault(rec["class"], dict(launches=0, hbm_bytes=0.0))
+            c["launches"] += rec["launches"]
+            c["hbm_bytes"] += rec["hbm_bytes_per_launch"] * rec["launches"]
+    out["classes"] = {k: dict(launches=v["launches"], hbm_bytes_per_launch=v["hbm_bytes"] / v["launches"])
+                      for k, v in classes.items()}
     print(json.dumps(out, indent=1))
 
 
