@@ -280,6 +280,9 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
     // the group's 8*PB MFMAs to land.  Loads are never skipped (index clamped to the last group): a
     // skipped load on one path makes the compiler's in-order vmcnt wait drain the newest loads.
     auto gclamp = [&](int x) { return x < G ? x : G - 1; };
+#ifdef NPS_X3_STAMP
+    unsigned long long bar_cycles = 0;  // consumer wave 0: cycles spent in the stage barriers
+#endif
     auto group = [&](int gg, const int r) {
         loadA(gclamp(gg + 1), Aw[r ^ 1]);
         loadB(gclamp(gg + 1), Bh[r ^ 1], 0);
@@ -298,7 +301,15 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
 #pragma unroll
             for (int pb = 0; pb < PB; ++pb) acc[cb][pb] = X3_MFMA(Aw[r][cb][1], Bh[r][pb], acc[cb][pb], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
-        if ((gg + 1) % NTAPS == 0) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if ((gg + 1) % NTAPS == 0) {
+#ifdef NPS_X3_STAMP
+            const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            bar_cycles += __builtin_amdgcn_s_memtime() - t0;
+#else
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#endif
+        }
         __builtin_amdgcn_sched_barrier(0);
     };
     X3_STAMP(0);
@@ -315,6 +326,9 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
     }
     if (g0 < G) group(g0, 0);
     X3_STAMP(2);
+#ifdef NPS_X3_STAMP
+    if (wave == 0 && lane == 0 && blockIdx.x < (1 << 17)) x3_stamps[blockIdx.x * 8 + 6] = bar_cycles;
+#endif
 
     // epilogue: undo the exact power-of-2 scales of the weights and the input
     const float inv = 1.f / (pow2_scale_for(a.wpack[packed_body(a.Cout, a.Cin, NTAPS)]) * in_scale_of(a));

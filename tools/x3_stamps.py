@@ -50,7 +50,8 @@ def main():
     print(f"cycles per WG (median): prologue {np.median(pro):.0f}  loop {np.median(loop):.0f} "
           f"(MFMA-only {ideal})  epilogue {np.median(epi):.0f}; loop p10/p90 {np.percentile(loop, 10):.0f}/"
           f"{np.percentile(loop, 90):.0f}")
-    print(f"loop efficiency {ideal / np.median(loop) * 100:.1f}%")
+    print(f"loop efficiency {ideal / np.median(loop) * 100:.1f}%; consumer wave 0 waits at stage barriers "
+          f"{np.median(st[:, 6]):.0f} cycles per WG (median)")
 
 
 if __name__ == "__main__":
