@@ -249,6 +249,21 @@ int nps_spectral_mix_bwd(const float* X2, const float* wpack, const float* gY, f
 int nps_spectral_unpack_grad(const float* gwpack, float* gw1, float* gw2, int Cin, int Cout, int H, int m1, int m2,
                              void* stream);
 
+/* SpectralConv3d (proc_fno.py:291-376: rfftn over (D, H, W) -> 4 retained corners weights1..4 -> irfftn)
+ * on NDHWC activations, composed of the 2-D stages above applied per axis:
+ *  W: dft_w over (B, D*H, W)                 -> X1 [B][D*H][m3][C]
+ *  H: dft_h over (B*D, H), m2 := m3          -> X2 [B*D][R2][m3][C]        R2 = min(H, 2*m2)
+ *  D: dft_h over (B, D),   m2 := R2*m3       -> X3 [B][R1][R2*m3][C]       R1 = min(D, 2*m1)
+ *  mix(X3, wpack, R := R1, m2 := R2*m3); idft_h (D), idft_h (H), idft_w over (B, D*H, W) (1/(D*H*W)).
+ * The backward is the same adjoint chain as the 2-D one, axis by axis.
+ * wpack: [R1][R2][m3][Cin][Cout] complex; where corners overlap the later reference write wins
+ * (w1 [:m1,:m2] < w2 [-m1:,:m2] < w3 [:m1,-m2:] < w4 [-m1:,-m2:], proc_fno.py:342-350). */
+int nps_spectral3d_pack_weights(const float* w1, const float* w2, const float* w3, const float* w4, float* wpack,
+                                int Cin, int Cout, int D, int H, int m1, int m2, int m3, void* stream);
+/* gweights1..4 [Cin][Cout][m1][m2][m3] from gwpack (0 where a later corner owns the mode) */
+int nps_spectral3d_unpack_grad(const float* gwpack, float* gw1, float* gw2, float* gw3, float* gw4, int Cin, int Cout,
+                               int D, int H, int m1, int m2, int m3, void* stream);
+
 /* TimeConvDense + add_delta + tanh + mask backward (dec_grid.py:126-146, :8-31): gpre is planar like
  * `pre`; ws[blocks][params] receives per-block partials of [w1 | b1 | w2 | b2] (blocks = B*ceil(H*W/64),
  * params = 2c*c*ka + 2c + c*2c*kb + c), reduced with nps_channel_sums. */

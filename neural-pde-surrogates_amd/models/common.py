@@ -171,6 +171,41 @@ class ConvTranspose2d_padded(ConvTranspose2d):
         self.pre_pad = pad
 
 
+class Conv3d(_PackedMixin, nn.Conv3d):
+    """nn.Conv3d parameters (common.py:37-47 with spatial_dim 3).  The FNO-3D pointwise `w` conv
+    (fno_kernel_size 1) runs as a 1x1 conv over the (D*H, W) view of NDHWC activations on the HIP
+    conv kernel; other 3-D convs are not on the MI355X path."""
+
+    def _check(self):
+        if tuple(self.kernel_size) != (1, 1, 1) or tuple(self.stride) != (1, 1, 1) or self.groups != 1 \
+                or tuple(self.dilation) != (1, 1, 1):
+            raise NotImplementedError("only pointwise (kernel 1) 3-D convs run on the MI355X path")
+
+    def geometry(self):
+        return 1, 1, 1, 1, (0, 0), (0, 0), 0
+
+    def run(self, srcs, frame_hw, **kw):
+        """srcs: NDHWC sources viewed as (B, D*H, W, C); frame_hw = (D*H, W)."""
+        self._check()
+        pk = self._packed(lambda w: ops.pack_conv_weight(w.reshape(w.shape[0], w.shape[1], 1, 1)))
+        return ops.conv2d(srcs, frame_hw, pk, self.bias, self.out_channels, 1, 1, **kw)
+
+    def run_ad(self, x):
+        self._check()
+        return ad.Conv2dFn.apply(self.geometry(), x, self.weight.reshape(self.out_channels, self.in_channels, 1, 1),
+                                 self.bias)
+
+    def forward(self, x):
+        B, C, D, H, W = x.shape
+        x4 = x.reshape(B, C, D * H, W)
+        if use_autograd(self):
+            y = ad.to_nchw(self.run_ad(ad.to_nhwc(x4)))
+        else:
+            x4 = ops.nchw_to_nhwc(x4)
+            y = ops.nhwc_to_nchw(self.run([ops.Src(x4)], (D * H, W)))
+        return y.reshape(B, self.out_channels, D, H, W)
+
+
 def get_conv_with_right_spatial_dim(spatial_dim, **kwargs):
     """common.py:37-47."""
     if spatial_dim == 1:
@@ -178,7 +213,7 @@ def get_conv_with_right_spatial_dim(spatial_dim, **kwargs):
     if spatial_dim == 2:
         return Conv2d(**kwargs)
     if spatial_dim == 3:
-        return nn.Conv3d(**kwargs)
+        return Conv3d(**kwargs)
     raise NotImplementedError(f"only 0<x<=3d convs implemented so far, but found spatial dim {spatial_dim}!")
 
 

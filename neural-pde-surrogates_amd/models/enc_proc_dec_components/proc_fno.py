@@ -44,25 +44,36 @@ class FNO(nn.Module):
     def __repr__(self):
         return f'FNO{self.num_spatial_dims}D'
 
-    def run(self, h, vb):
-        """NHWC: h (B,H,W,C), vb (B,H,W,K) or None."""
+    def run(self, h, vb, D=None):
+        """NHWC: h (B,H,W,C), vb (B,H,W,K) or None (3-D: NDHWC viewed as (B, D*H, W, C), depth D)."""
         if self.cond_mode == "film":
             raise NotImplementedError("FiLM conditioning is not on the MI355X path (twophase cfgs use concat)")
         for layer in self.fno_layers:
             srcs = [ops.Src(h)] + ([ops.Src(vb)] if (vb is not None and self.cond_mode == "concat") else [])
-            h = layer.run(srcs)
+            h = layer.run(srcs, D=D) if self.num_spatial_dims == 3 else layer.run(srcs)
         return h
 
-    def run_ad(self, h, vb):
+    def run_ad(self, h, vb, D=None):
         if self.cond_mode == "film":
             raise NotImplementedError("FiLM conditioning is not on the MI355X path (twophase cfgs use concat)")
         for layer in self.fno_layers:
             srcs = [ops.Src(h)] + ([ops.Src(vb)] if (vb is not None and self.cond_mode == "concat") else [])
-            h = layer.run_ad(ad.frame(srcs, h.shape[1:3]))
+            x = ad.frame(srcs, h.shape[1:3])
+            h = layer.run_ad(x, D) if self.num_spatial_dims == 3 else layer.run_ad(x)
         return h
 
     def forward(self, h: torch.Tensor, variables: torch.Tensor = None, variables_broadcast: torch.Tensor = None,
                 pos=None):
+        if self.num_spatial_dims == 3:  # (B, C, D, H, W): the layers run on the (B, D*H, W, C) view
+            B, C, D, H, W = h.shape
+            flat = lambda t: t.reshape(t.shape[0], t.shape[1], D * H, W)
+            if use_autograd(self):
+                vb = ad.to_nhwc(flat(variables_broadcast)) if variables_broadcast is not None else None
+                y = ad.to_nchw(self.run_ad(ad.to_nhwc(flat(h)), vb, D))
+            else:
+                vb = ops.nchw_to_nhwc(flat(variables_broadcast)) if variables_broadcast is not None else None
+                y = ops.nhwc_to_nchw(self.run(ops.nchw_to_nhwc(flat(h)), vb, D))
+            return y.reshape(B, y.shape[1], D, H, W)
         if use_autograd(self):
             vb = ad.to_nhwc(variables_broadcast) if variables_broadcast is not None else None
             return ad.to_nchw(self.run_ad(ad.to_nhwc(h), vb))
@@ -113,10 +124,19 @@ class FNO_Layer(nn.Module):
             else:
                 assert self.modes[i] <= s, 'modes should be at most the spatial dim all but the last spatial dimensions!'
 
-    def run(self, srcs, act_override=None):
-        """srcs: virtual NHWC input frame (h, vb).  Returns act(spectral(x) + w(x) [+ w2(x)])."""
+    def run(self, srcs, act_override=None, D=None):
+        """srcs: virtual NHWC input frame (h, vb) — for 3-D layers NDHWC sources viewed as (B, D*H, W, C).
+        Returns act(spectral(x) + w(x) [+ w2(x)])."""
+        if self.num_spatial_dims == 3:
+            DH, W = srcs[0].t.shape[1:3]
+            self._check_modes((D, DH // D, W))
+            if self.conv_mode != "single":
+                raise NotImplementedError("FNO_Layer 3-D: conv_mode 'single' only on the MI355X path")
+            act = activation_code(self.act) if act_override is None else act_override
+            out = self.w.run(srcs, (DH, W))
+            return self.conv.run(srcs, D, out=out, accumulate=True, act=act)
         if self.num_spatial_dims != 2:
-            raise NotImplementedError("FNO_Layer: 2-D only on the MI355X path")
+            raise NotImplementedError("FNO_Layer: 2-D / 3-D only on the MI355X path")
         H, W = srcs[0].t.shape[1:3]
         self._check_modes((H, W))
         act = activation_code(self.act) if act_override is None else act_override
@@ -125,10 +145,17 @@ class FNO_Layer(nn.Module):
             self.w2.run(srcs, (H, W), out=out, accumulate=True)
         return self.conv.run(srcs, out=out, accumulate=True, act=act)
 
-    def run_ad(self, x):
-        """Differentiable form: x (B,H,W,Cin) materialised frame."""
+    def run_ad(self, x, D=None):
+        """Differentiable form: x (B,H,W,Cin) materialised frame ((B, D*H, W, Cin) for 3-D layers)."""
+        if self.num_spatial_dims == 3:
+            DH, W = x.shape[1:3]
+            self._check_modes((D, DH // D, W))
+            if self.conv_mode != "single":
+                raise NotImplementedError("FNO_Layer 3-D: conv_mode 'single' only on the MI355X path")
+            y = ad.add_at(ad.spectral_conv3d(self.conv, x, D), self.w.run_ad(x))
+            return ad.act(y, activation_code(self.act))
         if self.num_spatial_dims != 2:
-            raise NotImplementedError("FNO_Layer: 2-D only on the MI355X path")
+            raise NotImplementedError("FNO_Layer: 2-D / 3-D only on the MI355X path")
         self._check_modes(x.shape[1:3])
         y = ad.add_at(ad.spectral_conv2d(self.conv, x), ad.conv2d(self.w, x))
         if self.conv_mode == "double":
@@ -136,6 +163,14 @@ class FNO_Layer(nn.Module):
         return ad.act(y, activation_code(self.act))
 
     def forward(self, x, p=None):
+        if self.num_spatial_dims == 3:
+            B, C, D, H, W = x.shape
+            x4 = x.reshape(B, C, D * H, W)
+            if use_autograd(self):
+                y = ad.to_nchw(self.run_ad(ad.to_nhwc(x4), D))
+            else:
+                y = ops.nhwc_to_nchw(self.run([ops.Src(ops.nchw_to_nhwc(x4))], D=D))
+            return y.reshape(B, y.shape[1], D, H, W)
         if use_autograd(self):
             return ad.to_nchw(self.run_ad(ad.to_nhwc(x)))
         x = ops.nchw_to_nhwc(x)
@@ -212,7 +247,8 @@ class SpectralConv1d(nn.Module):
 
 
 class SpectralConv3d(nn.Module):
-    """proc_fno.py:291-376 — parameters; the 3-D HIP path is a later-round item."""
+    """proc_fno.py:291-376: rfftn over (D, H, W) -> per-mode complex mixing of the 4 retained corners ->
+    irfftn, on the per-axis truncated-DFT HIP pipeline (include/nps.h, SpectralConv3d)."""
 
     def __init__(self, in_channels, out_channels, modes: tuple, feature_transform=False, feature_transform_dim=6,
                  transform_mode=1):
@@ -230,8 +266,36 @@ class SpectralConv3d(nn.Module):
             self.weights_feat = nn.Linear(feature_transform_dim,
                                           self.out_channels * 2 * self.modes1 * 2 * self.modes2 * self.modes3)
 
+    def _weights(self):
+        return [self.weights1, self.weights2, self.weights3, self.weights4]
+
+    def packed(self, D, H):
+        ws = self._weights()
+        key = (D, H, str(ws[0].device)) + tuple((w.data_ptr(), w._version) for w in ws)
+        if getattr(self, "_pk_key", None) != key:
+            self._pk = ops.pack_spectral3d_weight(ws, D, H)
+            self._pk_key = key
+        return self._pk
+
+    def run(self, srcs, D, out=None, accumulate=False, addend=None, act=0):
+        """srcs: NDHWC sources viewed as (B, D*H, W, C).  Returns (B, D*H, W, Cout)."""
+        if self.feature_transform:
+            raise NotImplementedError("FiLM spectral conditioning is not on the MI355X path")
+        H = srcs[0].t.shape[1] // D
+        return ops.spectral_conv3d(srcs, D, self.packed(D, H), self.modes1, self.modes2, self.modes3,
+                                   self.out_channels, out=out, accumulate=accumulate, addend=addend, act=act)
+
     def forward(self, x, p=None):
-        raise NotImplementedError("SpectralConv3d HIP path is not built yet (SURVEY.md §8f rank 4)")
+        if self.feature_transform:
+            raise NotImplementedError("FiLM spectral conditioning is not on the MI355X path")
+        B, C, D, H, W = x.shape
+        ops.check_modes3d(D, H, W, self.modes1, self.modes2, self.modes3)
+        x4 = x.reshape(B, C, D * H, W)
+        if use_autograd(self):
+            y = ad.to_nchw(ad.spectral_conv3d(self, ad.to_nhwc(x4), D))
+        else:
+            y = ops.nhwc_to_nchw(self.run([ops.Src(ops.nchw_to_nhwc(x4))], D))
+        return y.reshape(B, self.out_channels, D, H, W)
 
 
 def get_spectral_conv_with_right_spatial_dim(spatial_dim, **kwargs):

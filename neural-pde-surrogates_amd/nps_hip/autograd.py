@@ -442,6 +442,66 @@ def spectral_conv2d(module, x):
                                   module.weights2, module.packed(H))
 
 
+class SpectralConv3dFn(torch.autograd.Function):
+    """SpectralConv3d.forward (proc_fno.py:334-376) and its torch.fft / complex-einsum backward, axis by
+    axis with the 2-D kernels (include/nps.h, SpectralConv3d)."""
+
+    @staticmethod
+    def forward(ctx, meta, x, w1, w2, w3, w4, wpack):
+        m1, m2, m3, Cout, D = meta
+        x = _c(x)  # (B, D*H, W, Cin)
+        B, DH, W, Cin = x.shape
+        H = DH // D
+        y = ops.empty_nhwc(B, DH, W, Cout, x)
+        X3 = ops.spectral_conv3d_stages([Src(x)], D, H, W, Cin, wpack, m1, m2, m3, Cout, y)
+        ctx.meta, ctx.shape = meta, (B, D, H, W, Cin)
+        ctx.save_for_backward(X3, wpack)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        m1, m2, m3, Cout, D = ctx.meta
+        B, D, H, W, Cin = ctx.shape
+        X3, wpack = ctx.saved_tensors
+        R1, R2 = min(D, 2 * m1), min(H, 2 * m2)
+        gy = _c(gy)
+        dev = gy.device
+        c64 = torch.complex64
+        s = stream_ptr()
+        gZ2 = torch.empty((B, D * H, m3, Cout), dtype=c64, device=dev)
+        gZ1 = torch.empty((B * D, R2, m3, Cout), dtype=c64, device=dev)
+        gY = torch.empty((B, R1, R2 * m3, Cout), dtype=c64, device=dev)
+        gX3 = torch.empty((B, R1, R2 * m3, Cin), dtype=c64, device=dev)
+        gwp = torch.empty((R1, R2, m3, Cin, Cout), dtype=c64, device=dev)
+        check(lib.nps_spectral_idft_w_bwd(ptr(gy), ptr(gZ2), B, D * H, W, m3, Cout, s), "spectral3d idft_w_bwd")
+        check(lib.nps_spectral_dft_h(ptr(gZ2), ptr(gZ1), B * D, H, m2, m3, Cout, s), "spectral3d dft_h (H, bwd)")
+        check(lib.nps_spectral_dft_h(ptr(gZ1), ptr(gY), B, D, m1, R2 * m3, Cout, s), "spectral3d dft_h (D, bwd)")
+        check(lib.nps_spectral_mix_bwd(ptr(X3), ptr(wpack), ptr(gY), ptr(gX3), ptr(gwp), B, R1, R2 * m3, Cin, Cout,
+                                       s), "spectral3d mix_bwd")
+        dx = None
+        gws = [None] * 4
+        if ctx.needs_input_grad[1]:
+            gX2 = torch.empty((B, D, R2 * m3, Cin), dtype=c64, device=dev)
+            gX1 = torch.empty((B * D, H, m3, Cin), dtype=c64, device=dev)
+            check(lib.nps_spectral_idft_h(ptr(gX3), ptr(gX2), B, D, m1, R2 * m3, Cin, s), "spectral3d idft_h (D, bwd)")
+            check(lib.nps_spectral_idft_h(ptr(gX2), ptr(gX1), B * D, H, m2, m3, Cin, s), "spectral3d idft_h (H, bwd)")
+            dx = torch.empty((B, D * H, W, Cin), dtype=torch.float32, device=dev)
+            check(lib.nps_spectral_dft_w_bwd(ptr(gX1), ptr(dx), B, D * H, W, m3, Cin, s), "spectral3d dft_w_bwd")
+        if any(ctx.needs_input_grad[2:6]):
+            gws = [torch.empty((Cin, Cout, m1, m2, m3), dtype=c64, device=dev) for _ in range(4)]
+            check(lib.nps_spectral3d_unpack_grad(ptr(gwp), *[ptr(g) for g in gws], Cin, Cout, D, H, m1, m2, m3, s),
+                  "spectral3d_unpack_grad")
+        return (None, dx, *gws, None)
+
+
+def spectral_conv3d(module, x, D):
+    """x: (B, D*H, W, Cin) NDHWC view -> (B, D*H, W, Cout)."""
+    H = x.shape[1] // D
+    return SpectralConv3dFn.apply((module.modes1, module.modes2, module.modes3, module.out_channels, D), x,
+                                  module.weights1, module.weights2, module.weights3, module.weights4,
+                                  module.packed(D, H))
+
+
 # ------------------------------------------------------------------------- decoder / wrapper / loss
 class TimeConvDecodeFn(torch.autograd.Function):
     """TimeConvDense conv1d chain + add_delta('per_step') + tanh + spatial-cond mask

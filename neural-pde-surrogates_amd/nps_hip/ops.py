@@ -265,6 +265,65 @@ def spectral_conv2d(srcs: Sequence[Src], wpack: torch.Tensor, m1: int, m2: int, 
     return out
 
 
+def pack_spectral3d_weight(ws: Sequence[torch.Tensor], D: int, H: int) -> torch.Tensor:
+    """SpectralConv3d weights1..4 (Cin, Cout, m1, m2, m3) complex64 -> wpack [R1][R2][m3][Cin][Cout]."""
+    w1, w2, w3, w4 = [w.detach().contiguous() for w in ws]
+    Cin, Cout, m1, m2, m3 = w1.shape
+    R1, R2 = min(D, 2 * m1), min(H, 2 * m2)
+    out = torch.empty((R1, R2, m3, Cin, Cout), dtype=torch.complex64, device=w1.device)
+    check(lib.nps_spectral3d_pack_weights(ptr(w1), ptr(w2), ptr(w3), ptr(w4), ptr(out), Cin, Cout, D, H, m1, m2, m3,
+                                          stream_ptr()), "spectral3d_pack_weights")
+    return out
+
+
+def check_modes3d(D, H, W, m1, m2, m3):
+    """proc_fno.py:134-139 for three spatial dims."""
+    if not (m1 <= D and m2 <= H and m3 <= W // 2 + 1):
+        raise AssertionError("modes should be at most the spatial dim (// 2 + 1 for the last spatial dimension)")
+
+
+def spectral_conv3d_stages(x4: Sequence[Src], D, H, W, Cin, wpack, m1, m2, m3, Cout, out, accumulate=False,
+                           addend=None, act=0):
+    """The SpectralConv3d forward chain on a virtual NDHWC frame given as (B, D*H, W, C) sources.
+    Returns the X3 spectrum (kept for the backward)."""
+    B = x4[0].t.shape[0]
+    R1, R2 = min(D, 2 * m1), min(H, 2 * m2)
+    dev = x4[0].t.device
+    c64 = torch.complex64
+    X1 = torch.empty((B, D * H, m3, Cin), dtype=c64, device=dev)
+    X2 = torch.empty((B * D, R2, m3, Cin), dtype=c64, device=dev)
+    X3 = torch.empty((B, R1, R2 * m3, Cin), dtype=c64, device=dev)
+    Y = torch.empty((B, R1, R2 * m3, Cout), dtype=c64, device=dev)
+    Z1 = torch.empty((B, D, R2 * m3, Cout), dtype=c64, device=dev)
+    Z2 = torch.empty((B * D, H, m3, Cout), dtype=c64, device=dev)
+    s = stream_ptr()
+    check(lib.nps_spectral_dft_w(_c_src(x4), len(x4), B, D * H, W, Cin, m3, ptr(X1), s), "spectral3d dft_w")
+    check(lib.nps_spectral_dft_h(ptr(X1), ptr(X2), B * D, H, m2, m3, Cin, s), "spectral3d dft_h (H)")
+    check(lib.nps_spectral_dft_h(ptr(X2), ptr(X3), B, D, m1, R2 * m3, Cin, s), "spectral3d dft_h (D)")
+    check(lib.nps_spectral_mix(ptr(X3), ptr(wpack), ptr(Y), B, R1, R2 * m3, Cin, Cout, s), "spectral3d mix")
+    check(lib.nps_spectral_idft_h(ptr(Y), ptr(Z1), B, D, m1, R2 * m3, Cout, s), "spectral3d idft_h (D)")
+    check(lib.nps_spectral_idft_h(ptr(Z1), ptr(Z2), B * D, H, m2, m3, Cout, s), "spectral3d idft_h (H)")
+    check(lib.nps_spectral_idft_w(ptr(Z2), ptr(out), B, D * H, W, m3, Cout, 1 if accumulate else 0, ptr(addend), act,
+                                  s), "spectral3d idft_w")
+    return X3
+
+
+def spectral_conv3d(srcs: Sequence[Src], D: int, wpack: torch.Tensor, m1: int, m2: int, m3: int, Cout: int,
+                    out: Optional[torch.Tensor] = None, accumulate=False, addend=None, act=0):
+    """y = irfftn(P(rfftn(x))) on the 4 retained corners (proc_fno.py:334-376).  Sources are NDHWC
+    tensors viewed as (B, D*H, W, C); returns (B, D*H, W, Cout) (view it as (B, D, H, W, Cout))."""
+    t0 = srcs[0].t
+    B, DH, W = t0.shape[0], t0.shape[1], t0.shape[2]
+    H = DH // D
+    Cin = sum(s.t.shape[3] for s in srcs)
+    check_modes3d(D, H, W, m1, m2, m3)
+    if out is None:
+        out = empty_nhwc(B, DH, W, Cout, t0)
+        accumulate = False
+    spectral_conv3d_stages(srcs, D, H, W, Cin, wpack, m1, m2, m3, Cout, out, accumulate, addend, act)
+    return out
+
+
 # ----------------------------------------------------------- misc kernels -----
 def nchw_to_nhwc(x: torch.Tensor) -> torch.Tensor:
     x = x.contiguous()

@@ -12,6 +12,7 @@ import torch.nn.functional as F
 
 __all__ = [
     "crop_nd", "conv2d_ref", "conv_transpose_ref", "spectral_conv2d", "spectral_conv3d", "fno_layer", "fno",
+    "fno_layer3d", "fno3d",
     "residual_block", "unet_modern", "dilated_resnet", "ufno", "enc_elementwise", "add_delta",
     "dec_timeconvdense", "unet_structure",
 ]
@@ -113,6 +114,23 @@ def fno(sd, p, cfg, h, vb):
         h_in = torch.cat([h, vb], dim=1) if vb is not None else h
         h = fno_layer(sd, _j(p, f"fno_layers.{i}"), h_in, activation=True, padding_mode=pm,
                       conv_mode=cfg.get("fno_conv_mode", "single"))
+    return h
+
+
+def fno_layer3d(sd, p, x, activation=True):
+    """FNO_Layer.forward with num_spatial_dims=3, proc_fno.py:133-155: SpectralConv3d(x) + Conv3d 1x1x1 `w`
+    (fno_kernel_size 1, conv_mode 'single'), then GELU."""
+    x1 = spectral_conv3d(x, *[sd[_j(p, f"conv.weights{i}")] for i in range(1, 5)])
+    x2 = F.conv3d(x, sd[_j(p, "w.weight")], sd[_j(p, "w.bias")])
+    y = x1 + x2
+    return gelu(y) if activation else y
+
+
+def fno3d(sd, p, cfg, h, vb):
+    """FNO.forward (3-D, cond_mode='concat'), proc_fno.py:73-83."""
+    for i in range(cfg.get("hidden_blocks", 4)):
+        h_in = torch.cat([h, vb], dim=1) if vb is not None else h
+        h = fno_layer3d(sd, _j(p, f"fno_layers.{i}"), h_in)
     return h
 
 

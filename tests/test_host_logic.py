@@ -89,3 +89,19 @@ def test_simulate_window_indices():
     assert d[0, 0, :, 0, 0].tolist() == list(range(0, 25)) and l[0, 0, :, 0, 0].tolist() == list(range(25, 50))
     steps = list(range(25, 501 - 25 + 1, 25))
     assert len(steps) == (501 - 2 * 25) // 25 + 1 == 19
+
+
+def test_fno3d_construction_matches_reference_seeded_init():
+    """The 3-D FNO mirror (SpectralConv3d + pointwise Conv3d) builds the reference's parameters bit for bit."""
+    import torch
+    from conftest import load_golden
+    from models.enc_proc_dec_components.proc_fno import FNO
+    g = load_golden("fno3d")
+    kw = dict(g["kwargs"])
+    kw["fno_modes"] = tuple(kw["fno_modes"])
+    torch.manual_seed(42)
+    m = FNO(pde=None, **kw)
+    sd = m.state_dict()
+    assert list(sd) == list(g["state_dict"])
+    for k, v in g["state_dict"].items():
+        assert torch.equal(sd[k], v), k
