@@ -108,8 +108,9 @@ size_t nps_conv2d_packed_size(int Cout, int Cin, int ntaps);
  * weight w[Cout][Cin/4][3][3] for the space-to-depth 2x2 form (KH = KW = 2, Cin = 4C). */
 int nps_conv2d_pack_weights(const float* w, float* wpack, int Cout, int Cin, int KH, int KW,
                             int transposed_phase, void* stream);
-/* Same transforms, packed as [hi | lo * 2^11] fp16 MFMA fragments for precision = NPS_PREC_X3F16
- * (same buffer size as nps_conv2d_packed_size). */
+/* Same transforms, packed as [hi | lo] fp16 MFMA fragments of s*w for precision = NPS_PREC_X3F16, with s
+ * the power of 2 that maps max|w| into [2^13, 2^14) (max|w| is kept in the buffer's trailer; same buffer
+ * size as nps_conv2d_packed_size). */
 int nps_conv2d_pack_weights_x3(const float* w, float* wpack, int Cout, int Cin, int KH, int KW,
                                int transposed_phase, void* stream);
 /* 1 when a conv of this geometry runs on the split-fp16 kernel (stride-1, undilated 1x1 / 2x2 / 3x3). */
@@ -129,7 +130,8 @@ int nps_conv2d_plan(nps_conv2d_t* a);
 int nps_conv2d_fwd(const nps_conv2d_t* a, void* stream);
 
 /* Materialise a virtual frame: out[B][Hin][Win][Cin] = act(GN(frame)) using the prologue fields
- * of `a` (or the plain concat/crop when there is none).  One HBM pass that evaluates the
+ * of `a` (or the plain concat/crop when there is none); with a->out_C in (Cin, Cin + 4) the output
+ * rows are out_C channels wide, the extra channels zero (4-channel alignment for the split-fp16 conv).  One HBM pass that evaluates the
  * GroupNorm affine + GELU once per element (proc_unet_modern.py:245-247) ahead of a conv that
  * then stages raw bytes only. */
 int nps_frame_pack(const nps_conv2d_t* a, float* out, void* stream);
@@ -281,6 +283,13 @@ int nps_volume_rescale_bwd(const float* g, const double* new_tot, const double* 
 
 const char* nps_last_error(void);
 const char* nps_version(void);
+
+/* ---- on-disk data path: device-resident windowing (common/data_creator.py:48-78, create_data) ----
+ * out[b][c][t][hw] = u[b][c][steps[b] + offset + t][hw], t < tw; u (B, C, T, H*W) and out (B, C, tw, H*W)
+ * contiguous fp32 device arrays, steps[B] int32 on the device (offset = -tw: model inputs, 0: labels;
+ * the caller checks steps[b] + offset >= 0 and steps[b] + offset + tw <= T, as the reference asserts). */
+int nps_gather_windows(const float* u, const int* steps, float* out, int B, int C, int T, long HW, int tw, int offset,
+                       void* stream);
 
 #ifdef __cplusplus
 }

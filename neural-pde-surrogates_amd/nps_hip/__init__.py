@@ -101,6 +101,7 @@ _SIGS = {
     "nps_spectral_dft_w_bwd": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp]),
     "nps_spectral_mix_bwd": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _vp]),
     "nps_spectral_unpack_grad": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _vp]),
+    "nps_gather_windows": (_i, [_vp, _vp, _vp, _i, _i, _i, _l, _i, _i, _vp]),
     "nps_spectral3d_pack_weights": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp]),
     "nps_spectral3d_unpack_grad": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp]),
     "nps_timeconv_decode_bwd": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp, _vp, _i, _i, _i, _i,

@@ -324,6 +324,26 @@ def spectral_conv3d(srcs: Sequence[Src], D: int, wpack: torch.Tensor, m1: int, m
     return out
 
 
+# ------------------------------------------------------------------ data path -----
+def gather_windows(u: torch.Tensor, steps, tw: int, offset: int) -> torch.Tensor:
+    """out[b] = u[b][:, steps[b] + offset : steps[b] + offset + tw] for a device-resident trajectory batch
+    u (B, C, T, *spatial) — DataCreator.create_data's per-sample windows (common/data_creator.py:48-78) as
+    one HIP gather (nps_gather_windows)."""
+    u = u.contiguous()
+    B, C, T = u.shape[:3]
+    HW = math.prod(u.shape[3:]) if u.dim() > 3 else 1
+    if len(steps) != B:
+        raise ValueError(f"gather_windows: {len(steps)} steps for a batch of {B}")
+    for st in steps:
+        if st + offset < 0 or st + offset + tw > T:
+            raise AssertionError("this step - time window combination is not valid")
+    st_dev = torch.tensor([int(v) for v in steps], dtype=torch.int32).to(u.device, non_blocking=True)
+    out = torch.empty((B, C, tw) + tuple(u.shape[3:]), dtype=torch.float32, device=u.device)
+    check(lib.nps_gather_windows(ptr(u), ptr(st_dev), ptr(out), B, C, T, HW, tw, offset, stream_ptr()),
+          "gather_windows")
+    return out
+
+
 # ----------------------------------------------------------- misc kernels -----
 def nchw_to_nhwc(x: torch.Tensor) -> torch.Tensor:
     x = x.contiguous()

@@ -24,7 +24,9 @@ from nps_hip import autograd as ad
 
 
 class DataCreator:
-    """common/data_creator.py:48-78 (windowing only; the GNN graph builders are not built)."""
+    """common/data_creator.py:48-78 (windowing only; the GNN graph builders are not built).  Windows of
+    device-resident batches are cut on the device (one view when every sample shares the step, else one
+    HIP gather); the per-sample slicing + torch.cat of the reference remains for host tensors."""
 
     def __init__(self, pde=None, neighbors: int = 2, time_window: int = 5, t_resolution: int = 250,
                  x_resolution=100):
@@ -41,6 +43,7 @@ class DataCreator:
 
     def create_data(self, datapoints: torch.Tensor, steps: list, mode="both"):
         assert mode in ["data", "labels", "both"]
+        steps = list(steps)[:datapoints.shape[0]]  # zip(datapoints, steps) semantics (a short last batch)
         T = datapoints.shape[2]
         for step in steps:
             assert step - self.tw >= 0 and step + self.tw <= T, 'this step - time window combination is not valid'
@@ -48,6 +51,10 @@ class DataCreator:
             s = steps[0]
             data = datapoints[:, :, s - self.tw:s]
             labels = datapoints[:, :, s:s + self.tw]
+        elif datapoints.is_cuda and datapoints.dtype == torch.float32:
+            # per-sample windows of a device-resident batch: one HIP gather each (nps_gather_windows)
+            data = ops.gather_windows(datapoints, steps, self.tw, -self.tw) if mode != "labels" else None
+            labels = ops.gather_windows(datapoints, steps, self.tw, 0) if mode != "data" else None
         else:
             data = torch.stack([dp[:, s - self.tw:s] for dp, s in zip(datapoints, steps)])
             labels = torch.stack([dp[:, s:s + self.tw] for dp, s in zip(datapoints, steps)])
@@ -81,6 +88,23 @@ class AutoregressivePushforwardTrainer:
                                         time_window=self.config.time_window,
                                         t_resolution=self.config.base_resolution[0],
                                         x_resolution=self.config.base_resolution[1])
+
+    def get_dataloaders(self):
+        """trainers/base.py:157-179 (fixed-length time): train / valid / test loaders over the dataset's
+        splits.  On a GPU device the loaders are device-resident (data.DeviceLoader: batches read from the
+        memmaps, pinned and copied on a side HIP stream ahead of use); on the CPU they are the reference's
+        DataLoader(shuffle=True)."""
+        if getattr(self.config, "variable_time", False):
+            raise NotImplementedError("variable-length time (sim1d_var_t) is not on the grid path")
+        device = torch.device(self.config.device)
+        bs = self.config.batch_size
+        if device.type == "cuda":
+            from data.device_loader import DeviceLoader
+            return tuple(DeviceLoader(d, bs, shuffle=True, device=device)
+                         for d in (self.data.train, self.data.valid, self.data.test))
+        from torch.utils.data import DataLoader
+        return tuple(DataLoader(d, batch_size=bs, shuffle=True, num_workers=getattr(self.config, "nw", 0))
+                     for d in (self.data.train, self.data.valid, self.data.test))
 
     def _loss(self, pred, labels):
         c = self.criterion

@@ -28,4 +28,4 @@ for s in $STEPS; do
   esac
   echo "step $s ok"
 done
-tail -3 gpurun_out/${TAG}_tests.log 2>/dev/null; tail -1 gpurun_out/${TAG}_bench.log 2>/dev/null
+tail -3 gpurun_out/${TAG}_tests.log 2>/dev/null; tail -1 gpurun_out/${TAG}_bench.log 2>/dev/null; true
