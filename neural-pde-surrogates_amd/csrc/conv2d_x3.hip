@@ -47,6 +47,15 @@ __device__ unsigned long long x3_stamps[1 << 20];
 #define X3_RSTAMP(i)
 #endif
 
+// s_waitcnt vmcnt(N) that the compiler sees as redefining every register of rp: no read of a
+// register loaded by an inline-asm global_load can be scheduled above the wait that covers it.
+template <int N, int MAXP>
+__device__ __forceinline__ void x3_vm_wait(f32x4 (&rp)[MAXP]) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+#pragma unroll
+    for (int k = 0; k < MAXP; ++k) asm volatile("" : "+v"(rp[k]));
+}
+
 template <int N, typename F>
 __device__ __forceinline__ void static_for(F&& f) {
     if constexpr (N > 0) {
@@ -128,22 +137,42 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
         const int ptid = tid - 256;
         const int ybase = oy0 - a.pad_y, xbase = ox0 - a.pad_x;
         const int Hext = a.Hin + 2 * a.circ, Wext = a.Win + 2 * a.circ;
-        int sy[MAXP], sx[MAXP];
-#pragma unroll
-        for (int k = 0; k < MAXP; ++k) {
-            const int idx = ptid + k * 256;
-            const int p = idx >> 2;
-            const int pr = p / g.PW, pc = p - pr * g.PW;
-            const int ye = ybase + pr, xe = xbase + pc;
-            const bool ok = idx < NG && ye >= 0 && ye < Hext && xe >= 0 && xe < Wext;
-            sy[k] = ok ? (a.circ ? nps::wrap_mod(ye - a.circ, a.Hin) : ye) : -1;
-            sx[k] = ok ? (a.circ ? nps::wrap_mod(xe - a.circ, a.Win) : xe) : 0;
-        }
         const float xs = in_scale_of(a);
         f32x4 r0[MAXP];
+        // Per-slot source addresses: the patch pixel of slot k is fixed for the whole work-group, so its
+        // address in the current source (and whether it lies inside it) is computed only when a stage's
+        // source changes (a U-FNO frame has 1-3 sources); a stage then costs one add + one load per slot.
+        // Slot k holds channels [4*gq, 4*gq + 4) of the stage, gq = ptid & 3 for every k.
+        const int gq = ptid & 3;
+        const float* sbase[MAXP];
+        unsigned pixm = 0;  // slots whose pixel lies inside the current source
+        int cur_src = -1;
+        auto locate = [&](int sidx) {
+            const nps_src_t S0 = a.src[0], S1 = a.src[1], S2 = a.src[2];
+            const float* sptr = sidx == 0 ? S0.ptr : (sidx == 1 ? S1.ptr : S2.ptr);
+            const int sC = sidx == 0 ? S0.C : (sidx == 1 ? S1.C : S2.C);
+            const int sH = sidx == 0 ? S0.H : (sidx == 1 ? S1.H : S2.H);
+            const int sW = sidx == 0 ? S0.W : (sidx == 1 ? S1.W : S2.W);
+            const int soy = sidx == 0 ? S0.off_y : (sidx == 1 ? S1.off_y : S2.off_y);
+            const int sox = sidx == 0 ? S0.off_x : (sidx == 1 ? S1.off_x : S2.off_x);
+            pixm = 0;
+#pragma unroll
+            for (int k = 0; k < MAXP; ++k) {
+                const int idx = ptid + k * 256;
+                const int p = idx >> 2;
+                const int pr = p / g.PW, pc = p - pr * g.PW;
+                const int ye = ybase + pr, xe = xbase + pc;
+                bool ok = idx < NG && ye >= 0 && ye < Hext && xe >= 0 && xe < Wext;
+                const int fy = a.circ ? nps::wrap_mod(ye - a.circ, a.Hin) : ye;
+                const int fx = a.circ ? nps::wrap_mod(xe - a.circ, a.Win) : xe;
+                const int yy = fy - soy, xx = fx - sox;
+                ok = ok && yy >= 0 && yy < sH && xx >= 0 && xx < sW;
+                sbase[k] = sptr + (ok ? ((size_t)(b * sH + yy) * sW + xx) * sC : (size_t)b * sH * sW * sC);
+                pixm = ok ? (pixm | (1u << k)) : pixm;
+            }
+        };
         // issue() returns the mask of slots holding in-frame data; commit() zeroes the others
         auto issue = [&](int st, f32x4 (&rp)[MAXP]) -> unsigned {
-            unsigned okm = 0;
             const int c0 = st * CK;
             const int cend = min(c0 + CK, a.Cin);
             int sidx = 0, cbase = 0;
@@ -153,7 +182,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
                 for (int si = 0; si < NPS_MAX_SRC; ++si) {  // unrolled: static kernarg indexing
                     if (si < a.nsrc) {
                         const int hi = lo + a.src[si].C;
-                        if (c0 >= lo && cend <= hi && (a.src[si].C & 3) == 0 && ((c0 - lo) & 3) == 0) {
+                        if (c0 >= lo && cend <= hi) {  // host-checked (x3_sources_aligned): one source per stage
                             sidx = si;
                             cbase = lo;
                         }
@@ -161,29 +190,26 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
                     }
                 }
             }
-            // host-checked (x3_sources_aligned): every 16-channel stage lies in one 4-aligned source
-            {
-                const nps_src_t S0 = a.src[0], S1 = a.src[1], S2 = a.src[2];
-                const float* sptr = sidx == 0 ? S0.ptr : (sidx == 1 ? S1.ptr : S2.ptr);
-                const int sC = sidx == 0 ? S0.C : (sidx == 1 ? S1.C : S2.C);
-                const int sH = sidx == 0 ? S0.H : (sidx == 1 ? S1.H : S2.H);
-                const int sW = sidx == 0 ? S0.W : (sidx == 1 ? S1.W : S2.W);
-                const int soy = sidx == 0 ? S0.off_y : (sidx == 1 ? S1.off_y : S2.off_y);
-                const int sox = sidx == 0 ? S0.off_x : (sidx == 1 ? S1.off_x : S2.off_x);
-                const int cs = c0 - cbase;
-                // every lane loads (padding lanes from the sample's first pixel) and then selects: no
-                // branch around the loads, so the in-order vmcnt accounting stays exact
-#pragma unroll
-                for (int k = 0; k < MAXP; ++k) {
-                    const int gq = (ptid + k * 256) & 3;
-                    const int yy = sy[k] - soy, xx = sx[k] - sox;
-                    const bool ok = sy[k] >= 0 && yy >= 0 && yy < sH && xx >= 0 && xx < sW && c0 + gq * 4 < cend;
-                    const size_t off = ok ? ((size_t)(b * sH + yy) * sW + xx) * sC + cs + gq * 4 : (size_t)b * sH * sW * sC;
-                    rp[k] = *reinterpret_cast<const f32x4*>(sptr + off);
-                    okm = ok ? (okm | (1u << k)) : okm;  // zeroed at commit: no use of a load before all are issued
-                }
+            if (sidx != cur_src) {  // uniform
+                locate(sidx);
+                cur_src = sidx;
             }
-            return okm;
+            // this lane's channel offset in the source pixel; lanes past the channel tail of the last stage
+            // read the pixel's first channels instead (in bounds; zeroed at commit)
+            const bool chok = c0 + gq * 4 < cend;
+            const unsigned chm = chok ? ~0u : 0u;
+            const int cs = chok ? c0 - cbase + gq * 4 : 0;
+#pragma unroll
+            for (int k = 0; k < MAXP; ++k) {
+#ifdef NPS_X3_CLOAD
+                rp[k] = *reinterpret_cast<const f32x4*>(sbase[k] + cs);
+#else
+                // issued as inline asm: invisible to the compiler's vmcnt tracking, waited for by
+                // x3_vm_wait one loop iteration later (see the schedule below)
+                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(rp[k]) : "v"(sbase[k] + cs));
+#endif
+            }
+            return pixm & chm;
         };
         auto commit = [&](int st, const f32x4 (&rp)[MAXP], unsigned okm) {
             char* Pt = ring + (st % X3_NST) * stage_b;
@@ -205,15 +231,15 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
         for (int st = 0; st < nstages; ++st) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         return;
 #endif
+#ifdef NPS_X3_CLOAD
         // Iteration st (while the consumers compute stage st): fetch stage st + 2, split it into the ring
-        // slot (st + 2) % 3 that the consumers released at the last barrier, barrier.  The fetch is
-        // waited for inside the iteration that issued it (a load carried across the loop's back edge
-        // makes the compiler drain every load at the latch), so its latency hides behind one consumer
-        // stage.  Barriers: 1 + nstages, as the consumers.
+        // slot (st + 2) % 3 that the consumers released at the last barrier, barrier.  Compiler-tracked
+        // loads must be waited for in the iteration that issued them (a load carried across the loop's
+        // back edge makes the compiler drain every load at the latch).
         {
             f32x4 r1[MAXP];
             const unsigned m0 = issue(0, r0);
-            const unsigned m1 = issue(min(1, nstages - 1), r1);  // both prologue fetches in flight together
+            const unsigned m1 = issue(min(1, nstages - 1), r1);
             commit(0, r0, m0);
             if (nstages > 1) commit(1, r1, m1);
         }
@@ -225,6 +251,34 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
             }
             asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         }
+#else
+        // Iteration st (while the consumers compute stage st): wait for stage st + 2's fetch (issued one
+        // iteration earlier), split it into ring slot (st + 2) % 3 (released by the consumers at the
+        // last barrier), fetch stage st + 3, barrier.  Each fetch thus has a whole consumer stage plus
+        // the barrier to land.  The fetches are inline-asm loads, waited for with explicit vmcnt waits
+        // that take the destination registers as operands (so no use can move above the wait).
+        // Stage indices past the end are clamped (the fetch is still issued, so the count of loads in
+        // flight is the same on every path); commits past the end are skipped.  Barriers: 1 + nstages.
+        const int last = nstages - 1;
+        {
+            f32x4 r1[MAXP];
+            const unsigned m0 = issue(0, r0);
+            const unsigned m1 = issue(min(1, last), r1);
+            x3_vm_wait<MAXP>(r0);
+            commit(0, r0, m0);
+            x3_vm_wait<0>(r1);
+            if (nstages > 1) commit(1, r1, m1);
+        }
+        unsigned m = issue(min(2, last), r0);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        for (int st = 0; st < nstages; ++st) {
+            x3_vm_wait<0>(r0);
+            if (st + 2 < nstages) commit(st + 2, r0, m);
+            m = issue(min(st + 3, last), r0);
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+        x3_vm_wait<0>(r0);  // drain the last (clamped) fetch before the registers are reused
+#endif
         if (!x3_lds_epilogue(a)) return;
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // consumers' tile is in LDS
         x3_store_phase<TILE_PX>(a, b, cob, oy0, ox0, reinterpret_cast<const float*>(ring), tid);
