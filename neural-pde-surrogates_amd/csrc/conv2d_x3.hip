@@ -341,7 +341,6 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
         loadA(gclamp(gg + 1), Aw[r ^ 1]);
         loadB(gclamp(gg + 1), Bh[r ^ 1], 0);
         loadB(gclamp(gg + 1), Bl[r ^ 1], 1);
-        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int cb = 0; cb < CBW; ++cb)
 #pragma unroll
@@ -354,6 +353,19 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
         for (int cb = 0; cb < CBW; ++cb)
 #pragma unroll
             for (int pb = 0; pb < PB; ++pb) acc[cb][pb] = X3_MFMA(Aw[r][cb][1], Bh[r][pb], acc[cb][pb], 0, 0, 0);
+        // interleave the next group's loads with this group's MFMAs (one LDS read / one weight load per
+        // MFMA gap) instead of issuing them as a block in front of the MFMAs, which idles the matrix pipe
+#pragma unroll
+        for (int i = 0; i < 2 * CBW; ++i) {  // weights first: the longest latency gets the most cover
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // 1 VMEM read
+        }
+#pragma unroll
+        for (int i = 0; i < 2 * PB; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 6 * CBW * PB - 2 * PB - 2 * CBW, 0);
         __builtin_amdgcn_sched_barrier(0);
         if ((gg + 1) % NTAPS == 0) {
 #ifdef NPS_X3_STAMP
