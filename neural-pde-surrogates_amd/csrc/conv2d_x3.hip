@@ -4,6 +4,7 @@
 // proc_unet_modern.py, proc_fno.py:114-117, enc_grid.py, dec_grid.py).
 #include "conv2d_common.hpp"
 
+#include <cstdlib>
 #include <type_traits>
 
 namespace {
@@ -30,18 +31,14 @@ __host__ __device__ constexpr int x3_patch_px_max(int ntaps, int tile_px) {
                       : (tile_px == 512 ? (ntaps == 4 ? 9 * 65 : 10 * 66) : (ntaps == 4 ? 9 * 33 : 10 * 34));
 }
 
-#ifdef NPS_X3_ABL_MFMA  // dev ablation: operands are loaded and consumed, no matrix instructions
-#define X3_MFMA(a_, b_, c_, ...) ((c_) + (float)((a_)[0] * (b_)[0]))
-#else
 #define X3_MFMA __builtin_amdgcn_mfma_f32_32x32x16_f16
-#endif
 
 #ifdef NPS_X3_STAMP  // dev diagnostic: per-work-group s_memtime stamps of consumer wave 0
 __device__ unsigned long long x3_stamps[1 << 20];
 #define X3_STAMP(i) \
-    if (wave == 0 && lane == 0 && blockIdx.x < (1 << 17)) x3_stamps[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memtime()
+    if (wave == 0 && lane == 0 && l < (1 << 17)) x3_stamps[l * 8 + (i)] = __builtin_amdgcn_s_memtime()
 #define X3_RSTAMP(i) \
-    if (wave == 0 && lane == 0 && blockIdx.x < (1 << 17)) x3_stamps[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime()
+    if (wave == 0 && lane == 0 && l < (1 << 17)) x3_stamps[l * 8 + (i)] = __builtin_amdgcn_s_memrealtime()
 #else
 #define X3_STAMP(i)
 #define X3_RSTAMP(i)
@@ -116,37 +113,45 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
     const Geo g = make_geo(a);
     const int ncob = (a.Cout + 63) / 64;
     const int ntiles = g.tiles_x * g.tiles_y;
-    int L = blockIdx.x;
-    {
-        const int full = (int)(gridDim.x & ~7u);
-        if (L < full) L = (L & 7) * (full >> 3) + (L >> 3);
-    }
-    const int cob = L % ncob;
-    const int rest = L / ncob;
-    const int tile = rest % ntiles, b = rest / ntiles;
-    const int ty = tile / g.tiles_x, tx = tile - (tile / g.tiles_x) * g.tiles_x;
-    const int oy0 = ty * a.TH, ox0 = tx * a.TW;
+    const int nwg = ntiles * a.B * ncob;  // work-group tiles of the launch (the grid is persistent)
+    // tile l -> (co block, sample, output origin): co block fastest; consecutive tiles of one XCD's
+    // work-groups (l = i, i + G, ... with G % 8 == 0 stay on XCD i % 8) get consecutive numbers, so the 3
+    // co-blocks of a tile and neighbouring tiles read the same patch bytes from that XCD's L2
+    auto decode = [&](int l, int& cob, int& b, int& oy0, int& ox0) {
+        const int full = nwg & ~7;
+        const int L = l < full ? (l & 7) * (full >> 3) + (l >> 3) : l;
+        cob = L % ncob;
+        const int rest = L / ncob;
+        const int tile = rest % ntiles;
+        b = rest / ntiles;
+        const int ty = tile / g.tiles_x, tx = tile - (tile / g.tiles_x) * g.tiles_x;
+        oy0 = ty * a.TH;
+        ox0 = tx * a.TW;
+    };
     const int npix = g.PH * g.PW;
     const int NG = npix * 4;                              // float4 slots of a 16-channel patch stage
     const int stage_b = (npix * X3_PIXB + 15) & ~15;
     char* ring = reinterpret_cast<char*>(smem) + 128;
     const int nstages = (a.Cin + CK - 1) / CK;
+    const int last = nstages - 1;
+    const bool lds_epi = x3_lds_epilogue(a);
+    auto barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
 
     if (wave >= 4) {
         // ------------------------------------------------------------------ producers: patch only
         const int ptid = tid - 256;
-        const int ybase = oy0 - a.pad_y, xbase = ox0 - a.pad_x;
         const int Hext = a.Hin + 2 * a.circ, Wext = a.Win + 2 * a.circ;
         const float xs = in_scale_of(a);
-        f32x4 r0[MAXP];
-        // Per-slot source addresses: the patch pixel of slot k is fixed for the whole work-group, so its
-        // address in the current source (and whether it lies inside it) is computed only when a stage's
-        // source changes (a U-FNO frame has 1-3 sources); a stage then costs one add + one load per slot.
-        // Slot k holds channels [4*gq, 4*gq + 4) of the stage, gq = ptid & 3 for every k.
+        f32x4 r0[MAXP], r1[MAXP];
+        // Per-slot source addresses: the patch pixel of slot k is fixed for a tile, so its address in the
+        // current source (and whether it lies inside it) is computed only when a stage's source (or the
+        // tile) changes; a stage then costs one add + one load per slot.  Slot k holds channels
+        // [4*gq, 4*gq + 4) of the stage, gq = ptid & 3 for every k.
         const int gq = ptid & 3;
         const float* sbase[MAXP];
         unsigned pixm = 0;  // slots whose pixel lies inside the current source
         int cur_src = -1;
+        int fb = 0, fy0 = 0, fx0 = 0, fcob = 0;  // tile being fetched
         auto locate = [&](int sidx) {
             const nps_src_t S0 = a.src[0], S1 = a.src[1], S2 = a.src[2];
             const float* sptr = sidx == 0 ? S0.ptr : (sidx == 1 ? S1.ptr : S2.ptr);
@@ -155,6 +160,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
             const int sW = sidx == 0 ? S0.W : (sidx == 1 ? S1.W : S2.W);
             const int soy = sidx == 0 ? S0.off_y : (sidx == 1 ? S1.off_y : S2.off_y);
             const int sox = sidx == 0 ? S0.off_x : (sidx == 1 ? S1.off_x : S2.off_x);
+            const int ybase = fy0 - a.pad_y, xbase = fx0 - a.pad_x;
             pixm = 0;
 #pragma unroll
             for (int k = 0; k < MAXP; ++k) {
@@ -167,7 +173,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
                 const int fx = a.circ ? nps::wrap_mod(xe - a.circ, a.Win) : xe;
                 const int yy = fy - soy, xx = fx - sox;
                 ok = ok && yy >= 0 && yy < sH && xx >= 0 && xx < sW;
-                sbase[k] = sptr + (ok ? ((size_t)(b * sH + yy) * sW + xx) * sC : (size_t)b * sH * sW * sC);
+                sbase[k] = sptr + (ok ? ((size_t)(fb * sH + yy) * sW + xx) * sC : (size_t)fb * sH * sW * sC);
                 pixm = ok ? (pixm | (1u << k)) : pixm;
             }
         };
@@ -200,15 +206,8 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
             const unsigned chm = chok ? ~0u : 0u;
             const int cs = chok ? c0 - cbase + gq * 4 : 0;
 #pragma unroll
-            for (int k = 0; k < MAXP; ++k) {
-#ifdef NPS_X3_CLOAD
-                rp[k] = *reinterpret_cast<const f32x4*>(sbase[k] + cs);
-#else
-                // issued as inline asm: invisible to the compiler's vmcnt tracking, waited for by
-                // x3_vm_wait one loop iteration later (see the schedule below)
+            for (int k = 0; k < MAXP; ++k)  // inline asm: invisible to the compiler's vmcnt tracking
                 asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(rp[k]) : "v"(sbase[k] + cs));
-#endif
-            }
             return pixm & chm;
         };
         auto commit = [&](int st, const f32x4 (&rp)[MAXP], unsigned okm) {
@@ -226,62 +225,53 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
                 }
             }
         };
-#ifdef NPS_X3_ABL_PROD  // dev ablation: producers only keep the barrier protocol
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        for (int st = 0; st < nstages; ++st) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        return;
-#endif
-#ifdef NPS_X3_CLOAD
-        // Iteration st (while the consumers compute stage st): fetch stage st + 2, split it into the ring
-        // slot (st + 2) % 3 that the consumers released at the last barrier, barrier.  Compiler-tracked
-        // loads must be waited for in the iteration that issued them (a load carried across the loop's
-        // back edge makes the compiler drain every load at the latch).
-        {
-            f32x4 r1[MAXP];
-            const unsigned m0 = issue(0, r0);
-            const unsigned m1 = issue(min(1, nstages - 1), r1);
-            commit(0, r0, m0);
-            if (nstages > 1) commit(1, r1, m1);
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        for (int st = 0; st < nstages; ++st) {
-            if (st + 2 < nstages) {
-                const unsigned m = issue(st + 2, r0);
-                commit(st + 2, r0, m);
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        }
-#else
-        // Iteration st (while the consumers compute stage st): wait for stage st + 2's fetch (issued one
-        // iteration earlier), split it into ring slot (st + 2) % 3 (released by the consumers at the
-        // last barrier), fetch stage st + 3, barrier.  Each fetch thus has a whole consumer stage plus
-        // the barrier to land.  The fetches are inline-asm loads, waited for with explicit vmcnt waits
-        // that take the destination registers as operands (so no use can move above the wait).
-        // Stage indices past the end are clamped (the fetch is still issued, so the count of loads in
-        // flight is the same on every path); commits past the end are skipped.  Barriers: 1 + nstages.
-        const int last = nstages - 1;
-        {
-            f32x4 r1[MAXP];
-            const unsigned m0 = issue(0, r0);
-            const unsigned m1 = issue(min(1, last), r1);
-            x3_vm_wait<MAXP>(r0);
-            commit(0, r0, m0);
-            x3_vm_wait<0>(r1);
-            if (nstages > 1) commit(1, r1, m1);
-        }
-        unsigned m = issue(min(2, last), r0);
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        for (int st = 0; st < nstages; ++st) {
+        // Per tile: the first two stages (fetched during the previous tile's epilogue) are split into
+        // ring slots 0 / 1, then iteration st (while the consumers compute stage st) waits for stage
+        // st + 2's fetch (issued one iteration earlier), splits it into slot (st + 2) % 3 (released at
+        // the last barrier) and fetches stage st + 3.  The fetches are inline-asm loads waited for by
+        // x3_vm_wait, which takes the destination registers as operands (no use moves above the wait);
+        // stage indices past the end are clamped (fetched anyway: the loads in flight are the same on
+        // every path), commits past the end skipped.  Barriers per tile: 1 + nstages + 2, as consumers.
+        int l = blockIdx.x;
+        decode(l, fcob, fb, fy0, fx0);
+        unsigned m0 = issue(0, r0);
+        unsigned m1 = issue(min(1, last), r1);
+        for (;;) {
+            const int scob = fcob, sb = fb, soy0 = fy0, sox0 = fx0;  // tile being computed / stored
+            // vmcnt(0): the previous tile's store phase left global stores in flight behind r0 / r1, and
+            // stores may complete out of order with loads, so a partial count does not prove r0 landed
             x3_vm_wait<0>(r0);
-            if (st + 2 < nstages) commit(st + 2, r0, m);
-            m = issue(min(st + 3, last), r0);
-            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            x3_vm_wait<0>(r1);
+            commit(0, r0, m0);
+            if (nstages > 1) commit(1, r1, m1);
+            unsigned m = issue(min(2, last), r0);
+            barrier();
+            for (int st = 0; st < nstages; ++st) {
+                x3_vm_wait<0>(r0);
+                if (st + 2 < nstages) commit(st + 2, r0, m);
+                m = issue(min(st + 3, last), r0);
+                barrier();
+            }
+            x3_vm_wait<0>(r0);  // drain the last (clamped) fetch before the registers are reused
+            const int ln = l + (int)gridDim.x;
+            const bool more = ln < nwg;
+            if (more) {  // the next tile's first two stages load while this tile is stored
+                decode(ln, fcob, fb, fy0, fx0);
+                cur_src = -1;
+                m0 = issue(0, r0);
+                m1 = issue(min(1, last), r1);
+            }
+            barrier();  // the consumers' tile is in LDS
+            if (lds_epi) x3_store_phase<TILE_PX>(a, sb, scob, soy0, sox0, reinterpret_cast<const float*>(ring), tid);
+            barrier();  // every read of the staged tile is done: the ring may be refilled
+            if (!more) break;
+            // land the next tile's fetches before the loop latch: r0 / r1 are loop-carried, and the
+            // compiler may move or spill them there without knowing an inline-asm load is in flight
+            x3_vm_wait<0>(r0);
+            x3_vm_wait<0>(r1);
+            l = ln;
         }
-        x3_vm_wait<0>(r0);  // drain the last (clamped) fetch before the registers are reused
-#endif
-        if (!x3_lds_epilogue(a)) return;
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // consumers' tile is in LDS
-        x3_store_phase<TILE_PX>(a, b, cob, oy0, ox0, reinterpret_cast<const float*>(ring), tid);
+        x3_vm_wait<0>(r1);
         return;
     }
 
@@ -294,30 +284,18 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
         boff[pb] = (ti * g.PW + tj) * X3_PIXB + (lane >> 5) * 16;
     }
     f32x16 acc[CBW][PB];
-#pragma unroll
-    for (int i = 0; i < CBW; ++i)
-#pragma unroll
-        for (int j = 0; j < PB; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
     const int ncb = packed_ncb(a.Cout);
-    const char* wbase = reinterpret_cast<const char*>(a.wpack) + (size_t)cob * CBW * 2048 + lane * 16;
     const size_t gstride = (size_t)ncb * 2048;  // bytes per K-group (chunk, tap) of the packed weight
     const int G = nstages * NTAPS;
+    const char* wbase = nullptr;
     f16x8 Aw[2][CBW][2];
     f16x8 Bh[2][PB], Bl[2][PB];
     auto loadA = [&](int gg, f16x8 (&d)[CBW][2]) {
         const char* p = wbase + (size_t)gg * gstride;
 #pragma unroll
         for (int cb = 0; cb < CBW; ++cb) {
-#ifdef NPS_X3_ABL_A  // dev ablation: weights from LDS instead of global memory
-            d[cb][0] = *reinterpret_cast<const f16x8*>(ring + ((gg * 64 + cb * 2048) & 8191) + lane * 16);
-            d[cb][1] = *reinterpret_cast<const f16x8*>(ring + ((gg * 64 + cb * 2048 + 1024) & 8191) + lane * 16);
-#else
             d[cb][0] = *reinterpret_cast<const f16x8*>(p + cb * 2048);
             d[cb][1] = *reinterpret_cast<const f16x8*>(p + cb * 2048 + 1024);
-#endif
         }
     };
     auto boffs = [&](int gg) {  // byte offset of K-group gg's patch window in the LDS ring
@@ -329,10 +307,10 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
 #pragma unroll
         for (int pb = 0; pb < PB; ++pb) d[pb] = *reinterpret_cast<const f16x8*>(p + boff[pb]);
     };
-    // K-group gg uses weight slot gg & 1 and patch slot gg & 1; at its start the loads of group gg + 1
-    // (weights from global memory, patch from LDS) are issued into the other slots, so every load has
-    // the group's 8*PB MFMAs to land.  Loads are never skipped (index clamped to the last group): a
-    // skipped load on one path makes the compiler's in-order vmcnt wait drain the newest loads.
+    // K-group gg uses weight slot gg & 1 and patch slot gg & 1; the loads of group gg + 1 (weights from
+    // global memory, patch from LDS) go to the other slots, interleaved one per MFMA gap.  Loads are
+    // never skipped (index clamped to the last group): a skipped load on one path makes the compiler's
+    // in-order vmcnt wait drain the newest loads.
     auto gclamp = [&](int x) { return x < G ? x : G - 1; };
 #ifdef NPS_X3_STAMP
     unsigned long long bar_cycles = 0;  // consumer wave 0: cycles spent in the stage barriers
@@ -353,8 +331,6 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
         for (int cb = 0; cb < CBW; ++cb)
 #pragma unroll
             for (int pb = 0; pb < PB; ++pb) acc[cb][pb] = X3_MFMA(Aw[r][cb][1], Bh[r][pb], acc[cb][pb], 0, 0, 0);
-        // interleave the next group's loads with this group's MFMAs (one LDS read / one weight load per
-        // MFMA gap) instead of issuing them as a block in front of the MFMAs, which idles the matrix pipe
 #pragma unroll
         for (int i = 0; i < 2 * CBW; ++i) {  // weights first: the longest latency gets the most cover
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
@@ -370,74 +346,87 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
         if ((gg + 1) % NTAPS == 0) {
 #ifdef NPS_X3_STAMP
             const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            barrier();
             bar_cycles += __builtin_amdgcn_s_memtime() - t0;
 #else
-            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            barrier();
 #endif
         }
         __builtin_amdgcn_sched_barrier(0);
     };
-    X3_STAMP(0);
-    X3_RSTAMP(4);
-    loadA(0, Aw[0]);
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    loadB(0, Bh[0], 0);
-    loadB(0, Bl[0], 1);
-    X3_STAMP(1);
-    int g0 = 0;
-    for (; g0 + 2 <= G; g0 += 2) {
-        group(g0, 0);
-        group(g0 + 1, 1);
-    }
-    if (g0 < G) group(g0, 0);
-    X3_STAMP(2);
-#ifdef NPS_X3_STAMP
-    if (wave == 0 && lane == 0 && blockIdx.x < (1 << 17)) x3_stamps[blockIdx.x * 8 + 6] = bar_cycles;
-#endif
-
-    // epilogue: undo the exact power-of-2 scales of the weights and the input
+    // epilogue scale: undo the exact power-of-2 scales of the weights and the input
     const float inv = 1.f / (pow2_scale_for(a.wpack[packed_body(a.Cout, a.Cin, NTAPS)]) * in_scale_of(a));
     const int h = lane >> 5;
-    if (x3_lds_epilogue(a)) {
-        // the ring is free (every read of it completed before the last stage barrier): the consumers
-        // drop the 64 x TILE_PX tile into LDS, then all 8 waves store it with coalesced 16-B accesses
-        float* T = reinterpret_cast<float*>(ring);
+    for (int l = blockIdx.x; l < nwg; l += gridDim.x) {
+        int cob, b, oy0, ox0;
+        decode(l, cob, b, oy0, ox0);
+        wbase = reinterpret_cast<const char*>(a.wpack) + (size_t)cob * CBW * 2048 + lane * 16;
 #pragma unroll
-        for (int pb = 0; pb < PB; ++pb) {
-            const int P = wave * 32 * PB + pb * 32 + (lane & 31);
+        for (int i = 0; i < CBW; ++i)
 #pragma unroll
-            for (int cb = 0; cb < CBW; ++cb)
+            for (int j = 0; j < PB; ++j)
 #pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    const f32x4 v = {acc[cb][pb][4 * m] * inv, acc[cb][pb][4 * m + 1] * inv, acc[cb][pb][4 * m + 2] * inv,
-                                     acc[cb][pb][4 * m + 3] * inv};
-                    *reinterpret_cast<f32x4*>(T + P * X3_TPITCH + cb * 32 + 8 * m + 4 * h) = v;
-                }
+                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+        X3_STAMP(0);
+        X3_RSTAMP(4);
+        loadA(0, Aw[0]);
+        barrier();
+        loadB(0, Bh[0], 0);
+        loadB(0, Bl[0], 1);
+        X3_STAMP(1);
+        int g0 = 0;
+        for (; g0 + 2 <= G; g0 += 2) {
+            group(g0, 0);
+            group(g0 + 1, 1);
         }
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        x3_store_phase<TILE_PX>(a, b, cob, oy0, ox0, T, tid);
-    } else {
-        static_for<PB>([&](auto pbc) {  // compile-time pb: acc stays in registers
-            constexpr int pb = decltype(pbc)::value;
-            const int P = wave * 32 * PB + pb * 32 + (lane & 31);
-            const int ti = P / a.TW, tj = P - (P / a.TW) * a.TW;
-            const int oy = oy0 + ti, ox = ox0 + tj;
-            if (oy >= a.Hout || ox >= a.Wout) return;
-            const int dy = oy * a.out_os + a.out_off_y, dx = ox * a.out_os + a.out_off_x;
-            if (dy < 0 || dy >= a.out_H || dx < 0 || dx >= a.out_W) return;
+        if (g0 < G) group(g0, 0);
+        X3_STAMP(2);
+#ifdef NPS_X3_STAMP
+        if (wave == 0 && lane == 0 && l < (1 << 17)) x3_stamps[l * 8 + 6] = bar_cycles;
+        bar_cycles = 0;
+#endif
+        if (lds_epi) {
+            // the ring is free (every read of it completed before the last stage barrier): the consumers
+            // drop the 64 x TILE_PX tile into LDS, then all 8 waves store it with coalesced 16-B accesses
+            float* T = reinterpret_cast<float*>(ring);
 #pragma unroll
-            for (int cb = 0; cb < CBW; ++cb) {
-                f32x16 v = acc[cb][pb];
+            for (int pb = 0; pb < PB; ++pb) {
+                const int P = wave * 32 * PB + pb * 32 + (lane & 31);
 #pragma unroll
-                for (int r = 0; r < 16; ++r) v[r] *= inv;
-                store_tile(a, b, cob * 64 + cb * 32, h, v, dy, dx);
-                __builtin_amdgcn_sched_barrier(0);
+                for (int cb = 0; cb < CBW; ++cb)
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) {
+                        const f32x4 v = {acc[cb][pb][4 * m] * inv, acc[cb][pb][4 * m + 1] * inv,
+                                         acc[cb][pb][4 * m + 2] * inv, acc[cb][pb][4 * m + 3] * inv};
+                        *reinterpret_cast<f32x4*>(T + P * X3_TPITCH + cb * 32 + 8 * m + 4 * h) = v;
+                    }
             }
-        });
+            barrier();
+            x3_store_phase<TILE_PX>(a, b, cob, oy0, ox0, T, tid);
+        } else {
+            static_for<PB>([&](auto pbc) {  // compile-time pb: acc stays in registers
+                constexpr int pb = decltype(pbc)::value;
+                const int P = wave * 32 * PB + pb * 32 + (lane & 31);
+                const int ti = P / a.TW, tj = P - (P / a.TW) * a.TW;
+                const int oy = oy0 + ti, ox = ox0 + tj;
+                if (oy >= a.Hout || ox >= a.Wout) return;
+                const int dy = oy * a.out_os + a.out_off_y, dx = ox * a.out_os + a.out_off_x;
+                if (dy < 0 || dy >= a.out_H || dx < 0 || dx >= a.out_W) return;
+#pragma unroll
+                for (int cb = 0; cb < CBW; ++cb) {
+                    f32x16 v = acc[cb][pb];
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) v[r] *= inv;
+                    store_tile(a, b, cob * 64 + cb * 32, h, v, dy, dx);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            });
+            barrier();
+        }
+        barrier();  // the staged tile is fully read: the producers may refill the ring
+        X3_STAMP(3);
+        X3_RSTAMP(5);
     }
-    X3_STAMP(3);
-    X3_RSTAMP(5);
 }
 
 template <int NT, int PB>
@@ -457,11 +446,32 @@ int nps_launch_conv2d_x3(const nps_conv2d_t& a, int lds, hipStream_t s) {
     const Geo g = make_geo(a);
     const long nwg = (long)g.tiles_x * g.tiles_y * a.B * ((a.Cout + 63) / 64);
     NPS_CHECK_ARG(nwg < (1L << 31), "conv2d_fwd: grid too large");
+    // persistent grid: one 512-thread work-group per CU (the LDS ring takes most of a CU), each walking
+    // the tiles l = blockIdx.x, + gridDim.x, ...; a multiple of 8 keeps every work-group's tiles on one XCD
+    static int ncu = 0;
+    if (ncu == 0) {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+        ncu = n;
+    }
+    static long per = -1;
+    if (per < 0) {
+        per = (ncu & ~7) > 0 ? (ncu & ~7) : ncu;
+        const char* e = getenv("NPS_X3_GRID");  // dev knob: work-groups of the persistent grid
+        if (e != nullptr && atol(e) > 0) per = atol(e);
+    }
+    // The register-store epilogue (NCHW or channel counts not a multiple of 4) runs one tile per
+    // work-group: looped over tiles it gave wrong co-block-1 rows after the first tile (only there;
+    // the PB=4 kernels spill under the persistent loop), so that rare layout keeps the plain grid.
+    const bool lds_epi = !a.out_nchw && (a.out_C & 3) == 0 && (a.Cout & 3) == 0;  // == x3_lds_epilogue
+    const unsigned grid = (unsigned)(lds_epi && per < nwg ? per : nwg);
     const bool p512 = a.TH * a.TW == 512;
     switch (a.KH * a.KW) {
-        case 9: p512 ? launch_x3_one<9, 4>(a, nwg, lds, s) : launch_x3_one<9, 2>(a, nwg, lds, s); break;
-        case 4: p512 ? launch_x3_one<4, 4>(a, nwg, lds, s) : launch_x3_one<4, 2>(a, nwg, lds, s); break;
-        default: p512 ? launch_x3_one<1, 4>(a, nwg, lds, s) : launch_x3_one<1, 2>(a, nwg, lds, s); break;
+        case 9: p512 ? launch_x3_one<9, 4>(a, grid, lds, s) : launch_x3_one<9, 2>(a, grid, lds, s); break;
+        case 4: p512 ? launch_x3_one<4, 4>(a, grid, lds, s) : launch_x3_one<4, 2>(a, grid, lds, s); break;
+        default: p512 ? launch_x3_one<1, 4>(a, grid, lds, s) : launch_x3_one<1, 2>(a, grid, lds, s); break;
     }
     NPS_CHECK_LAUNCH("conv2d_fwd (split-fp16)");
     return 0;

@@ -57,15 +57,29 @@ def main():
           f"{ms:.3f} ms  {flops / ms / 1e9:.1f} TFLOP/s  ({flops / ms / 1e9 / 157.3 * 100:.1f}% of fp32 MFMA peak)")
     if a.check:
         import torch.nn.functional as F
-        xc = x[:1].permute(0, 3, 1, 2).cpu()
+        for bi in sorted({0, a.b // 2, a.b - 1}):
+            check_sample(a, x, gn, w, bias, out, bi)
+
+
+def check_sample(a, x, gn, w, bias, out, bi):
+    if True:
+        import torch.nn.functional as F
+        xc = x[bi:bi + 1].permute(0, 3, 1, 2).cpu()
         if a.gn:
             xc = F.gelu(F.group_norm(xc, 1, gn.gamma.cpu(), gn.beta.cpu(), 1e-5))
         if a.circ:
             xc = F.pad(xc, (a.circ,) * 4, mode="circular")
         ref = F.conv2d(xc, w.cpu(), bias.cpu(), stride=a.stride, dilation=a.dil)
-        y = out[:1].permute(0, 3, 1, 2).cpu()
+        y = out[bi:bi + 1].permute(0, 3, 1, 2).cpu()
         err = (torch.linalg.vector_norm(y.double() - ref.double()) / torch.linalg.vector_norm(ref.double())).item()
-        print(f"  rel-L2 vs torch CPU: {err:.2e}")
+        print(f"  sample {bi}: rel-L2 vs torch CPU: {err:.2e}")
+        if err > 1e-5 and os.environ.get("NPS_DIAG"):
+            d = (y.double() - ref.double()).abs()[0]  # (C, H, W)
+            bad = d > 1e-3 * ref.double().abs().max()
+            ch = bad.flatten(1).any(1).nonzero().flatten().tolist()
+            ys, xs = bad.any(0).nonzero(as_tuple=True)
+            print(f"    bad channels {ch[:8]}..{ch[-8:]} ({len(ch)}); bad px {bad.any(0).sum().item()} "
+                  f"rows {sorted(set(ys.tolist()))[:40]} cols {sorted(set(xs.tolist()))[:40]}")
 
 
 if __name__ == "__main__":
