@@ -106,7 +106,7 @@ def conv_roofline(model, x, cond, pos, sc):
 
 def _dtype():
     from nps_hip import ops
-    return "f32" if ops.CONV_PRECISION == ops.PREC_F32 else "f32 (2x2/3x3 convs: 3-pass split-fp16 MFMA)"
+    return "f32" if ops.CONV_PRECISION == ops.PREC_F32 else "f32 (1x1/2x2/3x3 convs: 3-pass split-fp16 MFMA)"
 
 
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
