@@ -115,6 +115,11 @@ int nps_conv2d_pack_weights_x3(const float* w, float* wpack, int Cout, int Cin, 
                                int transposed_phase, void* stream);
 /* 1 when a conv of this geometry runs on the split-fp16 kernel (stride-1, undilated 1x1 / 2x2 / 3x3). */
 int nps_conv2d_x3_eligible(int KH, int KW, int stride, int dil);
+/* 1 when the split-fp16 kernel applies a frame prologue itself (gn_groups > 0: GroupNorm affine with that
+ * many groups; pre_act 1: GELU) — the 3x3 kernel, with Cin / gn_groups a multiple of 4 — so the caller
+ * passes gn_* / pre_act to nps_conv2d_fwd instead of running nps_frame_pack first
+ * (replaces ResidualBlock's norm -> act -> conv, proc_unet_modern.py:62-99). */
+int nps_conv2d_x3_prologue_ok(int KH, int KW, int Cin, int gn_groups, int pre_act);
 /* 1 when the split-fp16 kernel can stage this virtual frame directly: every source boundary on a
  * multiple of 16 channels, every source's C a multiple of 4 (otherwise nps_frame_pack it first). */
 int nps_conv2d_x3_sources_ok(const nps_src_t* src, int nsrc);

@@ -516,8 +516,16 @@ bool pc_eligible(const nps_conv2d_t& a) {
            a.pre_act == 0;
 }
 
-// 3-pass split-fp16 kernel: every stride-1 undilated 1x1 / 2x2 / 3x3 conv without a prologue
-bool x3_eligible(const nps_conv2d_t& a) { return pc_eligible(a); }
+// 3-pass split-fp16 kernel: every stride-1 undilated 1x1 / 2x2 / 3x3 conv.  A frame prologue (GroupNorm
+// affine and/or GELU) is fused into the 3x3 kernel's producers when each 16-B channel quad lies in one
+// group; other prologue convs are fed by nps_frame_pack.
+bool x3_eligible(const nps_conv2d_t& a) {
+    const int nt = a.KH * a.KW;
+    const bool geo = a.stride == 1 && a.dil == 1 && a.KH == a.KW && (nt == 1 || nt == 4 || nt == 9);
+    if (a.gn_stats == nullptr && a.pre_act == 0) return geo;
+    return geo && nt == 9 && (a.pre_act == 0 || a.pre_act == 1) &&
+           (a.gn_stats == nullptr || (a.gn_groups > 0 && a.Cin % a.gn_groups == 0 && (a.Cin / a.gn_groups) % 4 == 0));
+}
 
 
 // producer/consumer variant per tap count: 1x1 convs use 192-channel x 128-pixel work-groups
@@ -582,6 +590,20 @@ extern "C" int nps_conv2d_x3_sources_ok(const nps_src_t* src, int nsrc) {
     t.nsrc = nsrc;
     for (int i = 0; i < nsrc && i < NPS_MAX_SRC; ++i) t.src[i] = src[i];
     return nsrc >= 1 && nsrc <= NPS_MAX_SRC && x3_sources_aligned(t) ? 1 : 0;
+}
+
+extern "C" int nps_conv2d_x3_prologue_ok(int KH, int KW, int Cin, int gn_groups, int pre_act) {
+    nps_conv2d_t t = {};
+    t.KH = KH;
+    t.KW = KW;
+    t.stride = 1;
+    t.dil = 1;
+    t.Cin = Cin;
+    static const double dummy[2] = {0.0, 0.0};
+    t.gn_stats = gn_groups > 0 ? dummy : nullptr;
+    t.gn_groups = gn_groups;
+    t.pre_act = pre_act;
+    return x3_eligible(t) ? 1 : 0;
 }
 
 extern "C" int nps_conv2d_x3_eligible(int KH, int KW, int stride, int dil) {

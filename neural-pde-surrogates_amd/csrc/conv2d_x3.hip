@@ -102,7 +102,9 @@ __device__ __forceinline__ void x3_store_phase(const nps_conv2d_t& a, int b, int
     }
 }
 
-template <int NTAPS, int PB>
+// PRO: the frame prologue (GroupNorm affine and/or GELU, proc_unet_modern.py:62-99) is applied by the
+// producers while staging, instead of a frame_pack pass in front of the conv.
+template <int NTAPS, int PB, bool PRO>
 __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
     constexpr int KWT = NTAPS == 9 ? 3 : (NTAPS == 4 ? 2 : 1);
     constexpr int CBW = 2;
@@ -142,7 +144,10 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
         const int ptid = tid - 256;
         const int Hext = a.Hin + 2 * a.circ, Wext = a.Win + 2 * a.circ;
         const float xs = in_scale_of(a);
-        f32x4 r0[MAXP], r1[MAXP];
+        // a register set: MAXP patch slots, then (PRO) the stage's GroupNorm operands gamma[4], beta[4]
+        // and the group's (sum, sum of squares) as two doubles, fetched with the patch
+        constexpr int NR = MAXP + (PRO ? 3 : 0);
+        f32x4 r0[NR], r1[NR];
         // Per-slot source addresses: the patch pixel of slot k is fixed for a tile, so its address in the
         // current source (and whether it lies inside it) is computed only when a stage's source (or the
         // tile) changes; a stage then costs one add + one load per slot.  Slot k holds channels
@@ -150,6 +155,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
         const int gq = ptid & 3;
         const float* sbase[MAXP];
         unsigned pixm = 0;  // slots whose pixel lies inside the current source
+        unsigned finm = 0;  // slots whose pixel lies inside the (circularly extended) frame
         int cur_src = -1;
         int fb = 0, fy0 = 0, fx0 = 0, fcob = 0;  // tile being fetched
         auto locate = [&](int sidx) {
@@ -162,6 +168,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
             const int sox = sidx == 0 ? S0.off_x : (sidx == 1 ? S1.off_x : S2.off_x);
             const int ybase = fy0 - a.pad_y, xbase = fx0 - a.pad_x;
             pixm = 0;
+            finm = 0;
 #pragma unroll
             for (int k = 0; k < MAXP; ++k) {
                 const int idx = ptid + k * 256;
@@ -169,6 +176,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
                 const int pr = p / g.PW, pc = p - pr * g.PW;
                 const int ye = ybase + pr, xe = xbase + pc;
                 bool ok = idx < NG && ye >= 0 && ye < Hext && xe >= 0 && xe < Wext;
+                finm = ok ? (finm | (1u << k)) : finm;
                 const int fy = a.circ ? nps::wrap_mod(ye - a.circ, a.Hin) : ye;
                 const int fx = a.circ ? nps::wrap_mod(xe - a.circ, a.Win) : xe;
                 const int yy = fy - soy, xx = fx - sox;
@@ -178,7 +186,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
             }
         };
         // issue() returns the mask of slots holding in-frame data; commit() zeroes the others
-        auto issue = [&](int st, f32x4 (&rp)[MAXP]) -> unsigned {
+        auto issue = [&](int st, f32x4 (&rp)[NR]) -> unsigned {
             const int c0 = st * CK;
             const int cend = min(c0 + CK, a.Cin);
             int sidx = 0, cbase = 0;
@@ -208,17 +216,62 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
 #pragma unroll
             for (int k = 0; k < MAXP; ++k)  // inline asm: invisible to the compiler's vmcnt tracking
                 asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(rp[k]) : "v"(sbase[k] + cs));
-            return pixm & chm;
+            if constexpr (PRO) {
+                // this lane's 4 frame channels share one group (host-checked: channels per group % 4 == 0);
+                // without GroupNorm (or past the channel tail) the loads read the packed weights instead
+                const int c = chok ? c0 + gq * 4 : 0;
+                const bool gn = a.gn_stats != nullptr;
+                const float* pg = gn ? a.gn_gamma + c : reinterpret_cast<const float*>(a.wpack);
+                const float* pb = gn ? a.gn_beta + c : reinterpret_cast<const float*>(a.wpack);
+                const double* ps = gn ? a.gn_stats + ((size_t)fb * a.gn_groups + c / (a.Cin / a.gn_groups)) * 2
+                                      : reinterpret_cast<const double*>(a.wpack);
+                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(rp[MAXP]) : "v"(pg));
+                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(rp[MAXP + 1]) : "v"(pb));
+                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(rp[MAXP + 2]) : "v"(ps));
+            }
+            // bits 0-15: slot data lies inside the source; bits 16-31: slot pixel lies inside the frame
+            return (pixm & chm) | ((finm & chm) << 16);
         };
-        auto commit = [&](int st, const f32x4 (&rp)[MAXP], unsigned okm) {
+        auto commit = [&](int st, const f32x4 (&rp)[NR], unsigned okm) {
             char* Pt = ring + (st % X3_NST) * stage_b;
+            float mean = 0.f, rstd = 0.f;
+            if constexpr (PRO) {
+                if (a.gn_stats != nullptr) {  // as frame_pack_kernel / the reference's GroupNorm
+                    const f32x4 sv = rp[MAXP + 2];
+                    double s1, s2;
+                    __builtin_memcpy(&s1, &sv, 8);
+                    __builtin_memcpy(&s2, reinterpret_cast<const char*>(&sv) + 8, 8);
+                    const double cnt = (double)(a.Cin / a.gn_groups) * a.Hin * a.Win;
+                    const double mu = s1 / cnt;
+                    double var = s2 / cnt - mu * mu;
+                    var = var < 0.0 ? 0.0 : var;
+                    mean = (float)mu;
+                    rstd = (float)(1.0 / sqrt(var + (double)a.gn_eps));
+                }
+            }
 #pragma unroll
             for (int k = 0; k < MAXP; ++k) {
                 const int idx = ptid + k * 256;
                 if (idx < NG) {
                     const f32x4 z = {0.f, 0.f, 0.f, 0.f};
                     f16x4 hi, lo;
-                    split4(((okm >> k) & 1u) ? rp[k] * xs : z, hi, lo);
+                    f32x4 v = ((okm >> k) & 1u) ? rp[k] : z;
+                    if constexpr (PRO) {
+                        if ((okm >> (16 + k)) & 1u) {
+                            if (a.gn_stats != nullptr) {
+#pragma unroll
+                                for (int e = 0; e < 4; ++e)
+                                    v[e] = (v[e] - mean) * rstd * rp[MAXP][e] + rp[MAXP + 1][e];
+                            }
+                            if (a.pre_act == 1) {
+#pragma unroll
+                                for (int e = 0; e < 4; ++e) v[e] = nps::gelu_erf(v[e]);
+                            }
+                        } else {
+                            v = z;  // the conv's own zero padding (and channels past Cin)
+                        }
+                    }
+                    split4(v * xs, hi, lo);
                     char* base = Pt + (idx >> 2) * X3_PIXB + (idx & 3) * 8;
                     *reinterpret_cast<f16x4*>(base) = hi;
                     *reinterpret_cast<f16x4*>(base + 32) = lo;
@@ -429,15 +482,15 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
     }
 }
 
-template <int NT, int PB>
+template <int NT, int PB, bool PRO = false>
 void launch_x3_one(const nps_conv2d_t& a, unsigned nwg, int lds, hipStream_t s) {
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)conv2d_x3_kernel<NT, PB>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void*)conv2d_x3_kernel<NT, PB, PRO>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   160 * 1024);
         attr_set = true;
     }
-    conv2d_x3_kernel<NT, PB><<<nwg, 512, lds, s>>>(a);
+    conv2d_x3_kernel<NT, PB, PRO><<<nwg, 512, lds, s>>>(a);
 }
 
 }  // namespace
@@ -468,8 +521,14 @@ int nps_launch_conv2d_x3(const nps_conv2d_t& a, int lds, hipStream_t s) {
     const bool lds_epi = !a.out_nchw && (a.out_C & 3) == 0 && (a.Cout & 3) == 0;  // == x3_lds_epilogue
     const unsigned grid = (unsigned)(lds_epi && per < nwg ? per : nwg);
     const bool p512 = a.TH * a.TW == 512;
+    const bool pro = a.gn_stats != nullptr || a.pre_act != 0;  // fused frame prologue: 3x3 only (host-checked)
     switch (a.KH * a.KW) {
-        case 9: p512 ? launch_x3_one<9, 4>(a, grid, lds, s) : launch_x3_one<9, 2>(a, grid, lds, s); break;
+        case 9:
+            if (pro)
+                p512 ? launch_x3_one<9, 4, true>(a, grid, lds, s) : launch_x3_one<9, 2, true>(a, grid, lds, s);
+            else
+                p512 ? launch_x3_one<9, 4>(a, grid, lds, s) : launch_x3_one<9, 2>(a, grid, lds, s);
+            break;
         case 4: p512 ? launch_x3_one<4, 4>(a, grid, lds, s) : launch_x3_one<4, 2>(a, grid, lds, s); break;
         default: p512 ? launch_x3_one<1, 4>(a, grid, lds, s) : launch_x3_one<1, 2>(a, grid, lds, s); break;
     }

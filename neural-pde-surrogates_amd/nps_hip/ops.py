@@ -18,6 +18,9 @@ GELU = 1
 # Conv arithmetic (include/nps.h NPS_PREC_*): exact fp32 MFMA, or the 3-pass split-fp16 MFMA products
 # (~2^-21 relative per product, 5.3x the fp32 MFMA rate) for the stride-1 undilated 1x1 / 2x2 / 3x3 convs.
 PREC_F32, PREC_X3F16 = 0, 1
+# split-fp16 3x3 convs apply their GroupNorm / GELU prologue while staging (nps_conv2d_x3_prologue_ok);
+# — off by default (NPS_FUSE_PROLOGUE=1): the erf-GELU makes the producers the bottleneck
+FUSE_PROLOGUE = os.environ.get("NPS_FUSE_PROLOGUE", "0") == "1"
 CONV_PRECISION = PREC_F32 if os.environ.get("NPS_CONV_PRECISION", "x3f16") == "f32" else PREC_X3F16
 
 
@@ -143,8 +146,11 @@ def conv2d(srcs: Sequence[Src], frame_hw, wpack: torch.Tensor, bias: Optional[to
     Cin = sum(s.t.shape[3] for s in srcs)
     cin_alg = Cin  # algorithmic input channels (before any zero channel padding)
     x3 = getattr(wpack, "nps_precision", PREC_F32) == PREC_X3F16
-    if ((gn is not None or pre_act) and stride == 1 and dil == 1 and KH == KW and KH in (1, 2, 3)) or (
-            x3 and not lib.nps_conv2d_x3_sources_ok(_c_src(srcs), len(srcs))):
+    aligned = not x3 or lib.nps_conv2d_x3_sources_ok(_c_src(srcs), len(srcs))
+    fused = (x3 and aligned and FUSE_PROLOGUE and (gn is not None or pre_act) and stride == 1 and dil == 1 and
+             lib.nps_conv2d_x3_prologue_ok(KH, KW, Cin, gn.groups if gn is not None else 0, pre_act))
+    if not fused and (((gn is not None or pre_act) and stride == 1 and dil == 1 and KH == KW and KH in (1, 2, 3))
+                      or not aligned):
         # the stride-1 producer/consumer convs stage raw bytes only (the split-fp16 one from 16-channel
         # aligned sources): materialise act(GN(frame)) / the concatenation once
         srcs = [Src(frame_pack(srcs, (Hin, Win), gn, pre_act, pad4=x3))]

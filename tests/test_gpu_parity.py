@@ -90,6 +90,38 @@ def test_residual_block_concat_crop_groupnorm():
     assert rel_l2(y, ref) < TOL
 
 
+@pytest.mark.parametrize("pm", ["circular", "zeros"])
+def test_residual_block_fused_prologue(monkeypatch, pm):
+    """The split-fp16 3x3 conv applying GroupNorm + GELU itself (NPS_FUSE_PROLOGUE=1): 16-channel aligned
+    concat with a padded crop (frame pixels no source covers get act(GN(0)), as frame_pack gives them)."""
+    from models.enc_proc_dec_components.proc_unet_modern import ResidualBlock
+    from nps_hip import ops
+    if ops.CONV_PRECISION != ops.PREC_X3F16:
+        pytest.skip("fused prologue is a split-fp16 kernel feature")
+    monkeypatch.setattr(ops, "FUSE_PROLOGUE", True)
+    packs = []
+    real_pack = ops.frame_pack
+    monkeypatch.setattr(ops, "frame_pack", lambda *a, **k: packs.append(k.get("gn")) or real_pack(*a, **k))
+    torch.manual_seed(1)
+    rb = ResidualBlock(32 + 16 + 4, 32, activation=_gelu(), norm=True, num_spatial_dims=2,
+                       padding_kwargs=dict(padding_mode=pm))
+    with torch.no_grad():
+        for n in (rb.norm1, rb.norm2):
+            n.weight.uniform_(0.5, 1.5)
+            n.bias.uniform_(-0.3, 0.3)
+    h = torch.randn(2, 32, 40, 36)
+    s = torch.randn(2, 16, 37, 33)   # crop_Nd pads 37x33 -> 40x36: uncovered frame rows / columns
+    v = torch.rand(2, 4, 40, 36)
+    x = torch.cat([h, Fo.crop_nd(s, h.shape), v], dim=1)
+    ref = Fo.residual_block({k: t.detach() for k, t in rb.state_dict().items()}, "", x, True, dict(padding_mode=pm))
+    rb = rb.to(DEV)
+    hd, sd_, vd = (ops.nchw_to_nhwc(t.to(DEV)) for t in (h, s, v))
+    srcs = [ops.Src(hd), ops.Src(sd_, ops.crop_offset(37, 40), ops.crop_offset(33, 36)), ops.Src(vd)]
+    y = ops.nhwc_to_nchw(rb.run(srcs, (40, 36))).cpu()
+    assert not any(g is not None for g in packs), "GroupNorm prologue went through frame_pack"
+    assert rel_l2(y, ref) < TOL
+
+
 # ------------------------------------------------------------------ spectral
 @pytest.mark.parametrize("name", ["spectral2d_a", "spectral2d_overlap", "spectral2d_nyq"])
 def test_spectral2d_golden(name):
