@@ -15,6 +15,7 @@ constexpr int KW_CHUNK = 16;   // W-bins per pass in the W-transforms
 constexpr int R_CHUNK = 8;     // retained rows per pass in dft_h
 constexpr int MAXR = 32;       // max retained rows in idft_h (m1 <= 16)
 constexpr int MAXB = 8;        // batch rows held in registers by the mixer per pass
+constexpr int WB = 16;         // pixels per batch of independent loads in the W-transforms
 
 // retained row r -> frequency k1 (proc_fno.py:266-269: rows [:m1] and [-m1:])
 __device__ __forceinline__ int row_k1(int r, int H, int R, int m1) { return r < m1 ? r : H - R + r; }
@@ -56,14 +57,22 @@ __global__ void dft_w_kernel(nps_conv2d_t a, int m2, float2* __restrict__ X1, fl
             float re[KW_CHUNK], im[KW_CHUNK];
 #pragma unroll
             for (int k = 0; k < KW_CHUNK; ++k) re[k] = im[k] = 0.f;
-            for (int w = 0; w < W; ++w) {
-                const float v = row[(size_t)w * sC];
+            // WB independent row loads are issued before their FMAs: one (b, h) row per work-group
+            // leaves too few waves per CU to cover HBM latency one load at a time
+            for (int w0 = 0; w0 < W; w0 += WB) {
+                float v[WB];
 #pragma unroll
-                for (int k = 0; k < KW_CHUNK; ++k) {
-                    if (k < nk) {
-                        const float2 t = tw[k * W + w];
-                        re[k] = fmaf(v, t.x, re[k]);
-                        im[k] = fmaf(-v, t.y, im[k]);
+                for (int j = 0; j < WB; ++j) v[j] = w0 + j < W ? row[(size_t)(w0 + j) * sC] : 0.f;
+#pragma unroll
+                for (int j = 0; j < WB; ++j) {
+                    const int w = w0 + j < W ? w0 + j : W - 1;  // past the row end v[j] = 0
+#pragma unroll
+                    for (int k = 0; k < KW_CHUNK; ++k) {
+                        if (k < nk) {
+                            const float2 t = tw[k * W + w];
+                            re[k] = fmaf(v[j], t.x, re[k]);
+                            im[k] = fmaf(-v[j], t.y, im[k]);
+                        }
                     }
                 }
             }
@@ -221,27 +230,38 @@ __global__ void idft_w_kernel(const float2* __restrict__ Z, float* __restrict__ 
                 zr[k] = z.x;
                 zi[k] = z.y;
             }
-            for (int w = 0; w < W; ++w) {
-                float v = 0.f;
+            // the read-modify-write stream of out / addend is batched WB pixels at a time (loads first)
+            const bool last_chunk = kb + KW_CHUNK >= m2;
+            const bool rd_out = kb > 0 || accumulate;
+            const bool rd_add = last_chunk && addend != nullptr;
+            for (int w0 = 0; w0 < W; w0 += WB) {
+                float prev[WB], add[WB];
 #pragma unroll
-                for (int k = 0; k < KW_CHUNK; ++k) {
-                    if (k < nk) {
-                        const float2 t = tw[(kb + k) * W + w];
-                        v = fmaf(zr[k], t.x, fmaf(-zi[k], t.y, v));
+                for (int j = 0; j < WB; ++j) {
+                    const size_t di = ((size_t)(b * H + h) * W + (w0 + j < W ? w0 + j : W - 1)) * Cout + o;
+                    prev[j] = rd_out ? out[di] : 0.f;
+                    add[j] = rd_add ? addend[di] : 0.f;
+                }
+#pragma unroll
+                for (int j = 0; j < WB; ++j) {
+                    const int w = w0 + j;
+                    if (w >= W) break;
+                    float v = 0.f;
+#pragma unroll
+                    for (int k = 0; k < KW_CHUNK; ++k) {
+                        if (k < nk) {
+                            const float2 t = tw[(kb + k) * W + w];
+                            v = fmaf(zr[k], t.x, fmaf(-zi[k], t.y, v));
+                        }
                     }
+                    // same float order as the unbatched form: v*scale (+ out) (+ addend), GELU
+                    v = kb == 0 ? (accumulate ? v * scale + prev[j] : v * scale) : prev[j] + v * scale;
+                    if (last_chunk) {
+                        if (addend) v += add[j];
+                        if (act == 1) v = nps::gelu_erf(v);
+                    }
+                    out[((size_t)(b * H + h) * W + w) * Cout + o] = v;
                 }
-                const size_t di = ((size_t)(b * H + h) * W + w) * Cout + o;
-                if (kb == 0) {
-                    v *= scale;
-                    if (accumulate) v += out[di];
-                } else {
-                    v = out[di] + v * scale;
-                }
-                if (kb + KW_CHUNK >= m2) {
-                    if (addend) v += addend[di];
-                    if (act == 1) v = nps::gelu_erf(v);
-                }
-                out[di] = v;
             }
         }
     }
