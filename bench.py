@@ -98,7 +98,8 @@ def conv_roofline(model, x, cond, pos, sc):
                for (p, t), (m, fl, c, _) in groups.items()}
     return dict(bound="mfma", achieved=round(achieved, 3), peak=round(peak, 1), unit="TFLOP/s",
                 frac=round(achieved / peak, 4), traffic=None,
-                kernel=KERNEL_NAMES.get(key, f"conv {key}"), arithmetic=key[0], launches=n,
+                kernel=KERNEL_NAMES.get(key, f"conv {key}"), arithmetic=key[0], kclass=f"{key[0]}_{key[1]}tap",
+                launches=n,
                 avg_launch_ms=round(ms / max(1, n), 4), flops_per_launch=flops / max(1, n),
                 algorithmic_bytes_per_launch=nbytes / max(1, n),
                 conv_ms_per_call=round(all_ms, 3), conv_classes=classes)
@@ -112,15 +113,18 @@ def _dtype():
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
 
-def attach_traffic(roof):
+def attach_traffic(roof, headline):
     """roofline.traffic: HBM bytes per launch of the dominant kernel from the committed rocprofv3 --pmc
-    passes (tools/pmc_traffic.sh; FETCH_SIZE doubled per MI355X_MICROARCH.md § HBM, + WRITE_SIZE)."""
+    passes (tools/pmc_traffic.sh; FETCH_SIZE doubled per MI355X_MICROARCH.md § HBM, + WRITE_SIZE).
+    Those passes profile the headline workload only; other workloads report traffic null."""
+    if not headline:
+        return roof
     try:
         with open(PMC_FILE) as f:
             pmc = json.load(f)
     except (OSError, ValueError):
         return roof
-    rec = pmc.get("classes", {}).get(f"{roof['arithmetic']}_{roof['kernel'].split('<')[1].split(',')[0]}tap")
+    rec = pmc.get("classes", {}).get(roof["kclass"])
     if rec:
         roof["traffic"] = rec["hbm_bytes_per_launch"]
         roof["traffic_source"] = f"{os.path.relpath(PMC_FILE, ROOT)} ({pmc.get('command', '')})"
@@ -231,11 +235,13 @@ def main():
     value = args.global_batch * tw * args.steps / elapsed
 
     if rank == 0:
-        roof = attach_traffic(conv_roofline(model, u_all[:, :, :tw], cond, pos, sc))
+        headline = (args.model, args.res, args.num_c, args.global_batch, args.fno_modes) == ("ufno", 256, 3, 16, None)
+        roof = attach_traffic(conv_roofline(model, u_all[:, :, :tw], cond, pos, sc), headline)
         cpu = cpu_baseline(model, ocfg, opde, args.res, args.num_c, calls=args.cpu_calls) if (
             args.cpu_calls > 0 and world == 1) else None
         line = {
-            "metric": "rollout timesteps/sec on 256x256 two-phase grid (sample-timesteps/s); rel-L2 vs CPU reference",
+            "metric": f"rollout timesteps/sec on {args.res}x{args.res} two-phase grid (sample-timesteps/s); "
+                      "rel-L2 vs CPU reference",
             "value": round(value, 3), "unit": "sample-timesteps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": _dtype(), "data": "synthetic",

@@ -11,7 +11,6 @@
 
 namespace {
 
-constexpr int KW_CHUNK = 16;   // W-bins per pass in the W-transforms
 constexpr int R_CHUNK = 8;     // retained rows per pass in dft_h
 constexpr int MAXR = 32;       // max retained rows in idft_h (m1 <= 16)
 constexpr int MAXB = 8;        // batch rows held in registers by the mixer per pass
@@ -31,14 +30,21 @@ __device__ __forceinline__ float2 twiddle(int k, int n, int N) {
 // X1[b][h][k2][c] = sum_w x[b][h][w][c] e^{-2 pi i k2 w / W}
 // With c2r_adj != 0 this is the adjoint of the c2r synthesis (backward of idft_w): every bin is scaled
 // by `scale` and, except DC / Nyquist, doubled (torch irfft backward: rfft(g)/N, columns 1..W-(W//2+1) x2).
+// KC bins per pass (a multiple of 4 >= the retained bins where possible): the twiddle table is laid out
+// [w][KC] so one pixel's KC twiddles are KC/2 broadcast ds_read_b128, and bins past m2 carry zero
+// twiddles (no per-bin branches in the inner loop).
+template <int KC>
 __global__ void dft_w_kernel(nps_conv2d_t a, int m2, float2* __restrict__ X1, float scale, int c2r_adj) {
-    extern __shared__ float2 tw[];  // [KW_CHUNK][W]
+    extern __shared__ __attribute__((aligned(16))) float2 tw[];  // [W][KC]
     const int h = blockIdx.x, b = blockIdx.y;
     const int W = a.Win, H = a.Hin, C = a.Cin;
-    for (int kb = 0; kb < m2; kb += KW_CHUNK) {
-        const int nk = min(KW_CHUNK, m2 - kb);
+    for (int kb = 0; kb < m2; kb += KC) {
+        const int nk = min(KC, m2 - kb);
         __syncthreads();
-        for (int i = threadIdx.x; i < nk * W; i += blockDim.x) tw[i] = twiddle(kb + i / W, i % W, W);
+        for (int i = threadIdx.x; i < KC * W; i += blockDim.x) {
+            const int w = i / KC, k = i - (i / KC) * KC;
+            tw[i] = k < nk ? twiddle(kb + k, w, W) : make_float2(0.f, 0.f);
+        }
         __syncthreads();
         for (int c = threadIdx.x; c < C; c += blockDim.x) {
             // locate the source of channel c
@@ -54,30 +60,33 @@ __global__ void dft_w_kernel(nps_conv2d_t a, int m2, float2* __restrict__ X1, fl
                 c0 += a.src[s].C;
             }
             const float* row = base + ((size_t)(b * H + h) * W) * sC + sc;
-            float re[KW_CHUNK], im[KW_CHUNK];
+            float re[KC], im[KC];
 #pragma unroll
-            for (int k = 0; k < KW_CHUNK; ++k) re[k] = im[k] = 0.f;
+            for (int k = 0; k < KC; ++k) re[k] = im[k] = 0.f;
             // WB independent row loads are issued before their FMAs: one (b, h) row per work-group
             // leaves too few waves per CU to cover HBM latency one load at a time
-            for (int w0 = 0; w0 < W; w0 += WB) {
+            auto bins = [&](float v, int w) {
+                const f32x4* t4 = reinterpret_cast<const f32x4*>(tw + w * KC);
+#pragma unroll
+                for (int q = 0; q < KC / 2; ++q) {
+                    const f32x4 t = t4[q];  // (cos, sin) of bins 2q, 2q + 1
+                    re[2 * q] = fmaf(v, t[0], re[2 * q]);
+                    im[2 * q] = fmaf(-v, t[1], im[2 * q]);
+                    re[2 * q + 1] = fmaf(v, t[2], re[2 * q + 1]);
+                    im[2 * q + 1] = fmaf(-v, t[3], im[2 * q + 1]);
+                }
+            };
+            int w0 = 0;
+            for (; w0 + WB <= W; w0 += WB) {
                 float v[WB];
 #pragma unroll
-                for (int j = 0; j < WB; ++j) v[j] = w0 + j < W ? row[(size_t)(w0 + j) * sC] : 0.f;
+                for (int j = 0; j < WB; ++j) v[j] = row[(size_t)(w0 + j) * sC];
 #pragma unroll
-                for (int j = 0; j < WB; ++j) {
-                    const int w = w0 + j < W ? w0 + j : W - 1;  // past the row end v[j] = 0
-#pragma unroll
-                    for (int k = 0; k < KW_CHUNK; ++k) {
-                        if (k < nk) {
-                            const float2 t = tw[k * W + w];
-                            re[k] = fmaf(v[j], t.x, re[k]);
-                            im[k] = fmaf(-v[j], t.y, im[k]);
-                        }
-                    }
-                }
+                for (int j = 0; j < WB; ++j) bins(v[j], w0 + j);
             }
+            for (; w0 < W; ++w0) bins(row[(size_t)w0 * sC], w0);
 #pragma unroll
-            for (int k = 0; k < KW_CHUNK; ++k) {
+            for (int k = 0; k < KC; ++k) {
                 if (k < nk) {
                     float f = scale;
                     const int kk = kb + k;
@@ -88,6 +97,9 @@ __global__ void dft_w_kernel(nps_conv2d_t a, int m2, float2* __restrict__ X1, fl
         }
     }
 }
+
+// bins per pass for m2 retained bins: the smallest multiple of 4 covering them (16 and chunked above)
+inline int kc_for(int m2) { return m2 <= 4 ? 4 : (m2 <= 8 ? 8 : (m2 <= 12 ? 12 : 16)); }
 
 // X2[b][r][k2][c] = sum_h X1[b][h][k2][c] e^{-2 pi i k1(r) h / H}
 __global__ void dft_h_kernel(const float2* __restrict__ X1, float2* __restrict__ X2, int H, int R, int m1, int m2,
@@ -203,20 +215,26 @@ __global__ void idft_h_kernel(const float2* __restrict__ Y, float2* __restrict__
 // out[b][h][w][o] (=|+=) act( sum_k c_k Re(Z[b][h][k][o] e^{2 pi i k w / W}) / (H W) [+ addend] )
 // doubling = 0, scale = 1 is the adjoint of the truncated real-input DFT (backward of dft_w):
 // gx[w] = sum_k Re(gX[k] e^{+2 pi i k w / W}).
+template <int KC>
 __global__ void idft_w_kernel(const float2* __restrict__ Z, float* __restrict__ out, int H, int W, int m2, int Cout,
                               int accumulate, const float* __restrict__ addend, int act, float scale_arg,
                               int doubling) {
-    extern __shared__ float2 tw[];  // [m2][W]
+    extern __shared__ __attribute__((aligned(16))) float2 tw[];  // [chunk][W][KC], zero past m2
     const int h = blockIdx.x, b = blockIdx.y;
-    for (int i = threadIdx.x; i < m2 * W; i += blockDim.x) tw[i] = twiddle(i / W, i % W, W);
+    const int nch = (m2 + KC - 1) / KC;
+    for (int i = threadIdx.x; i < nch * W * KC; i += blockDim.x) {
+        const int ch = i / (W * KC), r = i - ch * (W * KC);
+        const int w = r / KC, k = ch * KC + (r - (r / KC) * KC);
+        tw[i] = k < m2 ? twiddle(k, w, W) : make_float2(0.f, 0.f);
+    }
     __syncthreads();
     const float scale = scale_arg;
     for (int o = threadIdx.x; o < Cout; o += blockDim.x) {
-        float zr[KW_CHUNK], zi[KW_CHUNK];
-        for (int kb = 0; kb < m2; kb += KW_CHUNK) {
-            const int nk = min(KW_CHUNK, m2 - kb);
+        float zr[KC], zi[KC];
+        for (int kb = 0; kb < m2; kb += KC) {
+            const int nk = min(KC, m2 - kb);
 #pragma unroll
-            for (int k = 0; k < KW_CHUNK; ++k) {
+            for (int k = 0; k < KC; ++k) {
                 float2 z = make_float2(0.f, 0.f);
                 if (k < nk) {
                     const int kk = kb + k;
@@ -230,39 +248,51 @@ __global__ void idft_w_kernel(const float2* __restrict__ Z, float* __restrict__ 
                 zr[k] = z.x;
                 zi[k] = z.y;
             }
+            const float2* twc = tw + (size_t)(kb / KC) * W * KC;
             // the read-modify-write stream of out / addend is batched WB pixels at a time (loads first)
-            const bool last_chunk = kb + KW_CHUNK >= m2;
+            const bool last_chunk = kb + KC >= m2;
             const bool rd_out = kb > 0 || accumulate;
             const bool rd_add = last_chunk && addend != nullptr;
-            for (int w0 = 0; w0 < W; w0 += WB) {
+            const size_t rowo = (size_t)(b * H + h) * W;
+            auto pixel = [&](int w, float prev, float add) {
+                const f32x4* t4 = reinterpret_cast<const f32x4*>(twc + w * KC);
+                float v = 0.f;
+#pragma unroll
+                for (int q = 0; q < KC / 2; ++q) {
+                    const f32x4 t = t4[q];  // (cos, sin) of bins 2q, 2q + 1 (zero past m2)
+                    v = fmaf(zr[2 * q], t[0], fmaf(-zi[2 * q], t[1], v));
+                    v = fmaf(zr[2 * q + 1], t[2], fmaf(-zi[2 * q + 1], t[3], v));
+                }
+                // same float order as the unbatched form: v*scale (+ out) (+ addend), GELU
+                v = kb == 0 ? (accumulate ? v * scale + prev : v * scale) : prev + v * scale;
+                if (last_chunk) {
+                    if (addend) v += add;
+                    if (act == 1) v = nps::gelu_erf(v);
+                }
+                out[(rowo + w) * Cout + o] = v;
+            };
+            int w0 = 0;
+            for (; w0 + WB <= W; w0 += WB) {
                 float prev[WB], add[WB];
+                if (rd_out) {  // uniform branches around straight-line batches of loads
 #pragma unroll
-                for (int j = 0; j < WB; ++j) {
-                    const size_t di = ((size_t)(b * H + h) * W + (w0 + j < W ? w0 + j : W - 1)) * Cout + o;
-                    prev[j] = rd_out ? out[di] : 0.f;
-                    add[j] = rd_add ? addend[di] : 0.f;
+                    for (int j = 0; j < WB; ++j) prev[j] = out[(rowo + w0 + j) * Cout + o];
+                } else {
+#pragma unroll
+                    for (int j = 0; j < WB; ++j) prev[j] = 0.f;
+                }
+                if (rd_add) {
+#pragma unroll
+                    for (int j = 0; j < WB; ++j) add[j] = addend[(rowo + w0 + j) * Cout + o];
+                } else {
+#pragma unroll
+                    for (int j = 0; j < WB; ++j) add[j] = 0.f;
                 }
 #pragma unroll
-                for (int j = 0; j < WB; ++j) {
-                    const int w = w0 + j;
-                    if (w >= W) break;
-                    float v = 0.f;
-#pragma unroll
-                    for (int k = 0; k < KW_CHUNK; ++k) {
-                        if (k < nk) {
-                            const float2 t = tw[(kb + k) * W + w];
-                            v = fmaf(zr[k], t.x, fmaf(-zi[k], t.y, v));
-                        }
-                    }
-                    // same float order as the unbatched form: v*scale (+ out) (+ addend), GELU
-                    v = kb == 0 ? (accumulate ? v * scale + prev[j] : v * scale) : prev[j] + v * scale;
-                    if (last_chunk) {
-                        if (addend) v += add[j];
-                        if (act == 1) v = nps::gelu_erf(v);
-                    }
-                    out[((size_t)(b * H + h) * W + w) * Cout + o] = v;
-                }
+                for (int j = 0; j < WB; ++j) pixel(w0 + j, prev[j], add[j]);
             }
+            for (; w0 < W; ++w0)
+                pixel(w0, rd_out ? out[(rowo + w0) * Cout + o] : 0.f, rd_add ? addend[(rowo + w0) * Cout + o] : 0.f);
         }
     }
 }
@@ -347,6 +377,44 @@ __global__ void spec_unpack_grad_kernel(const float2* __restrict__ gwp, float2* 
     gw2[idx] = gwp[(((size_t)row_of(k1b) * m2 + k2) * Cin + ci) * Cout + o];
 }
 
+
+size_t dft_w_lds(int m2, int W) { return sizeof(float2) * kc_for(m2) * W; }
+size_t idft_w_lds(int m2, int W) {
+    const int kc = kc_for(m2);
+    return sizeof(float2) * ((m2 + kc - 1) / kc) * kc * W;
+}
+
+void launch_dft_w(dim3 grid, int bs, size_t lds, hipStream_t s, const nps_conv2d_t& a, int m2, float2* X1, float scale,
+                  int c2r_adj) {
+    switch (kc_for(m2)) {
+        case 4: dft_w_kernel<4><<<grid, bs, lds, s>>>(a, m2, X1, scale, c2r_adj); break;
+        case 8: dft_w_kernel<8><<<grid, bs, lds, s>>>(a, m2, X1, scale, c2r_adj); break;
+        case 12: dft_w_kernel<12><<<grid, bs, lds, s>>>(a, m2, X1, scale, c2r_adj); break;
+        default: dft_w_kernel<16><<<grid, bs, lds, s>>>(a, m2, X1, scale, c2r_adj); break;
+    }
+}
+
+template <int KC>
+void launch_idft_w_kc(dim3 grid, int bs, size_t lds, hipStream_t s, const float2* Z, float* out, int H, int W, int m2,
+                      int C, int accumulate, const float* addend, int act, float scale, int doubling) {
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)idft_w_kernel<KC>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+        attr_set = true;
+    }
+    idft_w_kernel<KC><<<grid, bs, lds, s>>>(Z, out, H, W, m2, C, accumulate, addend, act, scale, doubling);
+}
+
+void launch_idft_w(dim3 grid, int bs, size_t lds, hipStream_t s, const float2* Z, float* out, int H, int W, int m2,
+                   int C, int accumulate, const float* addend, int act, float scale, int doubling) {
+    switch (kc_for(m2)) {
+        case 4: launch_idft_w_kc<4>(grid, bs, lds, s, Z, out, H, W, m2, C, accumulate, addend, act, scale, doubling); break;
+        case 8: launch_idft_w_kc<8>(grid, bs, lds, s, Z, out, H, W, m2, C, accumulate, addend, act, scale, doubling); break;
+        case 12: launch_idft_w_kc<12>(grid, bs, lds, s, Z, out, H, W, m2, C, accumulate, addend, act, scale, doubling); break;
+        default: launch_idft_w_kc<16>(grid, bs, lds, s, Z, out, H, W, m2, C, accumulate, addend, act, scale, doubling); break;
+    }
+}
+
 }  // namespace
 
 extern "C" int nps_spectral_dft_w(const nps_src_t* src, int nsrc, int B, int H, int W, int C, int m2, float* X1,
@@ -367,10 +435,10 @@ extern "C" int nps_spectral_dft_w(const nps_src_t* src, int nsrc, int B, int H, 
     a.Hin = H;
     a.Win = W;
     a.Cin = C;
-    const size_t lds = sizeof(float2) * KW_CHUNK * W;
+    const size_t lds = dft_w_lds(m2, W);
     NPS_CHECK_ARG(lds <= 64 * 1024, "spectral_dft_w: W=%d too large", W);
     const int bs = C >= 256 ? 256 : ((C + 63) / 64) * 64;
-    dft_w_kernel<<<dim3(H, B), bs, lds, (hipStream_t)stream>>>(a, m2, reinterpret_cast<float2*>(X1), 1.f, 0);
+    launch_dft_w(dim3(H, B), bs, lds, (hipStream_t)stream, a, m2, reinterpret_cast<float2*>(X1), 1.f, 0);
     NPS_CHECK_LAUNCH("spectral_dft_w");
     return 0;
 }
@@ -424,7 +492,6 @@ extern "C" int nps_spectral_idft_h(const float* Y, float* Z, int B, int H, int m
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void*)idft_h_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
-        (void)hipFuncSetAttribute((const void*)idft_w_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
         attr_set = true;
     }
     idft_h_kernel<<<grid, 256, lds, (hipStream_t)stream>>>(reinterpret_cast<const float2*>(Y),
@@ -437,17 +504,11 @@ extern "C" int nps_spectral_idft_w(const float* Z, float* out, int B, int H, int
                                    const float* addend, int act, void* stream) {
     NPS_CHECK_ARG(Z && out && B > 0 && H > 0 && W > 0 && m2 > 0 && m2 <= W / 2 + 1 && Cout > 0,
                   "spectral_idft_w: bad args");
-    const size_t lds = sizeof(float2) * m2 * W;
+    const size_t lds = idft_w_lds(m2, W);
     NPS_CHECK_ARG(lds <= 96 * 1024, "spectral_idft_w: m2*W too large");
     const int bs = Cout >= 256 ? 256 : ((Cout + 63) / 64) * 64;
-    static bool attr_set = false;
-    if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)idft_w_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
-        attr_set = true;
-    }
-    idft_w_kernel<<<dim3(H, B), bs, lds, (hipStream_t)stream>>>(reinterpret_cast<const float2*>(Z), out, H, W, m2,
-                                                                Cout, accumulate, addend, act,
-                                                                1.0f / ((float)H * (float)W), 1);
+    launch_idft_w(dim3(H, B), bs, lds, (hipStream_t)stream, reinterpret_cast<const float2*>(Z), out, H, W, m2, Cout,
+                  accumulate, addend, act, 1.0f / ((float)H * (float)W), 1);
     NPS_CHECK_LAUNCH("spectral_idft_w");
     return 0;
 }
@@ -466,11 +527,11 @@ extern "C" int nps_spectral_idft_w_bwd(const float* gy, float* gZ, int B, int H,
     a.Hin = H;
     a.Win = W;
     a.Cin = Cout;
-    const size_t lds = sizeof(float2) * KW_CHUNK * W;
+    const size_t lds = dft_w_lds(m2, W);
     NPS_CHECK_ARG(lds <= 64 * 1024, "spectral_idft_w_bwd: W=%d too large", W);
     const int bs = Cout >= 256 ? 256 : ((Cout + 63) / 64) * 64;
-    dft_w_kernel<<<dim3(H, B), bs, lds, (hipStream_t)stream>>>(a, m2, reinterpret_cast<float2*>(gZ),
-                                                               1.0f / ((float)H * (float)W), 1);
+    launch_dft_w(dim3(H, B), bs, lds, (hipStream_t)stream, a, m2, reinterpret_cast<float2*>(gZ),
+                 1.0f / ((float)H * (float)W), 1);
     NPS_CHECK_LAUNCH("spectral_idft_w_bwd");
     return 0;
 }
@@ -479,16 +540,11 @@ extern "C" int nps_spectral_dft_w_bwd(const float* gX1, float* gx, int B, int H,
                                       void* stream) {
     NPS_CHECK_ARG(gX1 && gx && B > 0 && H > 0 && W > 0 && m2 > 0 && m2 <= W / 2 + 1 && Cin > 0,
                   "spectral_dft_w_bwd: bad args");
-    const size_t lds = sizeof(float2) * m2 * W;
+    const size_t lds = idft_w_lds(m2, W);
     NPS_CHECK_ARG(lds <= 96 * 1024, "spectral_dft_w_bwd: m2*W too large");
     const int bs = Cin >= 256 ? 256 : ((Cin + 63) / 64) * 64;
-    static bool attr_set = false;
-    if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)idft_w_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
-        attr_set = true;
-    }
-    idft_w_kernel<<<dim3(H, B), bs, lds, (hipStream_t)stream>>>(reinterpret_cast<const float2*>(gX1), gx, H, W, m2,
-                                                                Cin, 0, nullptr, 0, 1.0f, 0);
+    launch_idft_w(dim3(H, B), bs, lds, (hipStream_t)stream, reinterpret_cast<const float2*>(gX1), gx, H, W, m2, Cin, 0,
+                  nullptr, 0, 1.0f, 0);
     NPS_CHECK_LAUNCH("spectral_dft_w_bwd");
     return 0;
 }
