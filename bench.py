@@ -70,6 +70,7 @@ PEAK_TFLOPS = {"f32": FP32_MFMA_PEAK_TFLOPS, "x3f16": 2500.0 / 3.0}
 KERNEL_NAMES = {("x3f16", 9): "conv2d_x3_kernel<9,*> (3x3, split-fp16 MFMA)",
                 ("x3f16", 4): "conv2d_x3_kernel<4,*> (2x2 phase / space-to-depth, split-fp16 MFMA)",
                 ("x3f16", 1): "conv2d_x3_kernel<1,*> (1x1, split-fp16 MFMA)",
+                ("x3f16", 25): "conv2d_x3_kernel<25,2> (5x5 dilated on the lattice, split-fp16 MFMA)",
                 ("f32", 1): "conv2d_pc_kernel<1,32,2,3,2> (1x1, f32 MFMA)"}
 
 
@@ -107,7 +108,7 @@ def conv_roofline(model, x, cond, pos, sc):
 
 def _dtype():
     from nps_hip import ops
-    return "f32" if ops.CONV_PRECISION == ops.PREC_F32 else "f32 (1x1/2x2/3x3 convs: 3-pass split-fp16 MFMA)"
+    return "f32" if ops.CONV_PRECISION == ops.PREC_F32 else "f32 (1x1/2x2/3x3/5x5 convs: 3-pass split-fp16 MFMA)"
 
 
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")

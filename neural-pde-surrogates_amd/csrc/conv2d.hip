@@ -516,12 +516,14 @@ bool pc_eligible(const nps_conv2d_t& a) {
            a.pre_act == 0;
 }
 
-// 3-pass split-fp16 kernel: every stride-1 undilated 1x1 / 2x2 / 3x3 conv.  A frame prologue (GroupNorm
-// affine and/or GELU) is fused into the 3x3 kernel's producers when each 16-B channel quad lies in one
-// group; other prologue convs are fed by nps_frame_pack.
+// 3-pass split-fp16 kernel: every stride-1 undilated 1x1 / 2x2 / 3x3 conv and the (dilated) 5x5 convs of
+// the dilated ResNet.  A frame prologue (GroupNorm affine and/or GELU) is fused into the 3x3 kernel's
+// producers when each 16-B channel quad lies in one group; other prologue convs are fed by nps_frame_pack.
 bool x3_eligible(const nps_conv2d_t& a) {
     const int nt = a.KH * a.KW;
-    const bool geo = a.stride == 1 && a.dil == 1 && a.KH == a.KW && (nt == 1 || nt == 4 || nt == 9);
+    // 1x1 / 2x2 / 3x3 undilated; 5x5 at any dilation (DRN, proc_dilatedresnet.py: tiled on the lattice)
+    const bool geo = a.stride == 1 && a.KH == a.KW &&
+                     ((a.dil == 1 && (nt == 1 || nt == 4 || nt == 9)) || (nt == 25 && a.dil >= 1));
     if (a.gn_stats == nullptr && a.pre_act == 0) return geo;
     return geo && nt == 9 && (a.pre_act == 0 || a.pre_act == 1) &&
            (a.gn_stats == nullptr || (a.gn_groups > 0 && a.Cin % a.gn_groups == 0 && (a.Cin / a.gn_groups) % 4 == 0));

@@ -27,8 +27,10 @@ namespace {
 //     (the 3 co-blocks of a tile and neighbouring tiles read the same patch bytes from one L2).
 __host__ __device__ constexpr int x3_patch_px_max(int ntaps, int tile_px) {
     // largest (TH + k - 1) * (TW + k - 1) over the tile shapes nps_conv2d_plan uses for tile_px
-    return ntaps == 1 ? tile_px
-                      : (tile_px == 512 ? (ntaps == 4 ? 9 * 65 : 10 * 66) : (ntaps == 4 ? 9 * 33 : 10 * 34));
+    // (25 taps: 5x5, 256-pixel tiles only — a 512-pixel 5x5 patch ring does not fit LDS)
+    return ntaps == 1    ? tile_px
+           : ntaps == 25 ? (tile_px == 512 ? 12 * 68 : 12 * 36)
+                         : (tile_px == 512 ? (ntaps == 4 ? 9 * 65 : 10 * 66) : (ntaps == 4 ? 9 * 33 : 10 * 34));
 }
 
 #define X3_MFMA __builtin_amdgcn_mfma_f32_32x32x16_f16
@@ -70,14 +72,14 @@ __device__ __forceinline__ bool x3_lds_epilogue(const nps_conv2d_t& a) {
 // 16 consecutive threads cover one pixel's 64 channels (256 contiguous bytes of the NHWC output), with
 // the fused bias / addends / GELU / accumulate of store_tile, in the same float order.
 template <int TILE_PX>
-__device__ __forceinline__ void x3_store_phase(const nps_conv2d_t& a, int b, int cob, int oy0, int ox0,
+__device__ __forceinline__ void x3_store_phase(const nps_conv2d_t& a, int b, int cob, int oy0, int ox0, int lat,
                                                const float* T, int tid) {
 #pragma unroll 4
     for (int i = tid; i < TILE_PX * 16; i += 512) {
         const int P = i >> 4, q = i & 15;
         const int co0 = cob * 64 + q * 4;
         const int ti = P / a.TW, tj = P - (P / a.TW) * a.TW;
-        const int oy = oy0 + ti, ox = ox0 + tj;
+        const int oy = oy0 + ti * lat, ox = ox0 + tj * lat;  // lat: dilation-lattice step (1 unless dilated)
         const int dy = oy * a.out_os + a.out_off_y, dx = ox * a.out_os + a.out_off_x;
         if (co0 >= a.Cout || oy >= a.Hout || ox >= a.Wout || dy < 0 || dy >= a.out_H || dx < 0 || dx >= a.out_W)
             continue;
@@ -106,7 +108,7 @@ __device__ __forceinline__ void x3_store_phase(const nps_conv2d_t& a, int b, int
 // producers while staging, instead of a frame_pack pass in front of the conv.
 template <int NTAPS, int PB, bool PRO>
 __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
-    constexpr int KWT = NTAPS == 9 ? 3 : (NTAPS == 4 ? 2 : 1);
+    constexpr int KWT = NTAPS == 25 ? 5 : (NTAPS == 9 ? 3 : (NTAPS == 4 ? 2 : 1));
     constexpr int CBW = 2;
     constexpr int TILE_PX = 4 * PB * 32;
     constexpr int MAXP = (x3_patch_px_max(NTAPS, TILE_PX) * 4 + 255) / 256;
@@ -127,8 +129,10 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
         const int tile = rest % ntiles;
         b = rest / ntiles;
         const int ty = tile / g.tiles_x, tx = tile - (tile / g.tiles_x) * g.tiles_x;
-        oy0 = ty * a.TH;
-        ox0 = tx * a.TW;
+        // dilated convs tile on the dilation lattice (g.T = dil): tile (ty, tx) is lattice phase
+        // (ty % T, tx % T), block (ty / T, tx / T); its pixels are oy0 + ti * T, ox0 + tj * T
+        oy0 = (ty % g.T) + (ty / g.T) * a.TH * g.T;
+        ox0 = (tx % g.T) + (tx / g.T) * a.TW * g.T;
     };
     const int npix = g.PH * g.PW;
     const int NG = npix * 4;                              // float4 slots of a 16-channel patch stage
@@ -174,7 +178,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
                 const int idx = ptid + k * 256;
                 const int p = idx >> 2;
                 const int pr = p / g.PW, pc = p - pr * g.PW;
-                const int ye = ybase + pr, xe = xbase + pc;
+                const int ye = ybase + pr * g.rstep, xe = xbase + pc * g.rstep;
                 bool ok = idx < NG && ye >= 0 && ye < Hext && xe >= 0 && xe < Wext;
                 finm = ok ? (finm | (1u << k)) : finm;
                 const int fy = a.circ ? nps::wrap_mod(ye - a.circ, a.Hin) : ye;
@@ -315,7 +319,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
                 m1 = issue(min(1, last), r1);
             }
             barrier();  // the consumers' tile is in LDS
-            if (lds_epi) x3_store_phase<TILE_PX>(a, sb, scob, soy0, sox0, reinterpret_cast<const float*>(ring), tid);
+            if (lds_epi) x3_store_phase<TILE_PX>(a, sb, scob, soy0, sox0, g.T, reinterpret_cast<const float*>(ring), tid);
             barrier();  // every read of the staged tile is done: the ring may be refilled
             if (!more) break;
             // land the next tile's fetches before the loop latch: r0 / r1 are loop-carried, and the
@@ -455,13 +459,13 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
                     }
             }
             barrier();
-            x3_store_phase<TILE_PX>(a, b, cob, oy0, ox0, T, tid);
+            x3_store_phase<TILE_PX>(a, b, cob, oy0, ox0, g.T, T, tid);
         } else {
             static_for<PB>([&](auto pbc) {  // compile-time pb: acc stays in registers
                 constexpr int pb = decltype(pbc)::value;
                 const int P = wave * 32 * PB + pb * 32 + (lane & 31);
                 const int ti = P / a.TW, tj = P - (P / a.TW) * a.TW;
-                const int oy = oy0 + ti, ox = ox0 + tj;
+                const int oy = oy0 + ti * g.T, ox = ox0 + tj * g.T;
                 if (oy >= a.Hout || ox >= a.Wout) return;
                 const int dy = oy * a.out_os + a.out_off_y, dx = ox * a.out_os + a.out_off_x;
                 if (dy < 0 || dy >= a.out_H || dx < 0 || dx >= a.out_W) return;
@@ -528,6 +532,10 @@ int nps_launch_conv2d_x3(const nps_conv2d_t& a, int lds, hipStream_t s) {
                 p512 ? launch_x3_one<9, 4, true>(a, grid, lds, s) : launch_x3_one<9, 2, true>(a, grid, lds, s);
             else
                 p512 ? launch_x3_one<9, 4>(a, grid, lds, s) : launch_x3_one<9, 2>(a, grid, lds, s);
+            break;
+        case 25:  // 5x5 (DRN, dilated on the lattice): 256-pixel tiles only (host-checked by the LDS budget)
+            NPS_CHECK_ARG(!p512, "conv2d_fwd (split-fp16): 5x5 needs a 256-pixel tile");
+            launch_x3_one<25, 2>(a, grid, lds, s);
             break;
         case 4: p512 ? launch_x3_one<4, 4>(a, grid, lds, s) : launch_x3_one<4, 2>(a, grid, lds, s); break;
         default: p512 ? launch_x3_one<1, 4>(a, grid, lds, s) : launch_x3_one<1, 2>(a, grid, lds, s); break;
