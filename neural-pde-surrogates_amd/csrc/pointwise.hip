@@ -110,10 +110,12 @@ __global__ void timeconv_kernel(const float* __restrict__ pre, const float* __re
 }
 
 
-// Specialised TimeConvDense for a compile-time (num_c, tw): the block's 64 pixels of the planar
+// Specialised TimeConvDense for a compile-time (num_c, tw): the block's PX pixels of the planar
 // pre-decoder output are staged in LDS once (coalesced), both conv1d layers run from LDS with fully
-// unrolled taps and the weights read as wave-uniform (scalar-cache) loads.
-template <int NC, int TW>
+// unrolled taps and the weights read as wave-uniform (scalar-cache) loads.  PX sets the LDS per block
+// (4 * PX * NC * (3 TW + 2 L1) bytes): 64 pixels at NC = 3 is 107 KB, one block (4 waves) per CU;
+// 16 pixels lets 5 blocks share a CU.
+template <int NC, int TW, int PX>
 __global__ __launch_bounds__(256) void timeconv_fast_kernel(const float* __restrict__ pre, const float* __restrict__ u,
                                                             const float* __restrict__ w1, const float* __restrict__ b1,
                                                             const float* __restrict__ w2, const float* __restrict__ b2,
@@ -127,23 +129,25 @@ __global__ __launch_bounds__(256) void timeconv_fast_kernel(const float* __restr
     constexpr int C2 = 2 * NC;
     static_assert(L1 - KB + 1 == TW, "TimeConvDense kernel sizes");
     extern __shared__ float lds[];
-    float* xs = lds;                 // [NC*L][64]
-    float* d1 = lds + NC * L * 64;   // [C2][L1][64]
+    constexpr int NSLOT = 256 / PX;
+    constexpr int PP = PX + 1;       // row pitch: the NSLOT / 4 slots of a wave read rows 16 apart
+    float* xs = lds;                 // [NC*L][PP]
+    float* d1 = lds + NC * L * PP;   // [C2][L1][PP]
     const int b = blockIdx.y;
-    const int p = threadIdx.x & 63, slot = threadIdx.x >> 6;
-    const int p0 = blockIdx.x * 64;
-    const int np = min(64, HW - p0);
+    const int p = threadIdx.x % PX, slot = threadIdx.x / PX;
+    const int p0 = blockIdx.x * PX;
+    const int np = min(PX, HW - p0);
     const float* src = pre + (size_t)b * NC * L * HW + p0;
-    for (int i = threadIdx.x; i < NC * L * 64; i += 256) {
-        const int r = i >> 6, q = i & 63;
-        xs[i] = q < np ? src[(size_t)r * HW + q] : 0.f;
+    for (int i = threadIdx.x; i < NC * L * PX; i += 256) {
+        const int r = i / PX, q = i % PX;
+        xs[r * PP + q] = q < np ? src[(size_t)r * HW + q] : 0.f;
     }
     __syncthreads();
     // conv1 (stride 2) + GELU: each work item = one output channel x R1 consecutive positions, the
     // input window held in registers (R1*KA FMAs per 2*R1+KA-2 LDS reads)
     constexpr int R1 = 8;
     static_assert(L1 % R1 == 0, "conv1 run length");
-    for (int j = slot; j < C2 * (L1 / R1); j += 4) {
+    for (int j = slot; j < C2 * (L1 / R1); j += NSLOT) {
         const int o = j / (L1 / R1), t0 = (j - o * (L1 / R1)) * R1;
         float acc[R1];
 #pragma unroll
@@ -151,9 +155,9 @@ __global__ __launch_bounds__(256) void timeconv_fast_kernel(const float* __restr
 #pragma unroll
         for (int ci = 0; ci < NC; ++ci) {
             float xw[2 * (R1 - 1) + KA];
-            const float* xr = xs + (ci * L + 2 * t0) * 64 + p;
+            const float* xr = xs + (ci * L + 2 * t0) * PP + p;
 #pragma unroll
-            for (int k = 0; k < 2 * (R1 - 1) + KA; ++k) xw[k] = xr[k * 64];
+            for (int k = 0; k < 2 * (R1 - 1) + KA; ++k) xw[k] = xr[k * PP];
             const float* wr = w1 + (o * NC + ci) * KA;
 #pragma unroll
             for (int k = 0; k < KA; ++k) {
@@ -163,7 +167,7 @@ __global__ __launch_bounds__(256) void timeconv_fast_kernel(const float* __restr
             }
         }
 #pragma unroll
-        for (int r = 0; r < R1; ++r) d1[(o * L1 + t0 + r) * 64 + p] = nps::gelu_erf(acc[r]);
+        for (int r = 0; r < R1; ++r) d1[(o * L1 + t0 + r) * PP + p] = nps::gelu_erf(acc[r]);
     }
     __syncthreads();
     if (p >= np) return;
@@ -171,7 +175,7 @@ __global__ __launch_bounds__(256) void timeconv_fast_kernel(const float* __restr
     const float m = mask ? mask[((size_t)b * mask_S + mask_ch) * HW + pix] : 0.f;
     constexpr int R2 = 5;
     static_assert(TW % R2 == 0, "conv2 run length");
-    for (int j = slot; j < NC * (TW / R2); j += 4) {
+    for (int j = slot; j < NC * (TW / R2); j += NSLOT) {
         const int o2 = j / (TW / R2), t0 = (j - o2 * (TW / R2)) * R2;
         float acc[R2];
 #pragma unroll
@@ -179,9 +183,9 @@ __global__ __launch_bounds__(256) void timeconv_fast_kernel(const float* __restr
 #pragma unroll
         for (int o = 0; o < C2; ++o) {
             float dw[R2 - 1 + KB];
-            const float* dr = d1 + (o * L1 + t0) * 64 + p;
+            const float* dr = d1 + (o * L1 + t0) * PP + p;
 #pragma unroll
-            for (int k = 0; k < R2 - 1 + KB; ++k) dw[k] = dr[k * 64];
+            for (int k = 0; k < R2 - 1 + KB; ++k) dw[k] = dr[k * PP];
             const float* wr = w2 + (o2 * C2 + o) * KB;
 #pragma unroll
             for (int k = 0; k < KB; ++k) {
@@ -457,25 +461,26 @@ extern "C" int nps_timeconv_decode(const float* pre, const float* u, const float
         attr_set = true;
     }
     if (tw == 25 && (num_c == 1 || num_c == 3)) {
-        const size_t lds2 = sizeof(float) * 64 * num_c * (3 * 25 + 2 * L1);
+        constexpr int PX = 16;
+        const size_t lds2 = sizeof(float) * (PX + 1) * num_c * (3 * 25 + 2 * L1);
         hipStream_t st = (hipStream_t)stream;
         if (num_c == 1) {
             static bool set1 = false;
             if (!set1) {
-                (void)hipFuncSetAttribute((const void*)timeconv_fast_kernel<1, 25>,
+                (void)hipFuncSetAttribute((const void*)timeconv_fast_kernel<1, 25, PX>,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
                 set1 = true;
             }
-            timeconv_fast_kernel<1, 25><<<dim3((HW + 63) / 64, B), 256, lds2, st>>>(
+            timeconv_fast_kernel<1, 25, PX><<<dim3((HW + PX - 1) / PX, B), 256, lds2, st>>>(
                 pre, u, w1, b1, w2, b2, dtcum, mask, mask_S, mask_ch, out, HW, act_tanh);
         } else {
             static bool set3 = false;
             if (!set3) {
-                (void)hipFuncSetAttribute((const void*)timeconv_fast_kernel<3, 25>,
+                (void)hipFuncSetAttribute((const void*)timeconv_fast_kernel<3, 25, PX>,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
                 set3 = true;
             }
-            timeconv_fast_kernel<3, 25><<<dim3((HW + 63) / 64, B), 256, lds2, st>>>(
+            timeconv_fast_kernel<3, 25, PX><<<dim3((HW + PX - 1) / PX, B), 256, lds2, st>>>(
                 pre, u, w1, b1, w2, b2, dtcum, mask, mask_S, mask_ch, out, HW, act_tanh);
         }
         NPS_CHECK_LAUNCH("timeconv_decode");
