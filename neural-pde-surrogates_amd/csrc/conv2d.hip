@@ -497,8 +497,12 @@ __global__ void pack_weights_x3_kernel(const float* __restrict__ w, _Float16* __
     const int cb = r % ncb; r /= ncb;
     const int tap = r % ntaps; r /= ntaps;
     const int chunk = (int)r;
-    const float v = pow2_scale_for(*wmax) *
-                    weight_elem(w, Cout, Cin, KH, KW, tphase, cb * 32 + (lane & 31), chunk * CK + (lane >> 5) * 8 + j, tap);
+    // 1x1: chunk pair (2s, 2s + 1) covers channels [32s, 32s + 32) with lane half h holding the contiguous
+    // run [32s + 16h, 32s + 16h + 16): chunk 2s its first 8, chunk 2s + 1 its last 8 (conv1x1_x3_kernel
+    // fetches 64 contiguous bytes per lane); other tap counts: chunk c = channels [16c, 16c + 16)
+    const int ci = ntaps == 1 && tphase == -1 ? (chunk >> 1) * 32 + (lane >> 5) * 16 + (chunk & 1) * 8 + j
+                                              : chunk * CK + (lane >> 5) * 8 + j;
+    const float v = pow2_scale_for(*wmax) * weight_elem(w, Cout, Cin, KH, KW, tphase, cb * 32 + (lane & 31), ci, tap);
     const size_t frag = i >> 9;  // (chunk, tap, cb) fragment of 64 lanes x 8
     const size_t o = frag * 1024 + (size_t)lane * 8 + j;
     const h2f hv = pkrtz(v, 0.f);

@@ -18,8 +18,11 @@ __host__ __device__ inline int packed_ncb(int Cout) { return 6 * ((Cout + 191) /
 
 // floats of the fragment body of a packed weight; the buffer carries PACK_TRAILER more floats
 // (trailer[0] = max|w| of a split-fp16 packing)
+// 1x1 packings hold an even number of chunks: the split-fp16 1x1 kernel consumes them in pairs
+// (32-channel stages, see pack_weights_x3_kernel)
 __host__ __device__ inline size_t packed_body(int Cout, int Cin, int ntaps) {
-    const size_t nchunks = (Cin + CK - 1) / CK, ncb = packed_ncb(Cout);
+    const size_t nchunks = ntaps == 1 ? 2 * (size_t)((Cin + 2 * CK - 1) / (2 * CK)) : (Cin + CK - 1) / CK;
+    const size_t ncb = packed_ncb(Cout);
     return nchunks * ntaps * ncb * 2 * 64 * 4;
 }
 constexpr int PACK_TRAILER = 64;

@@ -490,16 +490,20 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
 // ---------------------------------------------------------------------------------------------
 // Split-fp16 1x1 conv without a patch ring: every wave is its own producer.  A 1x1 stage has 9x less
 // MFMA work per staged byte than a 3x3 one, so the ring kernel's single fetch in flight per work-group
-// leaves it bound by HBM latency.  Here a work-group is ncob = ceil(Cout / 64) waves over the same
-// PB * 32 output pixels (wave w: output channels [64w, 64w + 64)), each wave streams its B fragments
-// (the lane's pixel, 8 channels: two 16-B loads per pixel block) straight from HBM into a D-deep
-// register ring, so D - 1 stages are in flight per wave with no barrier; the co-block waves of a
-// work-group read the same bytes (one HBM fetch, L1/L2 hits).  The weights stream from L2 one K-group
-// ahead as in the ring kernel.  MFMA passes hi*hi, hi*lo, lo*hi as there; the epilogue is store_tile.
+// leaves it bound by HBM latency.  Here a work-group is up to 8 waves over the same PB * 32 output
+// pixels (wave w: output channels [co_lo + 64w, + 64), co_lo = 512 * blockIdx.z), each wave streaming
+// its B fragments straight from HBM into a D-deep register ring with no barrier; the co-block waves of
+// a work-group read the same bytes (one HBM fetch, L1/L2 hits).  A stage is 32 channels: lane half h
+// fetches the contiguous run [32s + 16h, + 16) of its pixel (64 B, four 16-B loads), which feeds two
+// K-groups — the packing (pack_weights_x3_kernel, ntaps == 1) orders the weights to match.  The
+// weights stream from L2 one stage ahead.  MFMA passes hi*hi, hi*lo, lo*hi as the ring kernel; the
+// epilogue goes through LDS (one contiguous channel run per pixel) or store_tile.
 template <int PB, int D>
-__global__ __launch_bounds__(256) void conv1x1_x3_kernel(const nps_conv2d_t a) {
+__global__ __launch_bounds__(512) void conv1x1_x3_kernel(const nps_conv2d_t a) {
     constexpr int CBW = 2;
-    const int lane = threadIdx.x & 63, cob = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int co_lo = blockIdx.z * 512;
+    const int cob = (co_lo >> 6) + wv;  // global 64-channel block of this wave
     const int b = blockIdx.y;
     const int h = lane >> 5;
     const int npx = a.Hout * a.Wout;
@@ -518,9 +522,10 @@ __global__ __launch_bounds__(256) void conv1x1_x3_kernel(const nps_conv2d_t a) {
         fx[pb] = a.circ ? nps::wrap_mod(xe - a.circ, a.Win) : xe;
         pin = ok ? (pin | (1u << pb)) : pin;
     }
-    const float* sp[PB];  // this lane's pixel in the current source (the sample base when outside it)
+    const float* sp[PB];  // this lane's pixel in its current source (the sample base when outside it)
     unsigned pok = 0;     // pixel blocks whose pixel lies inside the current source
-    int cur_src = -1;
+    int cur_src = -1;     // per lane: the two lane halves may read different sources
+    int cbase = 0;
     auto locate = [&](int sidx) {
         const nps_src_t S0 = a.src[0], S1 = a.src[1], S2 = a.src[2];
         const float* sptr = sidx == 0 ? S0.ptr : (sidx == 1 ? S1.ptr : S2.ptr);
@@ -538,56 +543,55 @@ __global__ __launch_bounds__(256) void conv1x1_x3_kernel(const nps_conv2d_t a) {
             pok = ok ? (pok | (1u << pb)) : pok;
         }
     };
-    const int nstages = (a.Cin + CK - 1) / CK;
+    const int nstages = (a.Cin + 2 * CK - 1) / (2 * CK);  // 32-channel stages
     const int last = nstages - 1;
-    f32x4 raw[D][PB][2];  // register ring of B stages (fp32, as loaded)
-    unsigned okm[D];      // per slot: bit 2*pb + q = float4 q of pixel block pb holds frame data
-    // fetch stage st into ring slot j (clamped stages are fetched anyway: uniform load counts)
-    auto issue = [&](int st, f32x4 (&r)[PB][2]) -> unsigned {
-        const int c0 = st * CK;
-        const int cend = min(c0 + CK, a.Cin);
-        int sidx = 0, cbase = 0;
-        {
-            int lo = 0;
+    f32x4 raw[D][PB][4];  // register ring of B stages (fp32, as loaded)
+    unsigned okm[D];      // per slot: bit 4*pb + q = float4 q of pixel block pb holds frame data
+    auto issue = [&](int st, f32x4 (&r)[PB][4]) -> unsigned {
+        const int c0 = st * 2 * CK + h * CK;  // this lane half's 16-channel run (inside one source:
+        int sidx = 0, lo = 0, sb = 0;         // sources are 16-aligned, host-checked)
 #pragma unroll
-            for (int si = 0; si < NPS_MAX_SRC; ++si) {
-                if (si < a.nsrc) {
-                    const int hi = lo + a.src[si].C;
-                    if (c0 >= lo && cend <= hi) {  // host-checked (x3_sources_aligned): one source per stage
-                        sidx = si;
-                        cbase = lo;
-                    }
-                    lo = hi;
+        for (int si = 0; si < NPS_MAX_SRC; ++si) {
+            if (si < a.nsrc) {
+                const int hi = lo + a.src[si].C;
+                if (c0 >= lo && c0 < hi) {
+                    sidx = si;
+                    sb = lo;
                 }
+                lo = hi;
             }
         }
-        if (sidx != cur_src) {  // uniform
+        if (sidx != cur_src) {  // per lane (the halves of a wave may differ)
             locate(sidx);
             cur_src = sidx;
+            cbase = sb;
         }
         unsigned m = 0;
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const bool chok = c0 + h * 8 + q * 4 < cend;  // past the channel tail: read channel 0, zeroed
-            const int cs = chok ? c0 - cbase + h * 8 + q * 4 : 0;
+        for (int q = 0; q < 4; ++q) {
+            const bool chok = c0 + q * 4 < a.Cin;  // past the channel tail: read channel 0, zeroed
+            const int cs = chok ? c0 - cbase + q * 4 : 0;
 #pragma unroll
             for (int pb = 0; pb < PB; ++pb) {
                 r[pb][q] = *reinterpret_cast<const f32x4*>(sp[pb] + cs);
-                m |= (chok && ((pok >> pb) & 1u)) ? 1u << (2 * pb + q) : 0u;
+                m |= (chok && ((pok >> pb) & 1u)) ? 1u << (4 * pb + q) : 0u;
             }
         }
         return m;
     };
     const int ncb = packed_ncb(a.Cout);
-    const size_t gstride = (size_t)ncb * 2048;
+    const size_t gstride = (size_t)ncb * 2048;  // bytes per chunk of the packed weight
     const char* wbase = reinterpret_cast<const char*>(a.wpack) + (size_t)cob * CBW * 2048 + lane * 16;
-    f16x8 Aw[2][CBW][2];  // weight fragments (L2-resident), one stage ahead
-    auto loadA = [&](int st, f16x8 (&d)[CBW][2]) {
-        const char* p = wbase + (size_t)st * gstride;
+    f16x8 Aw[2][2][CBW][2];  // [slot][chunk of the pair][cb][hi, lo]
+    auto loadA = [&](int st, f16x8 (&d)[2][CBW][2]) {
 #pragma unroll
-        for (int cb = 0; cb < CBW; ++cb) {
-            d[cb][0] = *reinterpret_cast<const f16x8*>(p + cb * 2048);
-            d[cb][1] = *reinterpret_cast<const f16x8*>(p + cb * 2048 + 1024);
+        for (int k = 0; k < 2; ++k) {
+            const char* p = wbase + (size_t)(2 * st + k) * gstride;
+#pragma unroll
+            for (int cb = 0; cb < CBW; ++cb) {
+                d[k][cb][0] = *reinterpret_cast<const f16x8*>(p + cb * 2048);
+                d[k][cb][1] = *reinterpret_cast<const f16x8*>(p + cb * 2048 + 1024);
+            }
         }
     };
     f32x16 acc[CBW][PB];
@@ -616,37 +620,43 @@ __global__ __launch_bounds__(256) void conv1x1_x3_kernel(const nps_conv2d_t a) {
             // keep the new fetches ahead of this stage's MFMAs: sunk below them, the MFMAs' wait for
             // this stage's operands would become vmcnt(0) and drain the whole ring every stage
             __builtin_amdgcn_sched_barrier(0);
-            f16x8 Bh[PB], Bl[PB];
-#pragma unroll
-            for (int pb = 0; pb < PB; ++pb) {
-                const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-                f16x4 h0, l0, h1, l1;
-                split4(((okm[j] >> (2 * pb)) & 1u) ? raw[j][pb][0] * xs : z, h0, l0);
-                split4(((okm[j] >> (2 * pb + 1)) & 1u) ? raw[j][pb][1] * xs : z, h1, l1);
-                Bh[pb] = f16x8{h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
-                Bl[pb] = f16x8{l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
-            }
             constexpr int r = j & 1;  // D is even: the weight slot parity is static
 #pragma unroll
-            for (int cb = 0; cb < CBW; ++cb)
+            for (int k = 0; k < 2; ++k) {  // the two K-groups of the stage: floats [8k, 8k + 8) of the run
+                f16x8 Bh[PB], Bl[PB];
 #pragma unroll
-                for (int pb = 0; pb < PB; ++pb) acc[cb][pb] = X3_MFMA(Aw[r][cb][0], Bh[pb], acc[cb][pb], 0, 0, 0);
+                for (int pb = 0; pb < PB; ++pb) {
+                    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+                    f16x4 h0, l0, h1, l1;
+                    split4(((okm[j] >> (4 * pb + 2 * k)) & 1u) ? raw[j][pb][2 * k] * xs : z, h0, l0);
+                    split4(((okm[j] >> (4 * pb + 2 * k + 1)) & 1u) ? raw[j][pb][2 * k + 1] * xs : z, h1, l1);
+                    Bh[pb] = f16x8{h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+                    Bl[pb] = f16x8{l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+                }
 #pragma unroll
-            for (int cb = 0; cb < CBW; ++cb)
+                for (int cb = 0; cb < CBW; ++cb)
 #pragma unroll
-                for (int pb = 0; pb < PB; ++pb) acc[cb][pb] = X3_MFMA(Aw[r][cb][0], Bl[pb], acc[cb][pb], 0, 0, 0);
+                    for (int pb = 0; pb < PB; ++pb)
+                        acc[cb][pb] = X3_MFMA(Aw[r][k][cb][0], Bh[pb], acc[cb][pb], 0, 0, 0);
 #pragma unroll
-            for (int cb = 0; cb < CBW; ++cb)
+                for (int cb = 0; cb < CBW; ++cb)
 #pragma unroll
-                for (int pb = 0; pb < PB; ++pb) acc[cb][pb] = X3_MFMA(Aw[r][cb][1], Bh[pb], acc[cb][pb], 0, 0, 0);
+                    for (int pb = 0; pb < PB; ++pb)
+                        acc[cb][pb] = X3_MFMA(Aw[r][k][cb][0], Bl[pb], acc[cb][pb], 0, 0, 0);
+#pragma unroll
+                for (int cb = 0; cb < CBW; ++cb)
+#pragma unroll
+                    for (int pb = 0; pb < PB; ++pb)
+                        acc[cb][pb] = X3_MFMA(Aw[r][k][cb][1], Bh[pb], acc[cb][pb], 0, 0, 0);
+            }
         });
     }
     const float inv = 1.f / (pow2_scale_for(a.wpack[packed_body(a.Cout, a.Cin, 1)]) * xs);
     if (x3_lds_epilogue(a)) {
-        // the work-group's ncob*64 x PB*32 tile goes through LDS (pitch = ncob*64 + 4 floats: conflict-free
-        // 16-B writes) and is stored pixel by pixel, each pixel's Cout channels one contiguous run
+        // the work-group's (waves*64) x PB*32 tile goes through LDS (pitch = waves*64 + 4 floats: conflict-
+        // free 16-B writes) and is stored pixel by pixel, each pixel's channels one contiguous run
         extern __shared__ __attribute__((aligned(16))) float T[];
-        const int pitch = (int)(blockDim.x) + 4;  // blockDim.x = 64 * ncob
+        const int pitch = (int)(blockDim.x) + 4;  // blockDim.x = 64 * waves
 #pragma unroll
         for (int pb = 0; pb < PB; ++pb) {
             const int P = pb * 32 + (lane & 31);
@@ -656,19 +666,20 @@ __global__ __launch_bounds__(256) void conv1x1_x3_kernel(const nps_conv2d_t a) {
                 for (int m = 0; m < 4; ++m) {
                     const f32x4 v = {acc[cb][pb][4 * m] * inv, acc[cb][pb][4 * m + 1] * inv,
                                      acc[cb][pb][4 * m + 2] * inv, acc[cb][pb][4 * m + 3] * inv};
-                    *reinterpret_cast<f32x4*>(T + P * pitch + cob * 64 + cb * 32 + 8 * m + 4 * h) = v;
+                    *reinterpret_cast<f32x4*>(T + P * pitch + wv * 64 + cb * 32 + 8 * m + 4 * h) = v;
                 }
         }
         __syncthreads();
-        const int C4 = a.Cout >> 2;
+        const int nco = min(a.Cout - co_lo, (int)blockDim.x);
+        const int C4 = nco >> 2;
         for (int i = threadIdx.x; i < PB * 32 * C4; i += blockDim.x) {
-            const int p = i / C4, co0 = (i - (i / C4) * C4) * 4;
+            const int p = i / C4, cl = (i - (i / C4) * C4) * 4, co0 = co_lo + cl;
             const int P = P0 + p;
             if (P >= npx) continue;
             const int oy = P / a.Wout, ox = P - (P / a.Wout) * a.Wout;
             const int dy = oy * a.out_os + a.out_off_y, dx = ox * a.out_os + a.out_off_x;
             if (dy < 0 || dy >= a.out_H || dx < 0 || dx >= a.out_W) continue;
-            const f32x4 accv = *reinterpret_cast<const f32x4*>(T + p * pitch + co0);
+            const f32x4 accv = *reinterpret_cast<const f32x4*>(T + p * pitch + cl);
             const size_t o = (((size_t)b * a.out_H + dy) * a.out_W + dx) * a.out_C + co0;
             const f32x4 z = {0.f, 0.f, 0.f, 0.f};
             const f32x4 bi = a.bias ? *reinterpret_cast<const f32x4*>(a.bias + co0) : z;
@@ -748,31 +759,26 @@ int nps_launch_conv2d_x3(const nps_conv2d_t& a, int lds, hipStream_t s) {
     const unsigned grid = (unsigned)(lds_epi && per < nwg ? per : nwg);
     const bool p512 = a.TH * a.TW == 512;
     const bool pro = a.gn_stats != nullptr || a.pre_act != 0;  // fused frame prologue: 3x3 only (host-checked)
-    // 1x1 convs without a prologue: the ring-free kernel (dev knob NPS_X3_1X1=ring keeps the ring kernel)
-    static int direct1 = -1;
-    if (direct1 < 0) {
-        const char* e = getenv("NPS_X3_1X1");
-        direct1 = (e != nullptr && e[0] == 'r') ? 0 : 1;
-    }
-    const int ncob = (a.Cout + 63) / 64;
-    if (direct1 && a.KH * a.KW == 1 && !pro && ncob <= 4) {
-        static int cfg = -1;  // dev knob NPS_X3_1X1_CFG: 0 = (PB 2, D 4), 1 = (2, 6), 2 = (1, 8), 3 = (1, 4)
-                              // (measured: 0 best or within 5 % on every rollout shape)
+    // 1x1 convs (never with a prologue: x3_eligible) run on the ring-free kernel, whose 32-channel
+    // stages match the 1x1 weight packing; work-group = min(ncob, 8) waves, blockIdx.z = 512-channel group
+    if (a.KH * a.KW == 1) {
+        NPS_CHECK_ARG(!pro, "conv2d_fwd (split-fp16): 1x1 prologue");
+        static int cfg = -1;  // dev knob NPS_X3_1X1_CFG: 0 = (PB 2, D 2), 1 = (1, 4)
         if (cfg < 0) {
             const char* e = getenv("NPS_X3_1X1_CFG");
-            cfg = e != nullptr ? atoi(e) & 3 : 0;
+            cfg = e != nullptr ? atoi(e) & 1 : 0;
         }
-        const int pb1 = cfg >= 2 ? 1 : 2;
+        const int pb1 = cfg == 1 ? 1 : 2;
+        const int ncob = (a.Cout + 63) / 64;
+        const int waves = ncob < 8 ? ncob : 8;
         const long nblk = ((long)a.Hout * a.Wout + pb1 * 32 - 1) / (pb1 * 32);
         NPS_CHECK_ARG(nblk < (1L << 31) && a.B < 65536, "conv2d_fwd: grid too large");
-        const dim3 grid1((unsigned)nblk, a.B);
-        const int lds1 = lds_epi ? pb1 * 32 * (64 * ncob + 4) * 4 : 0;
-        switch (cfg) {
-            case 1: conv1x1_x3_kernel<2, 6><<<grid1, 64 * ncob, lds1, s>>>(a); break;
-            case 2: conv1x1_x3_kernel<1, 8><<<grid1, 64 * ncob, lds1, s>>>(a); break;
-            case 3: conv1x1_x3_kernel<1, 4><<<grid1, 64 * ncob, lds1, s>>>(a); break;
-            default: conv1x1_x3_kernel<2, 4><<<grid1, 64 * ncob, lds1, s>>>(a); break;
-        }
+        const dim3 grid1((unsigned)nblk, a.B, (ncob + 7) / 8);
+        const int lds1 = lds_epi ? pb1 * 32 * (64 * waves + 4) * 4 : 0;
+        if (cfg == 1)
+            conv1x1_x3_kernel<1, 4><<<grid1, 64 * waves, lds1, s>>>(a);
+        else
+            conv1x1_x3_kernel<2, 2><<<grid1, 64 * waves, lds1, s>>>(a);
         NPS_CHECK_LAUNCH("conv2d_fwd (split-fp16 1x1)");
         return 0;
     }
@@ -788,7 +794,7 @@ int nps_launch_conv2d_x3(const nps_conv2d_t& a, int lds, hipStream_t s) {
             launch_x3_one<25, 2>(a, grid, lds, s);
             break;
         case 4: p512 ? launch_x3_one<4, 4>(a, grid, lds, s) : launch_x3_one<4, 2>(a, grid, lds, s); break;
-        default: p512 ? launch_x3_one<1, 4>(a, grid, lds, s) : launch_x3_one<1, 2>(a, grid, lds, s); break;
+        default: NPS_CHECK_ARG(false, "conv2d_fwd (split-fp16): unsupported tap count"); break;
     }
     NPS_CHECK_LAUNCH("conv2d_fwd (split-fp16)");
     return 0;

@@ -4,7 +4,8 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 TAG=${1:-x1}
 SHAPES=("--cin 388 --cout 192 --hw 260" "--cin 196 --cout 192 --hw 256" "--cin 84 --cout 192 --hw 256"
-        "--cin 192 --cout 192 --hw 132" "--cin 192 --cout 192 --hw 256")
+        "--cin 192 --cout 192 --hw 132" "--cin 192 --cout 192 --hw 256" "--cin 192 --cout 388 --hw 64"
+        "--cin 20 --cout 75 --hw 64" "--cin 48 --cout 512 --hw 40")
 for M in ${MODES:-direct ring}; do
   for A in "${SHAPES[@]}"; do
     echo "mode=$M $A"
