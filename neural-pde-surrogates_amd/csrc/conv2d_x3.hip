@@ -498,6 +498,10 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
 // K-groups — the packing (pack_weights_x3_kernel, ntaps == 1) orders the weights to match.  The
 // weights stream from L2 one stage ahead.  MFMA passes hi*hi, hi*lo, lo*hi as the ring kernel; the
 // epilogue goes through LDS (one contiguous channel run per pixel) or store_tile.
+// 64 zero bytes: the fetch address of B elements outside the frame or past the channel tail, so the
+// stage loop needs no masks (PMC: the 1x1 kernel issues 3-4k VALU instructions per wave)
+__device__ __attribute__((aligned(64))) float x3_zero16[16];
+
 template <int PB, int D>
 __global__ __launch_bounds__(512) void conv1x1_x3_kernel(const nps_conv2d_t a) {
     constexpr int CBW = 2;
@@ -509,6 +513,7 @@ __global__ __launch_bounds__(512) void conv1x1_x3_kernel(const nps_conv2d_t a) {
     const int npx = a.Hout * a.Wout;
     const int P0 = blockIdx.x * (PB * 32);
     const float xs = in_scale_of(a);
+    const bool scaled = a.in_scale != nullptr;  // range-scaled inputs (gradients); forward inputs are not
     // this lane's output pixel of each pixel block -> its (circularly extended) frame position
     int fy[PB], fx[PB];
     unsigned pin = 0;
@@ -522,8 +527,7 @@ __global__ __launch_bounds__(512) void conv1x1_x3_kernel(const nps_conv2d_t a) {
         fx[pb] = a.circ ? nps::wrap_mod(xe - a.circ, a.Win) : xe;
         pin = ok ? (pin | (1u << pb)) : pin;
     }
-    const float* sp[PB];  // this lane's pixel in its current source (the sample base when outside it)
-    unsigned pok = 0;     // pixel blocks whose pixel lies inside the current source
+    const float* sp[PB];  // this lane's pixel in its current source (x3_zero16 when outside it)
     int cur_src = -1;     // per lane: the two lane halves may read different sources
     int cbase = 0;
     auto locate = [&](int sidx) {
@@ -534,20 +538,17 @@ __global__ __launch_bounds__(512) void conv1x1_x3_kernel(const nps_conv2d_t a) {
         const int sW = sidx == 0 ? S0.W : (sidx == 1 ? S1.W : S2.W);
         const int soy = sidx == 0 ? S0.off_y : (sidx == 1 ? S1.off_y : S2.off_y);
         const int sox = sidx == 0 ? S0.off_x : (sidx == 1 ? S1.off_x : S2.off_x);
-        pok = 0;
 #pragma unroll
         for (int pb = 0; pb < PB; ++pb) {
             const int yy = fy[pb] - soy, xx = fx[pb] - sox;
             const bool ok = ((pin >> pb) & 1u) && yy >= 0 && yy < sH && xx >= 0 && xx < sW;
-            sp[pb] = sptr + (ok ? ((size_t)(b * sH + yy) * sW + xx) * sC : (size_t)b * sH * sW * sC);
-            pok = ok ? (pok | (1u << pb)) : pok;
+            sp[pb] = ok ? sptr + ((size_t)(b * sH + yy) * sW + xx) * sC : nullptr;
         }
     };
     const int nstages = (a.Cin + 2 * CK - 1) / (2 * CK);  // 32-channel stages
     const int last = nstages - 1;
-    f32x4 raw[D][PB][4];  // register ring of B stages (fp32, as loaded)
-    unsigned okm[D];      // per slot: bit 4*pb + q = float4 q of pixel block pb holds frame data
-    auto issue = [&](int st, f32x4 (&r)[PB][4]) -> unsigned {
+    f32x4 raw[D][PB][4];  // register ring of B stages (fp32, as loaded; zeros outside the frame)
+    auto issue = [&](int st, bool live, f32x4 (&r)[PB][4]) {
         const int c0 = st * 2 * CK + h * CK;  // this lane half's 16-channel run (inside one source:
         int sidx = 0, lo = 0, sb = 0;         // sources are 16-aligned, host-checked)
 #pragma unroll
@@ -566,18 +567,15 @@ __global__ __launch_bounds__(512) void conv1x1_x3_kernel(const nps_conv2d_t a) {
             cur_src = sidx;
             cbase = sb;
         }
-        unsigned m = 0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const bool chok = c0 + q * 4 < a.Cin;  // past the channel tail: read channel 0, zeroed
-            const int cs = chok ? c0 - cbase + q * 4 : 0;
+            const bool chok = live && c0 + q * 4 < a.Cin;  // past the channel tail (or a padded stage): zeros
 #pragma unroll
             for (int pb = 0; pb < PB; ++pb) {
-                r[pb][q] = *reinterpret_cast<const f32x4*>(sp[pb] + cs);
-                m |= (chok && ((pok >> pb) & 1u)) ? 1u << (4 * pb + q) : 0u;
+                const float* src = (chok && sp[pb] != nullptr) ? sp[pb] + (c0 - cbase + q * 4) : x3_zero16;
+                r[pb][q] = *reinterpret_cast<const f32x4*>(src);
             }
         }
-        return m;
     };
     const int ncb = packed_ncb(a.Cout);
     const size_t gstride = (size_t)ncb * 2048;  // bytes per chunk of the packed weight
@@ -606,7 +604,7 @@ __global__ __launch_bounds__(512) void conv1x1_x3_kernel(const nps_conv2d_t a) {
     // all-zero mask, so their MFMAs add exact zeros
     static_for<D - 1>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
-        okm[j] = issue(min(j, last), raw[j]) & (j <= last ? ~0u : 0u);
+        issue(min(j, last), j <= last, raw[j]);
     });
     loadA(0, Aw[0]);
     const int npad = (nstages + D - 1) / D * D;
@@ -615,7 +613,7 @@ __global__ __launch_bounds__(512) void conv1x1_x3_kernel(const nps_conv2d_t a) {
             constexpr int j = decltype(jc)::value;
             constexpr int jn = (j + D - 1) % D;
             const int st = s0 + j;
-            okm[jn] = issue(min(st + D - 1, last), raw[jn]) & (st + D - 1 <= last ? ~0u : 0u);
+            issue(min(st + D - 1, last), st + D - 1 <= last, raw[jn]);
             loadA(min(st + 1, last), Aw[(j + 1) & 1]);
             // keep the new fetches ahead of this stage's MFMAs: sunk below them, the MFMAs' wait for
             // this stage's operands would become vmcnt(0) and drain the whole ring every stage
@@ -626,10 +624,14 @@ __global__ __launch_bounds__(512) void conv1x1_x3_kernel(const nps_conv2d_t a) {
                 f16x8 Bh[PB], Bl[PB];
 #pragma unroll
                 for (int pb = 0; pb < PB; ++pb) {
-                    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
                     f16x4 h0, l0, h1, l1;
-                    split4(((okm[j] >> (4 * pb + 2 * k)) & 1u) ? raw[j][pb][2 * k] * xs : z, h0, l0);
-                    split4(((okm[j] >> (4 * pb + 2 * k + 1)) & 1u) ? raw[j][pb][2 * k + 1] * xs : z, h1, l1);
+                    f32x4 v0 = raw[j][pb][2 * k], v1 = raw[j][pb][2 * k + 1];
+                    if (scaled) {
+                        v0 *= xs;
+                        v1 *= xs;
+                    }
+                    split4(v0, h0, l0);
+                    split4(v1, h1, l1);
                     Bh[pb] = f16x8{h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
                     Bl[pb] = f16x8{l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
                 }
@@ -672,11 +674,35 @@ __global__ __launch_bounds__(512) void conv1x1_x3_kernel(const nps_conv2d_t a) {
         __syncthreads();
         const int nco = min(a.Cout - co_lo, (int)blockDim.x);
         const int C4 = nco >> 2;
+        // item i = (pixel p, channel quad): when C4 divides the block, a thread keeps one channel quad
+        // and steps pixels by blockDim / C4 (no per-item divisions)
+        const bool fixq = ((int)blockDim.x % C4) == 0;
+        const int pstep = fixq ? (int)blockDim.x / C4 : 0;
+        int fp = fixq ? (int)threadIdx.x / C4 : 0;
+        const int fcl = fixq ? ((int)threadIdx.x - fp * C4) * 4 : 0;
+        int foy = (P0 + fp) / a.Wout, fox = (P0 + fp) - ((P0 + fp) / a.Wout) * a.Wout;
         for (int i = threadIdx.x; i < PB * 32 * C4; i += blockDim.x) {
-            const int p = i / C4, cl = (i - (i / C4) * C4) * 4, co0 = co_lo + cl;
+            int p, cl, oy, ox;
+            if (fixq) {
+                p = fp;
+                cl = fcl;
+                oy = foy;
+                ox = fox;
+                fp += pstep;
+                fox += pstep;
+                while (fox >= a.Wout) {
+                    fox -= a.Wout;
+                    ++foy;
+                }
+            } else {
+                p = i / C4;
+                cl = (i - (i / C4) * C4) * 4;
+                oy = (P0 + p) / a.Wout;
+                ox = (P0 + p) - ((P0 + p) / a.Wout) * a.Wout;
+            }
+            const int co0 = co_lo + cl;
             const int P = P0 + p;
             if (P >= npx) continue;
-            const int oy = P / a.Wout, ox = P - (P / a.Wout) * a.Wout;
             const int dy = oy * a.out_os + a.out_off_y, dx = ox * a.out_os + a.out_off_x;
             if (dy < 0 || dy >= a.out_H || dx < 0 || dx >= a.out_W) continue;
             const f32x4 accv = *reinterpret_cast<const f32x4*>(T + p * pitch + cl);
