@@ -789,12 +789,12 @@ int nps_launch_conv2d_x3(const nps_conv2d_t& a, int lds, hipStream_t s) {
     // stages match the 1x1 weight packing; work-group = min(ncob, 8) waves, blockIdx.z = 512-channel group
     if (a.KH * a.KW == 1) {
         NPS_CHECK_ARG(!pro, "conv2d_fwd (split-fp16): 1x1 prologue");
-        static int cfg = -1;  // dev knob NPS_X3_1X1_CFG: 0 = (PB 2, D 2), 1 = (1, 4)
+        static int cfg = -1;  // dev knob NPS_X3_1X1_CFG: 0 = (PB 2, D 2), 1 = (1, 4), 2 = (1, 2)
         if (cfg < 0) {
             const char* e = getenv("NPS_X3_1X1_CFG");
-            cfg = e != nullptr ? atoi(e) & 1 : 0;
+            cfg = e != nullptr ? atoi(e) % 3 : 0;
         }
-        const int pb1 = cfg == 1 ? 1 : 2;
+        const int pb1 = cfg >= 1 ? 1 : 2;
         const int ncob = (a.Cout + 63) / 64;
         const int waves = ncob < 8 ? ncob : 8;
         const long nblk = ((long)a.Hout * a.Wout + pb1 * 32 - 1) / (pb1 * 32);
@@ -803,6 +803,8 @@ int nps_launch_conv2d_x3(const nps_conv2d_t& a, int lds, hipStream_t s) {
         const int lds1 = lds_epi ? pb1 * 32 * (64 * waves + 4) * 4 : 0;
         if (cfg == 1)
             conv1x1_x3_kernel<1, 4><<<grid1, 64 * waves, lds1, s>>>(a);
+        else if (cfg == 2)
+            conv1x1_x3_kernel<1, 2><<<grid1, 64 * waves, lds1, s>>>(a);
         else
             conv1x1_x3_kernel<2, 2><<<grid1, 64 * waves, lds1, s>>>(a);
         NPS_CHECK_LAUNCH("conv2d_fwd (split-fp16 1x1)");
