@@ -110,10 +110,12 @@ int nps_conv2d_pack_weights(const float* w, float* wpack, int Cout, int Cin, int
                             int transposed_phase, void* stream);
 /* Same transforms, packed as [hi | lo] fp16 MFMA fragments of s*w for precision = NPS_PREC_X3F16, with s
  * the power of 2 that maps max|w| into [2^13, 2^14) (max|w| is kept in the buffer's trailer; same buffer
- * size as nps_conv2d_packed_size). */
+ * size as nps_conv2d_packed_size).  1x1 weights are packed in 32-channel chunk pairs (each MFMA lane half
+ * owns a contiguous 16-channel run), so the chunk count of a 1x1 packing is even. */
 int nps_conv2d_pack_weights_x3(const float* w, float* wpack, int Cout, int Cin, int KH, int KW,
                                int transposed_phase, void* stream);
-/* 1 when a conv of this geometry runs on the split-fp16 kernel (stride-1, undilated 1x1 / 2x2 / 3x3). */
+/* 1 when a conv of this geometry runs on the split-fp16 kernel (stride-1: undilated 1x1 / 2x2 / 3x3, and
+ * 5x5 at any dilation — the dilated ResNet's convs, proc_dilatedresnet.py:15-84). */
 int nps_conv2d_x3_eligible(int KH, int KW, int stride, int dil);
 /* 1 when the split-fp16 kernel applies a frame prologue itself (gn_groups > 0: GroupNorm affine with that
  * many groups; pre_act 1: GELU) — the 3x3 kernel, with Cin / gn_groups a multiple of 4 — so the caller
