@@ -745,6 +745,158 @@ __global__ __launch_bounds__(512) void conv1x1_x3_kernel(const nps_conv2d_t a) {
     });
 }
 
+// 1x1 with the weights staged in LDS: a wave covers ALL output channels (NCB 32-channel blocks) of its
+// 32 pixels, so a work-group of 4 waves (128 pixels) fetches its input once per CU instead of once per
+// co-block wave.  Per 32-channel stage the 4 waves copy the stage's weight fragments (2 chunks x NCB
+// blocks x 2 KB) into one of two LDS buffers (fetched one stage ahead into registers, compiler-managed
+// loads), one barrier per stage; B as in conv1x1_x3_kernel (per-lane 64-B runs in a D-deep register
+// ring, zero page outside the frame).  Epilogue: store_tile per 32-channel block.
+template <int NCB, int D>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void conv1x1_wl_kernel(const nps_conv2d_t a) {
+    constexpr int WSTAGE = 2 * NCB * 2048;       // bytes of one stage's weight fragments
+    constexpr int WPT = WSTAGE / (256 * 16);     // 16-B pieces per thread per stage
+    static_assert(WSTAGE % (256 * 16) == 0, "weight stage split");
+    extern __shared__ __attribute__((aligned(16))) char wl[];  // [2][2 chunks][NCB][hi|lo][64][16 B]
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int b = blockIdx.y;
+    const int h = lane >> 5;
+    const int npx = a.Hout * a.Wout;
+    const int P = blockIdx.x * 128 + wv * 32 + (lane & 31);
+    const float xs = in_scale_of(a);
+    const bool scaled = a.in_scale != nullptr;
+    int fy, fx;
+    bool pin;
+    {
+        const int oy = P / a.Wout, ox = P - (P / a.Wout) * a.Wout;
+        const int ye = oy - a.pad_y, xe = ox - a.pad_x;
+        pin = P < npx && ye >= 0 && ye < a.Hin + 2 * a.circ && xe >= 0 && xe < a.Win + 2 * a.circ;
+        fy = a.circ ? nps::wrap_mod(ye - a.circ, a.Hin) : ye;
+        fx = a.circ ? nps::wrap_mod(xe - a.circ, a.Win) : xe;
+    }
+    const float* sp = nullptr;
+    int cur_src = -1, cbase = 0;
+    auto locate = [&](int sidx) {
+        const nps_src_t S0 = a.src[0], S1 = a.src[1], S2 = a.src[2];
+        const float* sptr = sidx == 0 ? S0.ptr : (sidx == 1 ? S1.ptr : S2.ptr);
+        const int sC = sidx == 0 ? S0.C : (sidx == 1 ? S1.C : S2.C);
+        const int sH = sidx == 0 ? S0.H : (sidx == 1 ? S1.H : S2.H);
+        const int sW = sidx == 0 ? S0.W : (sidx == 1 ? S1.W : S2.W);
+        const int yy = fy - (sidx == 0 ? S0.off_y : (sidx == 1 ? S1.off_y : S2.off_y));
+        const int xx = fx - (sidx == 0 ? S0.off_x : (sidx == 1 ? S1.off_x : S2.off_x));
+        const bool ok = pin && yy >= 0 && yy < sH && xx >= 0 && xx < sW;
+        sp = ok ? sptr + ((size_t)(b * sH + yy) * sW + xx) * sC : nullptr;
+    };
+    const int nstages = (a.Cin + 2 * CK - 1) / (2 * CK);
+    const int last = nstages - 1;
+    f32x4 raw[D][4];
+    auto issue = [&](int st, bool live, f32x4 (&r)[4]) {
+        const int c0 = st * 2 * CK + h * CK;
+        int sidx = 0, lo = 0, sb = 0;
+#pragma unroll
+        for (int si = 0; si < NPS_MAX_SRC; ++si) {
+            if (si < a.nsrc) {
+                const int hi = lo + a.src[si].C;
+                if (c0 >= lo && c0 < hi) {
+                    sidx = si;
+                    sb = lo;
+                }
+                lo = hi;
+            }
+        }
+        if (sidx != cur_src) {
+            locate(sidx);
+            cur_src = sidx;
+            cbase = sb;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const bool chok = live && c0 + q * 4 < a.Cin;
+            const float* src = (chok && sp != nullptr) ? sp + (c0 - cbase + q * 4) : x3_zero16;
+            r[q] = *reinterpret_cast<const f32x4*>(src);
+        }
+    };
+    // weight stage st: chunks 2st, 2st + 1, blocks [0, NCB) of each (the packed chunk holds packed_ncb blocks)
+    const size_t gstride = (size_t)packed_ncb(a.Cout) * 2048;
+    const char* wg = reinterpret_cast<const char*>(a.wpack);
+    f32x4 wr[WPT];
+    auto wfetch = [&](int st) {
+#pragma unroll
+        for (int i = 0; i < WPT; ++i) {
+            const int off = (i * 256 + (int)threadIdx.x) * 16;  // byte offset inside the stage
+            const int k = off / (NCB * 2048), rem = off - k * (NCB * 2048);
+            wr[i] = *reinterpret_cast<const f32x4*>(wg + (size_t)(2 * st + k) * gstride + rem);
+        }
+    };
+    auto wstore = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < WPT; ++i)
+            *reinterpret_cast<f32x4*>(wl + buf * WSTAGE + (i * 256 + (int)threadIdx.x) * 16) = wr[i];
+    };
+    f32x16 acc[NCB];
+#pragma unroll
+    for (int i = 0; i < NCB; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+    static_for<D - 1>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        issue(min(j, last), j <= last, raw[j]);
+    });
+    wfetch(0);
+    wstore(0);
+    wfetch(min(1, last));
+    __syncthreads();
+    const int npad = (nstages + D - 1) / D * D;
+    for (int s0 = 0; s0 < npad; s0 += D) {
+        static_for<D>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            constexpr int jn = (j + D - 1) % D;
+            const int st = s0 + j;
+            // weights of stage st + 1 (fetched last stage) -> the other buffer (its readers passed the
+            // previous barrier); then fetch stage st + 2's
+            wstore((st + 1) & 1);
+            wfetch(min(st + 2, last));
+            issue(min(st + D - 1, last), st + D - 1 <= last, raw[jn]);
+            __builtin_amdgcn_sched_barrier(0);
+            const char* wb = wl + (st & 1) * WSTAGE + lane * 16;
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                f16x4 h0, l0, h1, l1;
+                f32x4 v0 = raw[j][2 * k], v1 = raw[j][2 * k + 1];
+                if (scaled) {
+                    v0 *= xs;
+                    v1 *= xs;
+                }
+                split4(v0, h0, l0);
+                split4(v1, h1, l1);
+                const f16x8 Bh = f16x8{h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+                const f16x8 Bl = f16x8{l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+#pragma unroll
+                for (int cb = 0; cb < NCB; ++cb) {
+                    const f16x8 Ah = *reinterpret_cast<const f16x8*>(wb + (k * NCB + cb) * 2048);
+                    const f16x8 Al = *reinterpret_cast<const f16x8*>(wb + (k * NCB + cb) * 2048 + 1024);
+                    acc[cb] = X3_MFMA(Ah, Bh, acc[cb], 0, 0, 0);
+                    acc[cb] = X3_MFMA(Ah, Bl, acc[cb], 0, 0, 0);
+                    acc[cb] = X3_MFMA(Al, Bh, acc[cb], 0, 0, 0);
+                }
+            }
+            __syncthreads();
+        });
+    }
+    const float inv = 1.f / (pow2_scale_for(a.wpack[packed_body(a.Cout, a.Cin, 1)]) * xs);
+    if (P >= npx) return;
+    const int oy = P / a.Wout, ox = P - (P / a.Wout) * a.Wout;
+    const int dy = oy * a.out_os + a.out_off_y, dx = ox * a.out_os + a.out_off_x;
+    if (dy < 0 || dy >= a.out_H || dx < 0 || dx >= a.out_W) return;
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) {
+        if (cb * 32 >= a.Cout) continue;
+        f32x16 v = acc[cb];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] *= inv;
+        store_tile(a, b, cb * 32, h, v, dy, dx);
+    }
+}
+
 template <int NT, int PB, bool PRO = false>
 void launch_x3_one(const nps_conv2d_t& a, unsigned nwg, int lds, hipStream_t s) {
     static bool attr_set = false;
@@ -794,8 +946,26 @@ int nps_launch_conv2d_x3(const nps_conv2d_t& a, int lds, hipStream_t s) {
             const char* e = getenv("NPS_X3_1X1_CFG");
             cfg = e != nullptr ? atoi(e) % 3 : 0;
         }
-        const int pb1 = cfg >= 1 ? 1 : 2;
         const int ncob = (a.Cout + 63) / 64;
+        static int wl = -1;  // dev knob NPS_X3_1X1_WL=0: co-block waves instead of LDS-staged weights
+        if (wl < 0) {
+            const char* e = getenv("NPS_X3_1X1_WL");
+            wl = (e != nullptr && e[0] == '0') ? 0 : 1;
+        }
+        if (wl && a.Cout <= 192) {  // (Cout 193..256 measured slower with 8 blocks per wave: co-block waves)
+            const long nb = ((long)a.Hout * a.Wout + 127) / 128;
+            NPS_CHECK_ARG(nb < (1L << 31) && a.B < 65536, "conv2d_fwd: grid too large");
+            static bool set6 = false;
+            if (!set6) {
+                (void)hipFuncSetAttribute((const void*)conv1x1_wl_kernel<6, 4>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                set6 = true;
+            }
+            conv1x1_wl_kernel<6, 4><<<dim3((unsigned)nb, a.B), 256, 2 * 2 * 6 * 2048, s>>>(a);
+            NPS_CHECK_LAUNCH("conv2d_fwd (split-fp16 1x1, LDS weights)");
+            return 0;
+        }
+        const int pb1 = cfg >= 1 ? 1 : 2;
         const int waves = ncob < 8 ? ncob : 8;
         const long nblk = ((long)a.Hout * a.Wout + pb1 * 32 - 1) / (pb1 * 32);
         NPS_CHECK_ARG(nblk < (1L << 31) && a.B < 65536, "conv2d_fwd: grid too large");
