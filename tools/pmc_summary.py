@@ -25,9 +25,11 @@ def load(d, counter):
 
 
 def klass(name):
-    m = re.search(r"conv2d_x3_kernel<(\d+), \d+>", name)
+    m = re.search(r"conv2d_x3_kernel<(\d+), \d+(?:, (?:true|false))?>", name)
     if m:
         return f"x3f16_{m.group(1)}tap"
+    if re.search(r"conv1x1_(?:x3|wl)_kernel<", name):
+        return "x3f16_1tap"
     m = re.search(r"conv2d_pc_kernel<(\d+), \d+, \d+, \d+, \d+>", name)
     if m:
         return f"f32_{m.group(1)}tap"
