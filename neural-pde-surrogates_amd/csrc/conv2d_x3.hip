@@ -955,13 +955,18 @@ int nps_launch_conv2d_x3(const nps_conv2d_t& a, int lds, hipStream_t s) {
         if (wl && a.Cout <= 192) {  // (Cout 193..256 measured slower with 8 blocks per wave: co-block waves)
             const long nb = ((long)a.Hout * a.Wout + 127) / 128;
             NPS_CHECK_ARG(nb < (1L << 31) && a.B < 65536, "conv2d_fwd: grid too large");
-            static bool set6 = false;
-            if (!set6) {
-                (void)hipFuncSetAttribute((const void*)conv1x1_wl_kernel<6, 4>,
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-                set6 = true;
+            static int wd = -1;  // dev knob NPS_X3_WL_D: B-ring depth 2 / 3 / 4 (default 2: measured fastest
+            if (wd < 0) {        // on every rollout shape, profiles/r1_conv_shapes_1x1_wl_depth.log)
+                const char* e = getenv("NPS_X3_WL_D");
+                wd = (e != nullptr && (atoi(e) == 3 || atoi(e) == 4)) ? atoi(e) : 2;
             }
-            conv1x1_wl_kernel<6, 4><<<dim3((unsigned)nb, a.B), 256, 2 * 2 * 6 * 2048, s>>>(a);
+            const dim3 gw((unsigned)nb, a.B);
+            if (wd == 2)
+                conv1x1_wl_kernel<6, 2><<<gw, 256, 2 * 2 * 6 * 2048, s>>>(a);
+            else if (wd == 3)
+                conv1x1_wl_kernel<6, 3><<<gw, 256, 2 * 2 * 6 * 2048, s>>>(a);
+            else
+                conv1x1_wl_kernel<6, 4><<<gw, 256, 2 * 2 * 6 * 2048, s>>>(a);
             NPS_CHECK_LAUNCH("conv2d_fwd (split-fp16 1x1, LDS weights)");
             return 0;
         }
