@@ -32,6 +32,13 @@ CONV_CASES = [
     (132, 128, 5, 1, 4, "same", "circular", 40, 36),
     (81, 192, 1, 1, 1, 0, "zeros", 19, 23),         # encoder 1x1, Cin % 4 != 0
     (192, 75, 1, 1, 1, 0, "zeros", 16, 16),         # pre-decoder 1x1, Cout % 32 != 0
+    # 1x1 kernels: LDS-weight (Cout <= 192) and co-block waves (Cout > 192, 512-channel grid split)
+    (196, 192, 1, 1, 1, 0, "zeros", 37, 29),        # LDS weights, 32-channel stage tail (196 = 6*32 + 4)
+    (20, 192, 1, 1, 1, 1, "zeros", 13, 11),         # LDS weights, single partial stage, zero pad 1 (frame offset)
+    (48, 388, 1, 1, 1, 0, "zeros", 15, 17),         # co-block waves, 7 waves
+    (36, 600, 1, 1, 1, 0, "circular", 9, 10),       # co-block waves, two 512-channel groups
+    (12, 16, 5, 1, 1, 2, "zeros", 19, 21),          # undilated 5x5, zero pad (split-fp16 25-tap kernel)
+    (16, 24, 5, 1, 2, 4, "zeros", 23, 18),          # dilated 5x5 on the lattice, zero pad
 ]
 
 
