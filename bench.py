@@ -132,6 +132,25 @@ def attach_traffic(roof, headline):
     return roof
 
 
+def shard_bounds(global_batch, world, rank):
+    """[lo, hi) of this rank's samples of the global batch: equal contiguous shards (strong scaling; the
+    rollout samples are independent, so no collective touches the data path)."""
+    if global_batch % world != 0:
+        raise SystemExit(f"global batch {global_batch} not divisible by {world} ranks")
+    per = global_batch // world
+    return rank * per, (rank + 1) * per
+
+
+def max_over_ranks(elapsed, device):
+    """The job's wall time: the slowest rank's (one all-reduce MAX; identity in a single process)."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return elapsed
+    t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t.item()
+
+
 def cpu_baseline(model, ocfg, opde, res, num_c, calls=2, B=2):
     import oracle
     from trainers.synthetic import twophase_batch
@@ -186,9 +205,8 @@ def main():
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     dev = torch.device("cuda", local_rank)
-    if args.global_batch % world != 0:
-        raise SystemExit(f"global batch {args.global_batch} not divisible by {world} ranks")
-    B = args.global_batch // world
+    lo, hi = shard_bounds(args.global_batch, world, rank)
+    B = hi - lo
     tw = 25
 
     import argparse as _ap
@@ -204,9 +222,9 @@ def main():
                                       obstacle="disc")
     u_all, _, _, _ = twophase_batch(B, args.num_c, T, args.res, args.res, seed=1234 + rank, obstacle="disc",
                                     device=dev)
-    cond = cond[rank * B:(rank + 1) * B].to(dev)
-    pos = pos[rank * B:(rank + 1) * B].to(dev)
-    sc = sc[rank * B:(rank + 1) * B].to(dev)
+    cond = cond[lo:hi].to(dev)
+    pos = pos[lo:hi].to(dev)
+    sc = sc[lo:hi].to(dev)
     cfg = _ap.Namespace(time_window=tw, base_resolution=(T, args.res, args.res), device=dev, nr_gt_steps=1)
     tr = AutoregressivePushforwardTrainer(model=model, data=types.SimpleNamespace(pde=model.pde, data_interface=D.sim2d),
                                           criterion=nn.MSELoss(reduction="sum"), config=cfg)
@@ -228,11 +246,7 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = t.item()
+    elapsed = max_over_ranks(time.perf_counter() - t0, dev)
     value = args.global_batch * tw * args.steps / elapsed
 
     if rank == 0:
@@ -276,9 +290,8 @@ def run_train(args):
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     dev = torch.device("cuda", local_rank)
-    if args.global_batch % world != 0:
-        raise SystemExit(f"global batch {args.global_batch} not divisible by {world} ranks")
-    B = args.global_batch // world
+    lo, hi = shard_bounds(args.global_batch, world, rank)
+    B = hi - lo
     tw = 25
     model, _, _ = build_model(args.model, args.res, args.num_c, dev, fno_modes=args.fno_modes)
     model.train()
@@ -308,11 +321,7 @@ def run_train(args):
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = t.item()
+    elapsed = max_over_ranks(time.perf_counter() - t0, dev)
     if rank == 0:
         print(json.dumps({
             "metric": "pushforward training samples/sec (train_step + backward + all-reduce + Adam)",

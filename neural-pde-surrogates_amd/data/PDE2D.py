@@ -1,6 +1,11 @@
-"""PDE2DDataset (reference data/PDE2D.py:12-110): a MemMapDataset split into train / valid / test
-subsets plus the PDE2D metadata (dt, grid, conditioning counts) the models are built from."""
+"""PDE2DDataset: the twophase cfgs' dataset object (reference data/PDE2D.py:12-110).
+
+One MemMapDataset over <base_path>/<experiment>, split into train / valid / test Subsets (from a split
+yaml, else a trailing val / test fraction), plus the PDE2D metadata the model builder reads (time axis,
+grid lengths and sizes, conditioning channel counts).  `c_filter` keeps a subset of the trajectory
+channels (cfg_twophase_*: c_filter=[6])."""
 import os
+from typing import Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -13,6 +18,37 @@ from pdes import PDE2D
 from utils.load_yaml import load_yaml
 
 
+class ChannelFilter:
+    """Per-item transform u (C, T, ...) -> u[channels]."""
+
+    def __init__(self, channels: Sequence[int]):
+        self.channels = np.asarray(channels)
+
+    def __call__(self, u):
+        return u[self.channels]
+
+
+def split_indices(n: int, split_path: Optional[str], split_val: float,
+                  split_test: float) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """(train, valid, test) sample indices: the lists of a split yaml when given, else the last
+    int(split_test * n) samples for test, the int(split_val * n) before them for validation and the rest
+    for training (an empty valid / test fraction gives an empty split)."""
+    if split_path is not None:
+        s = load_yaml(split_path)
+        return tuple(np.array(s[k]) for k in ("train", "valid", "test"))
+    idx = np.arange(n)
+    n_val, n_test = int(split_val * n), int(split_test * n)
+    # negative-start slicing as the reference (idx[:-(v+t)], idx[-(v+t):-t], idx[-t:]): an empty valid
+    # or test fraction therefore selects nothing for training / everything for test
+    tr = idx[:-(n_val + n_test)]
+    va = idx[-(n_val + n_test):-n_test]
+    te = idx[-n_test:]
+    print(f"Warning: no split file given; splitting {n} samples by fraction "
+          f"(valid {split_val:g}, test {split_test:g}): train {tr.shape[0]} / valid {va.shape[0]} / "
+          f"test {te.shape[0]}")
+    return tr, va, te
+
+
 class PDE2DDataset(DatasetInterface):
     data_interface = D.sim2d
 
@@ -20,54 +56,35 @@ class PDE2DDataset(DatasetInterface):
                  t_conditioning: str = None, spatial_conditioning: str = None, c_filter: list = None,
                  split_file: str = None, split_val: float = .05, split_test: float = .05, name: str = "PDE2D",
                  preprocess: bool = False, preprocess_path: str = None):
-        data_path = os.path.join(base_path, f"{experiment}")
         self.experiment = experiment
-        if c_filter is not None:
-            c_filter = np.array(c_filter)
-            data_transform = lambda u: u[c_filter]  # noqa: E731  (PDE2D.py:34-36)
-        else:
-            data_transform = None
+        root = os.path.join(base_path, experiment)
         self.dataset = MemMapDataset(
-            data_path, data_file, data_format=data_format, conditioning=conditioning, t_conditioning=t_conditioning,
-            spatial_conditioning=spatial_conditioning, data_transform=data_transform, grid_transform=None,
-            preprocess=preprocess, preprocess_path=preprocess_path, conditioning_transform=None,
-            t_conditioning_transform=None)
-        if split_file is not None:  # :49-56
-            if not split_file.lower().endswith(".yaml"):
-                split_file = split_file + ".yaml"
-            split = load_yaml(os.path.join(data_path, split_file))
-            train_idx = np.array(split["train"])
-            valid_idx = np.array(split["valid"])
-            test_idx = np.array(split["test"])
-        else:  # :57-66
-            idx = np.arange(len(self.dataset))
-            n_val = int(split_val * len(self.dataset))
-            n_test = int(split_test * len(self.dataset))
-            train_idx = idx[:-(n_val + n_test)]
-            valid_idx = idx[-(n_val + n_test):-n_test]
-            test_idx = idx[-n_test:]
-            print(f"Warning: No data split provided. Using {(1 - split_val - split_test) * 100:.1f}%:"
-                  f"{split_val * 100:.1f}%:{split_test * 100:.1f}% train:valid:test ([0:{train_idx.shape[0]}], "
-                  f"[{train_idx.shape[0]}:{train_idx.shape[0] + valid_idx.shape[0]}], "
-                  f"[{train_idx.shape[0] + valid_idx.shape[0]}, "
-                  f"{train_idx.shape[0] + valid_idx.shape[0] + test_idx.shape[0]}]) ")
-        self.train_dataset = torch.utils.data.Subset(self.dataset, train_idx)
-        self.valid_dataset = torch.utils.data.Subset(self.dataset, valid_idx)
-        self.test_dataset = torch.utils.data.Subset(self.dataset, test_idx)
+            root, data_file, data_format=data_format, conditioning=conditioning, t_conditioning=t_conditioning,
+            spatial_conditioning=spatial_conditioning,
+            data_transform=ChannelFilter(c_filter) if c_filter is not None else None,
+            preprocess=preprocess, preprocess_path=preprocess_path)
+        split_path = None
+        if split_file is not None:
+            split_path = os.path.join(root, split_file if split_file.lower().endswith(".yaml") else split_file + ".yaml")
+        parts = split_indices(len(self.dataset), split_path, split_val, split_test)
+        self.train_dataset, self.valid_dataset, self.test_dataset = (torch.utils.data.Subset(self.dataset, p)
+                                                                     for p in parts)
+        self._pde = self._make_pde(name, conditioning, t_conditioning, spatial_conditioning)
 
-        nt_in = int(self.dataset.tmax / self.dataset.dt) + 1  # :73-92
-        nt_out = nt_in
-        tmin, tmax = transforms.get_t_downsample(self.dataset.tmin, self.dataset.tmax, nt_in, ratio_nt=1)
-        x = self.dataset.x
-        nx1, nx2 = x.shape[:2]
-        L1 = x[-1, 0, 0] - x[0, 0, 0]
-        L2 = x[0, -1, 1] - x[0, 0, 1]
-        _, _, _, cond, t_cond, spatial_cond = self.dataset[0]
-        n_cond_static = cond.shape[0] if conditioning is not None else 0
-        n_cond_dynamic = t_cond.shape[0] if t_conditioning is not None else 0
-        n_cond_spatial = spatial_cond.shape[0] if spatial_conditioning is not None else 0
-        self._pde = PDE2D(tmin=tmin, tmax=tmax, nt=nt_out, L1=L1, L2=L2, nx1=nx1, nx2=nx2, x=x, name=name,
-                          n_cond_static=n_cond_static, n_cond_dynamic=n_cond_dynamic, n_cond_spatial=n_cond_spatial)
+    def _make_pde(self, name, conditioning, t_conditioning, spatial_conditioning) -> PDE2D:
+        """PDE2D metadata (PDE2D.py:73-89): the full time axis of the files (nt = tmax / dt + 1), the grid
+        extents x[-1,0,0] - x[0,0,0] and x[0,-1,1] - x[0,0,1], and the channel count of each
+        conditioning array that is in use (read from item 0)."""
+        ds = self.dataset
+        nt = int(ds.tmax / ds.dt) + 1
+        tmin, tmax = transforms.get_t_downsample(ds.tmin, ds.tmax, nt, ratio_nt=1)
+        x = ds.x
+        item = ds[0]
+        counts = [item[i].shape[0] if used is not None else 0
+                  for i, used in ((3, conditioning), (4, t_conditioning), (5, spatial_conditioning))]
+        return PDE2D(tmin=tmin, tmax=tmax, nt=nt, L1=x[-1, 0, 0] - x[0, 0, 0], L2=x[0, -1, 1] - x[0, 0, 1],
+                     nx1=x.shape[0], nx2=x.shape[1], x=x, name=name, n_cond_static=counts[0],
+                     n_cond_dynamic=counts[1], n_cond_spatial=counts[2])
 
     @property
     def pde(self):

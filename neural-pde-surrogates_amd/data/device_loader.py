@@ -27,15 +27,28 @@ def _base_and_indices(ds):
     return ds, idx
 
 
+def _draw_int64(generator):
+    return int(torch.empty((), dtype=torch.int64).random_(generator=generator).item())
+
+
 class DeviceLoader:
     """Iterable of batches (u_base, u, x, conditioning, t_conditioning, spatial_conditioning) on `device`,
     the default-collated layout of the reference's DataLoader over the same dataset.
 
-    shuffle: a fresh permutation per epoch from `generator` (torch.Generator) or torch's global RNG, as
-    RandomSampler.  prefetch: batches read / in flight ahead of the consumer."""
+    Sample order is the one torch's DataLoader would produce from the same RNG state, so a run driven by
+    this loader sees the reference's batches (trainers/base.py:169-179: DataLoader(shuffle=True)):
+      * single process: each epoch draws the iterator's base seed and then RandomSampler's seed from
+        `generator` (torch's global RNG when None), exactly as DataLoader + RandomSampler do, and permutes
+        with randperm on a generator seeded by the latter;
+      * num_replicas > 1 (one process per GPU): the samples of `rank` under DistributedSampler semantics
+         — a permutation seeded by `seed + epoch` (set_epoch), padded by wrapping (or cut
+        with drop_last) to a multiple of num_replicas, rank r taking positions r, r + R, ...; the shards
+        of one epoch are disjoint and cover the split once when its size divides by num_replicas.
+    prefetch: batches read / in flight ahead of the consumer."""
 
     def __init__(self, dataset, batch_size: int, shuffle: bool = False, drop_last: bool = False,
-                 device="cuda", prefetch: int = 2, generator: Optional[torch.Generator] = None):
+                 device="cuda", prefetch: int = 2, generator: Optional[torch.Generator] = None,
+                 num_replicas: int = 1, rank: int = 0, seed: int = 0):
         self.base, self.indices = _base_and_indices(dataset)
         self.batch_size = int(batch_size)
         self.shuffle = shuffle
@@ -43,16 +56,57 @@ class DeviceLoader:
         self.device = torch.device(device)
         self.prefetch = max(1, int(prefetch))
         self.generator = generator
+        if not (num_replicas >= 1 and 0 <= rank < num_replicas):
+            raise ValueError(f"invalid rank {rank} of {num_replicas} replicas")
+        self.num_replicas, self.rank, self.seed = int(num_replicas), int(rank), int(seed)
+        self.epoch = 0
+
+    def set_epoch(self, epoch: int):
+        """DistributedSampler.set_epoch: a different permutation per epoch, the same on every rank."""
+        self.epoch = int(epoch)
+
+    def _num_samples(self):
+        n, R = len(self.indices), self.num_replicas
+        if R == 1:
+            return n
+        # DistributedSampler: with drop_last the tail that does not fill every replica is cut
+        return (n - R) // R + 1 if (self.drop_last and n % R != 0) else -(-n // R)
 
     def __len__(self):
+        n = self._num_samples()
+        # drop_last of a sharded loader applies to the shard split (above), the batch split keeps the tail
+        if self.drop_last and self.num_replicas == 1:
+            return n // self.batch_size
+        return (n + self.batch_size - 1) // self.batch_size
+
+    def shard_positions(self):
+        """Positions (into this split) of the samples this rank visits this epoch, in visiting order.
+        Consumes RNG exactly as iterating a torch DataLoader over the same split does."""
         n = len(self.indices)
-        return n // self.batch_size if self.drop_last else (n + self.batch_size - 1) // self.batch_size
+        _draw_int64(self.generator)  # DataLoader iterator base seed (drawn even with num_workers=0)
+        if self.num_replicas == 1:
+            if not self.shuffle:
+                return torch.arange(n)
+            if self.generator is None:  # RandomSampler without a generator: a private one, freshly seeded
+                g = torch.Generator()
+                g.manual_seed(_draw_int64(None))
+            else:
+                g = self.generator
+            return torch.randperm(n, generator=g)
+        if self.shuffle:
+            g = torch.Generator()
+            g.manual_seed(self.seed + self.epoch)
+            order = torch.randperm(n, generator=g)
+        else:
+            order = torch.arange(n)
+        total = self._num_samples() * self.num_replicas
+        if total > n:
+            order = order.repeat(-(-total // n))  # wrap-around padding
+        order = order[:total]
+        return order[self.rank:total:self.num_replicas]
 
     def _batches(self):
-        order = self.indices
-        if self.shuffle:
-            perm = torch.randperm(len(order), generator=self.generator).numpy()
-            order = order[perm]
+        order = self.indices[self.shard_positions().numpy()]
         for i in range(len(self)):
             yield order[i * self.batch_size:(i + 1) * self.batch_size]
 

@@ -45,8 +45,32 @@ def precompute_and_save_memmap(memmap_in, filename, transform, dtype):
 
 
 
+# the optional arrays of a dataset directory: (key in self.data, position in the item tuple)
+_OPTIONAL = (("baseline", 0), ("conditioning", 3), ("t_conditioning", 4), ("spatial_conditioning", 5))
+
+
+def read_grid(config: dict, dtype) -> Tuple[torch.Tensor, list]:
+    """Grid of a <data_file>.yaml: a 1-D `x` list, or axes x1, x2, ... (each key present exactly once,
+    numbered from 1) combined into an (n1, n2, ..., ndim) coordinate tensor (meshgrid 'ij').
+    Returns (x, [per-axis coordinate tensors])."""
+    if "x" in config:
+        x = torch.tensor(config["x"], dtype=dtype)
+        return x, [x]
+    axes = sorted(int(k[1:]) for k in config if k.startswith("x") and k[1:].isdigit())
+    if axes != list(range(1, len(axes) + 1)):
+        raise ValueError(f"grid axes {['x' + str(a) for a in axes]} are not numbered 1..{len(axes)}")
+    if not axes:
+        raise ValueError("no grid (x or x1, x2, ...) in the dataset yaml")
+    coords = [torch.tensor(config[f"x{a}"], dtype=dtype) for a in axes]
+    if len(coords) == 1:
+        return coords[0], coords
+    return torch.stack(torch.meshgrid(*coords, indexing="ij"), dim=-1), coords
+
+
 class MemMapDataset(Dataset):
-    """memmap_dataset.py:78-305."""
+    """memmap_dataset.py:78-305: trajectories + optional baseline / conditioning arrays of one directory,
+    items (u_base, u, x, conditioning, t_conditioning, spatial_conditioning) with per-item transforms
+    (applied on access, or once up front into temporary memmaps with preprocess=True)."""
 
     def __init__(self, path: str, data_file: str, baseline_file: str = None, conditioning: str = None,
                  t_conditioning: str = None, spatial_conditioning: str = None, data_transform=None,
@@ -55,82 +79,58 @@ class MemMapDataset(Dataset):
                  raggedmemmap_batch_size: int = 128, dtype: torch.dtype = torch.float32, preprocess: bool = False,
                  preprocess_path: str = None, load_all: bool = False) -> None:
         super().__init__()
+        if data_format not in ("memmap", "raggedmemmap"):
+            raise AssertionError("data format must be memmap (numpy) or raggedmemmap (numpy+mmap_ninja)")
         self.dtype = dtype
-        assert data_format in ["memmap", "raggedmemmap"], \
-            "data format must be memmap (numpy) or raggedmemmap (numpy+mmap_ninja)"
         self.data_format = data_format
+        files = dict(baseline=baseline_file, conditioning=conditioning, t_conditioning=t_conditioning,
+                     spatial_conditioning=spatial_conditioning)
+        given = dict(data=data_transform, baseline=baseline_transform, conditioning=conditioning_transform,
+                     t_conditioning=t_conditioning_transform, spatial_conditioning=spatial_conditioning_transform)
+        # a transform only counts for an array that is in use
+        self.transforms = {k: (t if k == "data" or files[k] is not None else None) for k, t in given.items()}
         self.return_baseline = baseline_file is not None
         self.return_conditioning = conditioning is not None
         self.return_t_conditioning = t_conditioning is not None
         self.return_spatial_conditioning = spatial_conditioning is not None
-        self.data_transform = data_transform
+        self.data_transform = self.transforms["data"]
+        self.baseline_transform = self.transforms["baseline"]
+        self.conditioning_transform = self.transforms["conditioning"]
+        self.t_conditioning_transform = self.transforms["t_conditioning"]
+        self.spatial_conditioning_transform = self.transforms["spatial_conditioning"]
         self.grid_transform = grid_transform
-        self.baseline_transform = baseline_transform if self.return_baseline else None
-        self.conditioning_transform = conditioning_transform if self.return_conditioning else None
-        self.t_conditioning_transform = t_conditioning_transform if self.return_t_conditioning else None
-        self.spatial_conditioning_transform = spatial_conditioning_transform if self.return_spatial_conditioning \
-            else None
+
+        # preprocessing only pays when one of the trajectory / conditioning transforms exists (:152-156;
+        # a spatial-conditioning transform alone does not enable it)
+        if preprocess and all(self.transforms[k] is None for k in ("data", "baseline", "conditioning",
+                                                                    "t_conditioning")):
+            print("preprocess=True ignored: no transform to precompute")
+            preprocess = False
         self.preprocess = preprocess
-        if all(v is None for v in [self.data_transform, self.baseline_transform, self.conditioning_transform,
-                                   self.t_conditioning_transform]):  # :152-156
-            if self.preprocess:
-                print("Overriding preprocess to False, since no transforms were specified")
-                self.preprocess = False
-        if self.preprocess:
-            self.preprocess_dir = preprocess_path if preprocess_path is not None else os.path.join(path, "tmp")
+        self.preprocess_dir = (preprocess_path or os.path.join(path, "tmp")) if preprocess else None
+        if preprocess:
             os.makedirs(self.preprocess_dir, exist_ok=True)
-        else:
-            self.preprocess_dir = None
 
-        self.data = {"data": load_data(self.data_format, path, data_file)}
-        for key, name, on in (("baseline", baseline_file, self.return_baseline),
-                              ("conditioning", conditioning, self.return_conditioning),
-                              ("t_conditioning", t_conditioning, self.return_t_conditioning),
-                              ("spatial_conditioning", spatial_conditioning, self.return_spatial_conditioning)):
-            if on:
-                self.data[key] = load_data(self.data_format, path, name)
+        self.data = {"data": load_data(data_format, path, data_file)}
+        self.data.update({k: load_data(data_format, path, f) for k, f in files.items() if f is not None})
 
-        self.config = load_yaml(os.path.join(path, data_file + ".yaml"))  # :178-200
-        if "x" in self.config:
-            self.x = torch.tensor(self.config["x"], dtype=self.dtype)
-            self.x_all = [self.x]
-        else:
-            x_keys = [k for k in self.config if k.startswith("x")]
-            x_keys = [int(k[1:]) for k in x_keys if str.isdigit(k[1:])]
-            if set(range(1, len(x_keys) + 1)) != set(x_keys):
-                raise ValueError(f"Found grid keys {['x' + str(k) for k in x_keys]}, "
-                                 f"expected keys {['x' + str(k) for k in range(1, len(x_keys) + 1)]}")
-            if len(x_keys) == 0:
-                raise ValueError(f"Could not find a grid in {data_file}.yaml")
-            x_keys = sorted("x" + str(k) for k in x_keys)
-            self.x_all = [torch.tensor(self.config[k], dtype=self.dtype) for k in x_keys]
-            if len(self.x_all) == 1:
-                self.x = self.x_all[0]
-            else:
-                self.x = torch.movedim(torch.stack(torch.meshgrid(*self.x_all, indexing="ij")), 0, -1)
-        self.tmin = self.config["tmin"]
-        self.tmax = self.config["tmax"]
-        self.dt = self.config["dt"]
-        if self.grid_transform is not None:
-            self.x = self.grid_transform(self.x)
+        self.config = load_yaml(os.path.join(path, data_file + ".yaml"))
+        self.x, self.x_all = read_grid(self.config, self.dtype)
+        self.tmin, self.tmax, self.dt = self.config["tmin"], self.config["tmax"], self.config["dt"]
+        if grid_transform is not None:  # the grid is shared by every item: transformed once
+            self.x = grid_transform(self.x)
 
-        if self.preprocess:  # :205-226 (memmap)
+        if preprocess:
             self.preprocess_output = {}
-            for data_name, on, transform in (("data", True, self.data_transform),
-                                             ("baseline", self.return_baseline, self.baseline_transform),
-                                             ("conditioning", self.return_conditioning, self.conditioning_transform),
-                                             ("t_conditioning", self.return_t_conditioning,
-                                              self.t_conditioning_transform),
-                                             ("spatial_conditioning", self.return_spatial_conditioning,
-                                              self.spatial_conditioning_transform)):
-                if not on or transform is None:
+            for key, t in self.transforms.items():
+                if t is None or key not in self.data:
                     continue
-                fname = os.path.join(self.preprocess_dir, f"{data_name}_{os.getpid()}_{id(self)}.npy")
-                self.data[data_name] = precompute_and_save_memmap(self.data[data_name], fname, transform, self.dtype)
-                self.preprocess_output[data_name] = fname
+                fname = os.path.join(self.preprocess_dir, f"{key}_{os.getpid()}_{id(self)}.npy")
+                self.data[key] = precompute_and_save_memmap(self.data[key], fname, t, self.dtype)
+                self.preprocess_output[key] = fname
             self._finalizer = weakref.finalize(self, MemMapDataset._delete_files, dict(self.preprocess_output))
 
-        if load_all:  # :228-231
+        if load_all:
             self.data = {k: np.asarray(v[:]) for k, v in self.data.items()}
 
     @staticmethod

@@ -1,15 +1,23 @@
-"""The one transform helper the 2-D dataset path uses (reference data/transforms.py:135-147)."""
+"""Time-axis resampling helper of the 2-D dataset path (reference data/transforms.py:135-147)."""
 
 
 def get_t_downsample(tmin, tmax, nt_in, nt_out=None, ratio_nt=None):
-    tdelta = tmax - tmin
-    range_old = [tmin + (x / (nt_in - 1) * tdelta) for x in range(0, nt_in)]
-    if nt_out is None and ratio_nt is None:
-        raise ValueError("Either nt_out or ratio_nt must be specified")
-    elif ratio_nt is None:
+    """(first, last) time of a uniform nt_in-point time axis on [tmin, tmax] kept every `ratio_nt`-th point
+    (ratio_nt = nt_in / nt_out when only nt_out is given; it must be integral).  Point i of the axis is
+    tmin + (i / (nt_in - 1)) * (tmax - tmin), evaluated in that order so the floats equal the
+    reference's."""
+    if ratio_nt is None:
+        if nt_out is None:
+            raise ValueError("Either nt_out or ratio_nt must be specified")
         ratio_nt = nt_in / nt_out
     if not isinstance(ratio_nt, int):
-        assert ratio_nt.is_integer()
+        if not float(ratio_nt).is_integer():
+            raise AssertionError(f"time downsampling ratio {ratio_nt} is not an integer")
         ratio_nt = int(ratio_nt)
-    range_new = range_old[::ratio_nt]
-    return range_new[0], range_new[-1]
+    span = tmax - tmin
+    last = ((nt_in - 1) // ratio_nt) * ratio_nt  # index of the last kept point
+
+    def t_at(i):
+        return tmin + (i / (nt_in - 1) * span)
+
+    return t_at(0), t_at(last)

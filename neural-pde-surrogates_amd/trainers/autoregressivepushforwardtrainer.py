@@ -1,4 +1,5 @@
-"""Autoregressive rollout driver (reference trainers/autoregressivepushforwardtrainer.py).
+"""Autoregressive rollout driver (reference trainers/autoregressivepushforwardtrainer.py) on TrainInterface
+(trainers/base.py: train / test / checkpointing, the train.py surface).
 
 `simulate` keeps the reference's signature, loop bounds (:354-358), loss
 normalisation (:422, :433-434) and return conventions, with the trajectory
@@ -21,6 +22,7 @@ from torch import nn
 from common.interfaces import D, M
 from nps_hip import ops
 from nps_hip import autograd as ad
+from trainers.base import TrainInterface
 
 
 class DataCreator:
@@ -65,46 +67,20 @@ class DataCreator:
         return data, labels
 
 
-class AutoregressivePushforwardTrainer:
+class AutoregressivePushforwardTrainer(TrainInterface):
     data_interface = [D.sim1d, D.sim2d, D.sim1d_var_t]
     model_interface = [M.AR_TB, M.AR_TB_GNN]
 
     def __init__(self, model, data, criterion, optimizer=None, lr_scheduler=None, config: argparse.Namespace = None,
-                 save_path: str = "models/model.pt", max_train_batches=float("inf"), epoch_callback=None,
-                 grad_sync=None, **kwargs):
-        self.model = model
-        self.max_train_batches = max_train_batches
-        self.epoch_callback = epoch_callback
-        self.grad_sync = grad_sync
-        self.data = data
-        self.config = config if config is not None else argparse.Namespace(**kwargs)
-        self.config.save_path = save_path
-        self.criterion = criterion
-        self.optimizer = optimizer
-        self.lr_scheduler = lr_scheduler
+                 save_path: str = "models/model.pt", **kwargs):
+        super().__init__(model=model, data=data, criterion=criterion, optimizer=optimizer, lr_scheduler=lr_scheduler,
+                         config=config, save_path=save_path, **kwargs)
         if not hasattr(self.config, "process_settings"):
             self.config.process_settings = {}
         self.data_creator = DataCreator(pde=self.data.pde, neighbors=getattr(self.config, "neighbors", 3),
                                         time_window=self.config.time_window,
                                         t_resolution=self.config.base_resolution[0],
                                         x_resolution=self.config.base_resolution[1])
-
-    def get_dataloaders(self):
-        """trainers/base.py:157-179 (fixed-length time): train / valid / test loaders over the dataset's
-        splits.  On a GPU device the loaders are device-resident (data.DeviceLoader: batches read from the
-        memmaps, pinned and copied on a side HIP stream ahead of use); on the CPU they are the reference's
-        DataLoader(shuffle=True)."""
-        if getattr(self.config, "variable_time", False):
-            raise NotImplementedError("variable-length time (sim1d_var_t) is not on the grid path")
-        device = torch.device(self.config.device)
-        bs = self.config.batch_size
-        if device.type == "cuda":
-            from data.device_loader import DeviceLoader
-            return tuple(DeviceLoader(d, bs, shuffle=True, device=device)
-                         for d in (self.data.train, self.data.valid, self.data.test))
-        from torch.utils.data import DataLoader
-        return tuple(DataLoader(d, batch_size=bs, shuffle=True, num_workers=getattr(self.config, "nw", 0))
-                     for d in (self.data.train, self.data.valid, self.data.test))
 
     def _loss(self, pred, labels):
         c = self.criterion
@@ -158,31 +134,6 @@ class AutoregressivePushforwardTrainer:
                           spatial_cond=spatial_conditioning)
         loss = self._train_loss(pred, labels)
         return loss, pred
-
-    def train_one_epoch(self, loader, epoch) -> float:
-        """trainers/base.py:472-507: zero_grad -> train_step -> backward -> [RCCL all-reduce] -> step."""
-        self.model.train()
-        device = self.config.device
-        total_loss = 0
-        n = 0
-        for batch_idx, batch in enumerate(loader):
-            batch_on_device = tuple(t.to(device) if isinstance(t, torch.Tensor) else t for t in batch)
-            self.optimizer.zero_grad()
-            loss, preds = self.train_step(batch_on_device, epoch, batch_idx, loader=loader)
-            loss.backward()
-            if self.grad_sync is not None:
-                self.grad_sync.finish()
-            self.optimizer.step()
-            total_loss += loss.detach() / batch_on_device[0].shape[0]
-            n += 1
-            if batch_idx >= self.max_train_batches:
-                break
-        total_loss = total_loss / max(1, n)
-        if self.epoch_callback is not None:
-            self.epoch_callback(self, loader, epoch)
-        if self.lr_scheduler is not None and (epoch + 1) % self.config.lr_step_interval == 0:
-            self.lr_scheduler.step()
-        return total_loss
 
     def simulate(self, u, conditioning, x, compute_loss, include_data, nr_gt_steps, t_res,
                  t_conditioning=torch.empty(0), spatial_conditioning=torch.empty(0), clip_min=True, use_bc=True,
@@ -244,3 +195,75 @@ class AutoregressivePushforwardTrainer:
             return data_pred
         else:
             return losses, (data_gt, data_pred)
+
+    def test_step(self, batch: Tuple, batch_idx: int, use_train_loss_calc=False, include_data=False,
+                  max_test_len=None):
+        """autoregressivepushforwardtrainer.py:165-286 (grid models, fixed-length time): one-step losses of
+        every window (ground-truth input), then the full rollout.  Returns (mean unrolled loss, metrics
+        {'Unrolled base losses', 'Unrolled forward losses', 'Mean per-step loss', 'Step s, mean loss'...}
+        [, (gt, pred, per-sample info)])."""
+        if use_train_loss_calc:
+            raise RuntimeError("We should probably not have use_train_loss=True when having implemented the "
+                               "test_step method...")
+        if self.data.data_interface == D.sim1d_var_t:
+            raise NotImplementedError("variable-length time (sim1d_var_t) is not on the grid path")
+        if self.model.model_interface != M.AR_TB:
+            raise NotImplementedError("graph (GNN) models are not on the MI355X path")
+        u_base, u_super, x, conditioning, t_conditioning, spatial_conditioning = batch
+        t_res = self.data_creator.t_res
+        tw = self.data_creator.tw
+        device = self.config.device
+        B = u_super.shape[0]
+        use_t = torch.numel(t_conditioning) != 0
+        per_step, per_step_named = [], {}
+        for step in range(tw, t_res - tw + 1, tw):
+            same = [step] * B
+            data, labels = self.data_creator.create_data(u_super, same)
+            t_cond = self.data_creator.create_data(t_conditioning, same, mode="labels") if use_t else None
+            pred = self.model(data.to(device), cond=conditioning, bc=None, pos=x, t_cond=t_cond,
+                              spatial_cond=spatial_conditioning)
+            loss = self._loss(pred, labels.to(device)).float() / B
+            per_step.append(loss)
+            per_step_named[f"Step {step}, mean loss"] = loss
+        per_step = torch.stack(per_step)
+        out = self._test_unrolled_losses(batch, include_data, max_test_len, divide_by_t=True)
+        metrics = {"Unrolled base losses": out[1], "Unrolled forward losses": out[0],
+                   "Mean per-step loss": torch.mean(per_step), **per_step_named}
+        if include_data:
+            return torch.mean(out[0]), metrics, out[2]
+        return torch.mean(out[0]), metrics
+
+    def _test_unrolled_losses(self, batch, include_data=False, max_test_len=None, divide_by_t=True):
+        """autoregressivepushforwardtrainer.py:442-514: the summed per-window rollout loss of `simulate`
+        (from nr_gt_steps ground-truth windows) and the numerical baseline's loss against the
+        high-resolution solution (0 when the dataset has no baseline)."""
+        if self.data.data_interface == D.sim1d_var_t:
+            raise NotImplementedError("variable-length time (sim1d_var_t) is not on the grid path")
+        u_base, u_super, x, conditioning, t_conditioning, spatial_conditioning = batch
+        t_res = self.data_creator.t_res
+        tw = self.data_creator.tw
+        nr_gt = self.config.nr_gt_steps
+        res = self.simulate(u_super, conditioning, x, t_conditioning=t_conditioning,
+                            spatial_conditioning=spatial_conditioning, compute_loss=True, include_data=include_data,
+                            nr_gt_steps=nr_gt, t_res=t_res, u_mask=None, divide_by_t=divide_by_t)
+        losses, sims = (res[0], res[1]) if include_data else (res, None)
+        B = u_super.shape[0]
+        spatial = math.prod(self.config.base_resolution[1:])
+        base, n_t = [], 0
+        for step in range(tw * nr_gt, t_res - tw + 1, tw):
+            if torch.numel(u_base) == 0:
+                base.append(torch.zeros(0))  # no baseline solver data: contributes nothing
+                continue
+            same = [step] * B
+            _, lab_super = self.data_creator.create_data(u_super, same)
+            _, lab_base = self.data_creator.create_data(u_base, same)
+            base.append(self._loss(lab_super, lab_base).float() / spatial / B)
+            n_t += tw
+        base_loss = torch.sum(torch.cat([b.reshape(-1).cpu() for b in base]))
+        if divide_by_t:
+            base_loss = base_loss / (n_t if n_t > 0 else 1)
+        unrolled = torch.sum(torch.stack(losses))  # divide_by_t already applied by simulate
+        if not include_data:
+            return unrolled, base_loss
+        gt, pred = torch.cat(sims[0], dim=2), torch.cat(sims[1], dim=2)
+        return unrolled, base_loss, [gt, pred, [{} for _ in range(B)]]

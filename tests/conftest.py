@@ -21,10 +21,20 @@ def load_golden(name):
     return torch.load(os.path.join(GOLDEN, f"{name}.pt"), weights_only=True)
 
 
+def _as_f64(t):
+    """fp64 CPU copy; complex tensors are compared through their (re, im) pairs, so both parts count."""
+    import torch
+    t = t.detach().cpu()
+    if t.is_complex():
+        t = torch.view_as_real(t.resolve_conj())
+    return t.to(torch.float64)
+
+
 def rel_l2(a, b):
     import torch
-    a = a.detach().to("cpu", torch.float64)
-    b = b.detach().to("cpu", torch.float64)
+    a, b = _as_f64(a), _as_f64(b)
+    if a.shape != b.shape:
+        raise AssertionError(f"rel_l2: shape mismatch {tuple(a.shape)} vs {tuple(b.shape)}")
     return (torch.linalg.vector_norm(a - b) / torch.linalg.vector_norm(b)).item()
 
 

@@ -84,3 +84,110 @@ def test_grad_allreduce_matches_full_batch(bucket_bytes, overlap):
             assert nb > 1
         for k in want:
             torch.testing.assert_close(got[k], want[k], rtol=1e-6, atol=1e-6)
+
+
+# ----------------------------------------------------------------- model-shaped all-reduce, shards, bench
+class _ModelShaped(torch.nn.Module):
+    """The U-FNO block's parameter shapes: SpectralConv2d weights1/weights2 complex (196, 192, 10, 10), a
+    3x3 conv (192, 196, 3, 3) + bias, a GroupNorm affine pair and a 1x1 conv (278 MB of
+    gradients for the full model, reduced as real pairs in several buckets)."""
+
+    def __init__(self):
+        super().__init__()
+        g = torch.Generator().manual_seed(0)
+        s = 1.0 / (196 * 192)
+        self.w1 = torch.nn.Parameter(s * torch.rand(196, 192, 10, 10, dtype=torch.cfloat, generator=g))
+        self.w2 = torch.nn.Parameter(s * torch.rand(196, 192, 10, 10, dtype=torch.cfloat, generator=g))
+        self.conv = torch.nn.Parameter(0.02 * torch.randn(192, 196, 3, 3, generator=g))
+        self.bias = torch.nn.Parameter(0.1 * torch.randn(192, generator=g))
+        self.gamma = torch.nn.Parameter(1 + 0.1 * torch.randn(196, generator=g))
+        self.beta = torch.nn.Parameter(0.1 * torch.randn(196, generator=g))
+        self.pw = torch.nn.Parameter(0.05 * torch.randn(192, 196, generator=g))
+
+    def forward(self, x):  # x (B, 196, 20, 20): a spectral-style contraction + a conv + a pointwise map
+        xf = torch.fft.rfft2(x)[:, :, :10, :10]
+        y = torch.einsum("bixy,ioxy->boxy", xf, self.w1) + torch.einsum("bixy,ioxy->boxy", xf.conj(), self.w2)
+        h = torch.nn.functional.group_norm(x, 1, self.gamma, self.beta)
+        c = torch.nn.functional.conv2d(h, self.conv, self.bias)
+        p = torch.einsum("oi,bixy->boxy", self.pw, x)
+        return (y.abs() ** 2).sum() + (c ** 2).mean() + p.square().mean()
+
+
+def _model_worker(rank, world, port, q, done):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "neural-pde-surrogates_amd"), os.path.join(root, "tests")]
+    from trainers.distributed import GradAllReducer
+    import bench
+    torch.set_num_threads(2)
+    m = _ModelShaped()
+    sync = GradAllReducer(m.parameters(), bucket_bytes=16 * 1024 * 1024)
+    sync.broadcast_parameters(0)
+    x = torch.randn(4, 196, 20, 20, generator=torch.Generator().manual_seed(1))
+    lo, hi = bench.shard_bounds(4, world, rank)
+    m.zero_grad()
+    m(x[lo:hi]).backward()
+    sync.finish()
+    grads = {k: p.grad.clone() for k, p in m.named_parameters()}
+    # data shards of a DeviceLoader over an on-disk split (DistributedSampler semantics)
+    from data_fixture import write_twophase_dataset, DATASET_KW
+    from data import PDE2DDataset, DeviceLoader
+    import tempfile
+    d = tempfile.mkdtemp() if rank == 0 else None
+    obj = [d]
+    dist.broadcast_object_list(obj, src=0)
+    if rank == 0:
+        write_twophase_dataset(obj[0], shape=(10, 8, 11, 8, 6), with_split=False)
+    dist.barrier()
+    ds = PDE2DDataset(base_path=obj[0], **dict(DATASET_KW, split_file=None, split_val=0.0, split_test=0.0))
+    dl = DeviceLoader(ds.test, batch_size=2, shuffle=True, device="cpu", num_replicas=world, rank=rank)
+    shards = {}
+    for epoch in (0, 1):
+        dl.set_epoch(epoch)
+        seen = [int(i) for b in dl for i in b[1].flatten(1).sum(1).mul(1e4).round().tolist()]
+        allseen = [None] * world
+        dist.all_gather_object(allseen, seen)
+        shards[epoch] = allseen
+    elapsed = bench.max_over_ranks(1.0 + rank, torch.device("cpu"))
+    q.put((rank, grads, len(sync.buckets), (lo, hi), shards, elapsed))
+    done.wait(timeout=120)  # keep the tensors' shared memory alive until the parent has received them
+    dist.destroy_process_group()
+
+
+def test_model_shaped_allreduce_shards_and_bench_reduction():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    done = ctx.Event()
+    port = _free_port()
+    procs = [ctx.Process(target=_model_worker, args=(r, world, port, q, done)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=150) for _ in range(world)], key=lambda r: r[0])
+    done.set()
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    m = _ModelShaped()
+    x = torch.randn(4, 196, 20, 20, generator=torch.Generator().manual_seed(1))
+    m.zero_grad()
+    (m(x[:2]) + m(x[2:])).div(2).backward()  # 1-process gradient of the mean of the two shard losses
+    want = {k: p.grad for k, p in m.named_parameters()}
+    for rank, grads, nb, (lo, hi), shards, elapsed in res:
+        assert nb >= 3  # 60 MB of complex weights + the rest in 16 MB buckets
+        assert (lo, hi) == (2 * rank, 2 * rank + 2)
+        assert elapsed == 2.0  # the slowest rank's time on every rank
+        for k in want:
+            torch.testing.assert_close(grads[k], want[k], rtol=1e-5, atol=1e-7)
+    # every epoch: the ranks' shards are disjoint and cover the 10-sample split exactly once
+    shards = res[0][4]
+    ds_ids = None
+    for epoch, per_rank in shards.items():
+        allids = sorted(per_rank[0] + per_rank[1])
+        assert len(per_rank[0]) == len(per_rank[1]) == 5
+        assert len(set(allids)) == 10
+        ds_ids = allids if ds_ids is None else ds_ids
+        assert allids == ds_ids
+    assert shards[0][0] != shards[1][0]  # set_epoch reshuffles
