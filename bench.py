@@ -301,7 +301,7 @@ def run_train(args):
         sync.broadcast_parameters(0)
     u, cond, pos, sc = twophase_batch(B, args.num_c, 2 * tw, args.res, args.res, seed=1234 + rank,
                                       obstacle="disc", device=dev)
-    batch = (u[:, :, :1], u, pos, cond, torch.empty(0, device=dev), sc)
+    batch = (u[:, :, :1], u, pos, cond, torch.empty(B, 0, device=dev), sc)  # collated layout (B, 0)
     cfg = types.SimpleNamespace(time_window=tw, base_resolution=(2 * tw, args.res, args.res), device=dev,
                                 batch_size=B, lr_step_interval=25, unrolling=0)
     opt = torch.optim.Adam(model.parameters(), lr=1e-4)

@@ -88,11 +88,28 @@ typedef struct {
      * nps_conv2d_x3_eligible() and nps_conv2d_x3_sources_ok(), with the weight packed by
      * nps_conv2d_pack_weights_x3 */
     int precision;
-    /* NPS_PREC_X3F16 only: device pointer to max|input| (nps_absmax) or NULL; the input is scaled by an
-     * exact power of 2 into fp16's normal range before the split and the result scaled back
-     * (used for gradients, whose magnitude is arbitrary) */
+    /* Input range of a NPS_PREC_X3F16 conv.  The input is scaled by an exact power of 2 (max|x| into
+     * [2^13, 2^14)) before the fp16 split and the result scaled back, so values of any magnitude keep
+     * fp32-class accuracy (|x| >= max|x| * 2^-16 keep 22 bits; smaller ones an absolute error below
+     * max|x| * 2^-37).  Each pointer is NULL or a RANGE TAG (NPS_TAG_FLOATS floats: NPS_TAG_SUB
+     * sub-slots NPS_TAG_STRIDE floats apart, the tag's value is their max) holding an upper bound of
+     * |x| over the source(s) it covers; the conv uses the max of the non-NULL tags, and scale 1 when
+     * all three are NULL.  in_scale: set explicitly (nps_absmax of a gradient) or the tag of source 0;
+     * in_tag1 / in_tag2: the tags of sources 1 / 2. */
     const float* in_scale;
+    const float* in_tag1;
+    const float* in_tag2;
+    /* Range tag of the output (any precision, NULL = none): the conv raises it (atomic max of the
+     * non-negative float bits, one sub-slot per wave) to >= max |value| of every element it writes.
+     * Zero it before the first writer (tags are allocated from a zeroed arena, see ops.py). */
+    float* out_tag;
 } nps_conv2d_t;
+
+/* Range tags (nps_conv2d_t.in_scale / in_tag* / out_tag): 64 sub-slots 256 B apart, so the atomics of
+ * thousands of work-groups spread over 64 addresses; readers take the max over the sub-slots. */
+#define NPS_TAG_SUB 64
+#define NPS_TAG_STRIDE 64
+#define NPS_TAG_FLOATS (NPS_TAG_SUB * NPS_TAG_STRIDE)
 
 #define NPS_PREC_F32 0
 #define NPS_PREC_X3F16 1
@@ -125,8 +142,9 @@ int nps_conv2d_x3_prologue_ok(int KH, int KW, int Cin, int gn_groups, int pre_ac
 /* 1 when the split-fp16 kernel can stage this virtual frame directly: every source boundary on a
  * multiple of 16 channels, every source's C a multiple of 4 (otherwise nps_frame_pack it first). */
 int nps_conv2d_x3_sources_ok(const nps_src_t* src, int nsrc);
-/* *out = max |x[i]| (the input range a split-fp16 conv scales by, nps_conv2d_t.in_scale) */
-int nps_absmax(const float* x, long n, float* out, void* stream);
+/* Range tag `tag` (NPS_TAG_FLOATS floats) := max |x[i]| (zeroed, then raised) — the input range a
+ * split-fp16 conv scales by (nps_conv2d_t.in_scale / in_tag*). */
+int nps_absmax(const float* x, long n, float* tag, void* stream);
 /* Stride-2 3x3 convs (U-Net Downsample, proc_unet_modern.py:445-455) run as 2x2 stride-1 convs
  * over a space-to-depth copy: out[B][Hq][Wq][4C], channel (dy*2+dx)*C + c = x[2y+dy-pad][2x+dx-pad][c]
  * (zero outside); pack the weight with transposed_phase = -2 (Cin = 4C). */
@@ -169,9 +187,10 @@ int nps_spectral_pack_weights(const float* w1, const float* w2, float* wpack, in
 int nps_spectral_mix(const float* X2, const float* wpack, float* Y, int B, int R, int m2, int Cin, int Cout,
                      void* stream);
 int nps_spectral_idft_h(const float* Y, float* Z, int B, int H, int m1, int m2, int Cout, void* stream);
-/* out[B][H][W][Cout] (= or +=) y ; optional addend, act as in nps_conv2d_t */
+/* out[B][H][W][Cout] (= or +=) y ; optional addend, act as in nps_conv2d_t; out_tag (or NULL): the
+ * output's range tag, raised to cover every value written (nps_conv2d_t.out_tag) */
 int nps_spectral_idft_w(const float* Z, float* out, int B, int H, int W, int m2, int Cout, int accumulate,
-                        const float* addend, int act, void* stream);
+                        const float* addend, int act, float* out_tag, void* stream);
 
 /* ---- grid encoder / decoder / wrapper ---------------------------------
  * Encoder input packing, enc_grid.py:41-50 + enc_proc_dec.py:127-137:

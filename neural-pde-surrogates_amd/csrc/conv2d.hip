@@ -196,6 +196,7 @@ __global__ __launch_bounds__(WAVES * 64) void conv2d_fwd_kernel(const nps_conv2d
 
     // ---------------- epilogue ----------------
     const int h = lane >> 5;
+    float amax = 0.f;
 #pragma unroll
     for (int pb = 0; pb < 2; ++pb) {
         const int P = wave * 64 + pb * 32 + (lane & 31);
@@ -205,8 +206,9 @@ __global__ __launch_bounds__(WAVES * 64) void conv2d_fwd_kernel(const nps_conv2d
         const int dy = oy * a.out_os + a.out_off_y, dx = ox * a.out_os + a.out_off_x;
         if (dy < 0 || dy >= a.out_H || dx < 0 || dx >= a.out_W) continue;
 #pragma unroll
-        for (int cb = 0; cb < 2; ++cb) store_tile(a, b, cob * 64 + cb * 32, h, acc[cb][pb], dy, dx);
+        for (int cb = 0; cb < 2; ++cb) store_tile(a, b, cob * 64 + cb * 32, h, acc[cb][pb], dy, dx, amax);
     }
+    nps::tag_publish(a.out_tag, amax, nps::wave_salt());
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -427,6 +429,7 @@ __global__ __launch_bounds__(512) void conv2d_pc_kernel(const nps_conv2d_t a) {
 
     // epilogue
     const int h = lane >> 5;
+    float amax = 0.f;
 #pragma unroll
     for (int pb = 0; pb < PB; ++pb) {
         const int P = wpx * 32 * PB + pb * 32 + (lane & 31);
@@ -437,10 +440,11 @@ __global__ __launch_bounds__(512) void conv2d_pc_kernel(const nps_conv2d_t a) {
         if (dy < 0 || dy >= a.out_H || dx < 0 || dx >= a.out_W) continue;
 #pragma unroll
         for (int cb = 0; cb < CBW; ++cb) {
-            store_tile(a, b, (cob * NCBG + wco * CBW + cb) * 32, h, acc[cb][pb], dy, dx);
+            store_tile(a, b, (cob * NCBG + wco * CBW + cb) * 32, h, acc[cb][pb], dy, dx, amax);
             __builtin_amdgcn_sched_barrier(0);  // keep each tile's epilogue loads local (register pressure)
         }
     }
+    nps::tag_publish(a.out_tag, amax, nps::wave_salt());
 }
 
 // Weight element (co, ci, tap) of the conv being packed, from w in the layout the mode implies.
@@ -484,7 +488,7 @@ __global__ void pack_weights_kernel(const float* __restrict__ w, float* __restri
 
 // Packed layout (3-pass split fp16, same bytes): [chunk][tap][cb][hl (2)][lane (64)][8 halves]
 // element j of lane = (hi | lo) of s * w[co = cb*32 + (lane&31)][ci = chunk*16 + (lane>>5)*8 + j][tap],
-// s = pow2_scale_for(max|w|) (max|w| is in the buffer's trailer, written by nps_absmax beforehand)
+// s = pow2_scale_for(max|w|) (max|w| is in the buffer's trailer, written by nps_absmax_scalar beforehand)
 __global__ void pack_weights_x3_kernel(const float* __restrict__ w, _Float16* __restrict__ wp, int Cout, int Cin,
                                        int KH, int KW, int tphase, size_t total_pairs, const float* __restrict__ wmax) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // (hi, lo) pair index
@@ -583,7 +587,7 @@ extern "C" int nps_conv2d_pack_weights_x3(const float* w, float* wpack, int Cout
     float* wmax = wpack + pairs;                             // trailer[0]
     const long nw = transposed_phase == -1 ? (long)Cout * Cin * KH * KW
                                            : (transposed_phase == -2 ? (long)Cout * (Cin / 4) * 9 : (long)Cout * Cin * 16);
-    if (nps_absmax(w, nw, wmax, stream) != 0) return -2;
+    if (nps_absmax_scalar(w, nw, wmax, (hipStream_t)stream) != 0) return -2;
     const int bs = 256;
     pack_weights_x3_kernel<<<(unsigned)((pairs + bs - 1) / bs), bs, 0, (hipStream_t)stream>>>(
         w, reinterpret_cast<_Float16*>(wpack), Cout, Cin, KH, KW, transposed_phase, pairs, wmax);
@@ -958,10 +962,14 @@ __global__ void frame_pack_kernel(nps_conv2d_t a, float* __restrict__ out) {
         const int n = a.Hin * a.Win * C4;
         const f32x4* src = reinterpret_cast<const f32x4*>(S0.ptr + (size_t)b * a.Hin * a.Win * a.Cin);
         f32x4* dst = reinterpret_cast<f32x4*>(out + (size_t)b * a.Hin * a.Win * a.Cin);
+        float amax = 0.f;
         for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
             const int c = (i % C4) * 4;
-            dst[i] = prologue4(a, tab, cpg, c, src[i]);
+            const f32x4 r = prologue4(a, tab, cpg, c, src[i]);
+            dst[i] = r;
+            amax = fmaxf(amax, fmaxf(fmaxf(fabsf(r[0]), fabsf(r[1])), fmaxf(fabsf(r[2]), fabsf(r[3]))));
         }
+        nps::tag_publish(a.out_tag, amax, nps::wave_salt());
         return;
     }
     // output channel stride oC >= Cin (a.out_C; channels [Cin, oC) are written as zeros)
@@ -975,6 +983,7 @@ __global__ void frame_pack_kernel(nps_conv2d_t a, float* __restrict__ out) {
         // used (the branchy per-quad gather leaves one 16-B load in flight per thread)
         constexpr int U = 4;
         const int lo1 = S0.C, lo2 = S0.C + (a.nsrc > 1 ? S1.C : 0);
+        float amax = 0.f;
         for (int i0 = blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += stride * U) {
             f32x4 v[U];
             int cq[U], pq[U];
@@ -1007,13 +1016,17 @@ __global__ void frame_pack_kernel(nps_conv2d_t a, float* __restrict__ out) {
                 f32x4 r = v[u];
                 if (cq[u] < a.Cin) r = prologue4(a, tab, cpg, cq[u], r);  // zero padding is normalised too
 #pragma unroll
-                for (int e = 0; e < 4; ++e)
+                for (int e = 0; e < 4; ++e) {
                     if (cq[u] + e >= a.Cin) r[e] = 0.f;
+                    amax = fmaxf(amax, fabsf(r[e]));
+                }
                 *reinterpret_cast<f32x4*>(out + ((size_t)b * a.Hin * a.Win + pq[u]) * oC + cq[u]) = r;
             }
         }
+        nps::tag_publish(a.out_tag, amax, nps::wave_salt());
         return;
     }
+    float amax = 0.f;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const int pix = i / C4;
         const int c = (i - pix * C4) * 4;
@@ -1021,8 +1034,10 @@ __global__ void frame_pack_kernel(nps_conv2d_t a, float* __restrict__ out) {
         f32x4 v = {0.f, 0.f, 0.f, 0.f};
         if (c < a.Cin) v = prologue4(a, tab, cpg, c, fetch4(a, b, y, x, c));
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
+        for (int e = 0; e < 4; ++e) {
             if (c + e >= a.Cin) v[e] = 0.f;
+            amax = fmaxf(amax, fabsf(v[e]));
+        }
         float* dst = out + ((size_t)(b * a.Hin + y) * a.Win + x) * oC + c;
         if ((oC & 3) == 0) {
             *reinterpret_cast<f32x4*>(dst) = v;
@@ -1032,6 +1047,7 @@ __global__ void frame_pack_kernel(nps_conv2d_t a, float* __restrict__ out) {
                 if (c + e < oC) dst[e] = v[e];
         }
     }
+    nps::tag_publish(a.out_tag, amax, nps::wave_salt());
 }
 }  // namespace
 
@@ -1056,26 +1072,53 @@ extern "C" int nps_frame_pack(const nps_conv2d_t* ap, float* out, void* stream) 
 
 // ------------------------------------------------------------------ absmax (input range of split-fp16 convs)
 namespace {
-__global__ void absmax_kernel(const float* __restrict__ x, long n, unsigned int* __restrict__ out) {
+__global__ void absmax_kernel(const float* __restrict__ x, long n, float* __restrict__ tag) {
+    float m = 0.f;
+    const long n4 = ((reinterpret_cast<size_t>(x) & 15) == 0) ? n >> 2 : 0;  // 16-B loads when aligned
+    const long stride = (long)gridDim.x * blockDim.x;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+        const f32x4 v = reinterpret_cast<const f32x4*>(x)[i];
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+    }
+    for (long i = n4 * 4 + (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) m = fmaxf(m, fabsf(x[i]));
+    nps::tag_publish(tag, m, nps::wave_salt());
+}
+
+// plain scalar max|x| into *out (one float; the packed-weight trailer): single-address atomics, used once
+// per parameter version
+__global__ void absmax_scalar_kernel(const float* __restrict__ x, long n, unsigned int* __restrict__ out) {
     float m = 0.f;
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
         m = fmaxf(m, fabsf(x[i]));
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-    if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));  // non-negative floats order as uints
+    m = nps::wave_max(m);
+    if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
 }
 }  // namespace
 
-extern "C" int nps_absmax(const float* x, long n, float* out, void* stream) {
-    NPS_CHECK_ARG(x && out && n > 0, "absmax: bad args");
-    hipStream_t s = (hipStream_t)stream;
+int nps_absmax_scalar(const float* x, long n, float* out, hipStream_t s) {
     if (hipMemsetAsync(out, 0, sizeof(float), s) != hipSuccess) {
         nps::set_error("absmax: memset failed");
         return -2;
     }
     long nb = (n + 256 * 16 - 1) / (256 * 16);
     nb = nb < 1 ? 1 : (nb > 1024 ? 1024 : nb);
-    absmax_kernel<<<(unsigned)nb, 256, 0, s>>>(x, n, reinterpret_cast<unsigned int*>(out));
+    absmax_scalar_kernel<<<(unsigned)nb, 256, 0, s>>>(x, n, reinterpret_cast<unsigned int*>(out));
+    NPS_CHECK_LAUNCH("absmax (scalar)");
+    return 0;
+}
+namespace {
+}  // namespace
+
+extern "C" int nps_absmax(const float* x, long n, float* out, void* stream) {
+    NPS_CHECK_ARG(x && out && n > 0, "absmax: bad args");
+    hipStream_t s = (hipStream_t)stream;
+    if (hipMemsetAsync(out, 0, sizeof(float) * NPS_TAG_FLOATS, s) != hipSuccess) {
+        nps::set_error("absmax: memset failed");
+        return -2;
+    }
+    long nb = (n + 256 * 16 - 1) / (256 * 16);
+    nb = nb < 1 ? 1 : (nb > 1024 ? 1024 : nb);
+    absmax_kernel<<<(unsigned)nb, 256, 0, s>>>(x, n, out);
     NPS_CHECK_LAUNCH("absmax");
     return 0;
 }

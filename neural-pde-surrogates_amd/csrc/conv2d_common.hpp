@@ -91,8 +91,9 @@ __device__ __forceinline__ f32x4 fetch4(const nps_conv2d_t& a, int b, int y, int
 // vectorised path: all loads of the tile (bias, addends, accumulate source) are issued before
 // any store, then 16-B stores.  Order of the float ops matches the reference:
 // act(acc + bias + addends) or act(acc + bias) + addends, then + out when accumulating.
+// `amax` is raised to max |stored value| (the output's range tag, nps_conv2d_t.out_tag).
 __device__ __forceinline__ void store_tile(const nps_conv2d_t& a, int b, int co_base, int h, const f32x16& acc,
-                                           int dy, int dx) {
+                                           int dy, int dx, float& amax) {
     if (!a.out_nchw && (a.out_C & 3) == 0 && (a.Cout & 3) == 0) {
         const size_t base = (((size_t)b * a.out_H + dy) * a.out_W + dx) * a.out_C;
         f32x4 bi[4], a0[4], a1[4], o[4];
@@ -119,6 +120,7 @@ __device__ __forceinline__ void store_tile(const nps_conv2d_t& a, int b, int co_
                 if (a.add_after_act) v = v + a0[m][e] + a1[m][e];
                 if (a.accumulate) v += o[m][e];
                 r[e] = v;
+                amax = fmaxf(amax, fabsf(v));
             }
             *reinterpret_cast<f32x4*>(a.out + base + co0) = r;
         }
@@ -148,6 +150,7 @@ __device__ __forceinline__ void store_tile(const nps_conv2d_t& a, int b, int co_
             }
             if (a.accumulate) v += a.out[di];
             a.out[di] = v;
+            amax = fmaxf(amax, fabsf(v));
         }
     }
 }
@@ -168,9 +171,14 @@ __device__ __forceinline__ float pow2_scale_for(float m) {
     if (!(m > 0.f) || !(m < 3.0e38f)) return 1.f;
     return ldexpf(1.f, 13 - ilogbf(m));
 }
-// input scale of a split-fp16 conv: from a.in_scale (device pointer to max|x|, nps_absmax) or 1
+// input scale of a split-fp16 conv: from the range tags of its input (in_scale, in_tag1, in_tag2: the max
+// of the non-NULL ones) or 1 when it has none.  Wave-collective (every lane of the wave active).
 __device__ __forceinline__ float in_scale_of(const nps_conv2d_t& a) {
-    return a.in_scale == nullptr ? 1.f : pow2_scale_for(*a.in_scale);
+    if (a.in_scale == nullptr && a.in_tag1 == nullptr && a.in_tag2 == nullptr) return 1.f;
+    return pow2_scale_for(fmaxf(nps::tag_read(a.in_scale), fmaxf(nps::tag_read(a.in_tag1), nps::tag_read(a.in_tag2))));
+}
+__device__ __forceinline__ bool has_in_scale(const nps_conv2d_t& a) {
+    return a.in_scale != nullptr || a.in_tag1 != nullptr || a.in_tag2 != nullptr;
 }
 
 typedef _Float16 h2f __attribute__((ext_vector_type(2)));
@@ -213,3 +221,5 @@ inline int x3_lds_bytes(const nps_conv2d_t& a) {
 
 // conv2d_x3.hip: launch of the split-fp16 kernel for a planned nps_conv2d_t
 int nps_launch_conv2d_x3(const nps_conv2d_t& a, int lds, hipStream_t s);
+// conv2d.hip: *out = max |x[i]| as one float (the packed-weight trailer; nps_absmax writes a range tag)
+int nps_absmax_scalar(const float* x, long n, float* out, hipStream_t s);

@@ -46,15 +46,6 @@ __device__ unsigned long long x3_stamps[1 << 20];
 #define X3_RSTAMP(i)
 #endif
 
-// s_waitcnt vmcnt(N) that the compiler sees as redefining every register of rp: no read of a
-// register loaded by an inline-asm global_load can be scheduled above the wait that covers it.
-template <int N, int MAXP>
-__device__ __forceinline__ void x3_vm_wait(f32x4 (&rp)[MAXP]) {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-#pragma unroll
-    for (int k = 0; k < MAXP; ++k) asm volatile("" : "+v"(rp[k]));
-}
-
 template <int N, typename F>
 __device__ __forceinline__ void static_for(F&& f) {
     if constexpr (N > 0) {
@@ -73,7 +64,7 @@ __device__ __forceinline__ bool x3_lds_epilogue(const nps_conv2d_t& a) {
 // the fused bias / addends / GELU / accumulate of store_tile, in the same float order.
 template <int TILE_PX>
 __device__ __forceinline__ void x3_store_phase(const nps_conv2d_t& a, int b, int cob, int oy0, int ox0, int lat,
-                                               const float* T, int tid) {
+                                               const float* T, int tid, float& amax) {
 #pragma unroll 4
     for (int i = tid; i < TILE_PX * 16; i += 512) {
         const int P = i >> 4, q = i & 15;
@@ -99,6 +90,7 @@ __device__ __forceinline__ void x3_store_phase(const nps_conv2d_t& a, int b, int
             if (a.add_after_act) v = v + a0[e] + a1[e];
             if (a.accumulate) v += ov[e];
             r[e] = v;
+            amax = fmaxf(amax, fabsf(v));
         }
         *reinterpret_cast<f32x4*>(a.out + o) = r;
     }
@@ -218,8 +210,8 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
             const unsigned chm = chok ? ~0u : 0u;
             const int cs = chok ? c0 - cbase + gq * 4 : 0;
 #pragma unroll
-            for (int k = 0; k < MAXP; ++k)  // inline asm: invisible to the compiler's vmcnt tracking
-                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(rp[k]) : "v"(sbase[k] + cs));
+            for (int k = 0; k < MAXP; ++k)  // compiler-visible loads: waited before first use, spill-safe
+                rp[k] = *reinterpret_cast<const f32x4*>(sbase[k] + cs);
             if constexpr (PRO) {
                 // this lane's 4 frame channels share one group (host-checked: channels per group % 4 == 0);
                 // without GroupNorm (or past the channel tail) the loads read the packed weights instead
@@ -229,9 +221,9 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
                 const float* pb = gn ? a.gn_beta + c : reinterpret_cast<const float*>(a.wpack);
                 const double* ps = gn ? a.gn_stats + ((size_t)fb * a.gn_groups + c / (a.Cin / a.gn_groups)) * 2
                                       : reinterpret_cast<const double*>(a.wpack);
-                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(rp[MAXP]) : "v"(pg));
-                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(rp[MAXP + 1]) : "v"(pb));
-                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(rp[MAXP + 2]) : "v"(ps));
+                rp[MAXP] = *reinterpret_cast<const f32x4*>(pg);
+                rp[MAXP + 1] = *reinterpret_cast<const f32x4*>(pb);
+                rp[MAXP + 2] = *reinterpret_cast<const f32x4*>(ps);
             }
             // bits 0-15: slot data lies inside the source; bits 16-31: slot pixel lies inside the frame
             return (pixm & chm) | ((finm & chm) << 16);
@@ -285,31 +277,27 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
         // Per tile: the first two stages (fetched during the previous tile's epilogue) are split into
         // ring slots 0 / 1, then iteration st (while the consumers compute stage st) waits for stage
         // st + 2's fetch (issued one iteration earlier), splits it into slot (st + 2) % 3 (released at
-        // the last barrier) and fetches stage st + 3.  The fetches are inline-asm loads waited for by
-        // x3_vm_wait, which takes the destination registers as operands (no use moves above the wait);
+        // the last barrier) and fetches stage st + 3.  The fetches are ordinary (compiler-visible) loads:
+        // the compiler waits for them before their first use, across the raw barriers, and a spill of a
+        // register set waits for its loads first (an inline-asm load protocol is not spill-safe);
         // stage indices past the end are clamped (fetched anyway: the loads in flight are the same on
         // every path), commits past the end skipped.  Barriers per tile: 1 + nstages + 2, as consumers.
         int l = blockIdx.x;
+        float pmax = 0.f;  // max |stored value| of this thread's share of the store phases (out_tag)
         decode(l, fcob, fb, fy0, fx0);
         unsigned m0 = issue(0, r0);
         unsigned m1 = issue(min(1, last), r1);
         for (;;) {
             const int scob = fcob, sb = fb, soy0 = fy0, sox0 = fx0;  // tile being computed / stored
-            // vmcnt(0): the previous tile's store phase left global stores in flight behind r0 / r1, and
-            // stores may complete out of order with loads, so a partial count does not prove r0 landed
-            x3_vm_wait<0>(r0);
-            x3_vm_wait<0>(r1);
             commit(0, r0, m0);
             if (nstages > 1) commit(1, r1, m1);
             unsigned m = issue(min(2, last), r0);
             barrier();
             for (int st = 0; st < nstages; ++st) {
-                x3_vm_wait<0>(r0);
                 if (st + 2 < nstages) commit(st + 2, r0, m);
                 m = issue(min(st + 3, last), r0);
                 barrier();
             }
-            x3_vm_wait<0>(r0);  // drain the last (clamped) fetch before the registers are reused
             const int ln = l + (int)gridDim.x;
             const bool more = ln < nwg;
             if (more) {  // the next tile's first two stages load while this tile is stored
@@ -319,16 +307,13 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
                 m1 = issue(min(1, last), r1);
             }
             barrier();  // the consumers' tile is in LDS
-            if (lds_epi) x3_store_phase<TILE_PX>(a, sb, scob, soy0, sox0, g.T, reinterpret_cast<const float*>(ring), tid);
+            if (lds_epi)
+                x3_store_phase<TILE_PX>(a, sb, scob, soy0, sox0, g.T, reinterpret_cast<const float*>(ring), tid, pmax);
             barrier();  // every read of the staged tile is done: the ring may be refilled
             if (!more) break;
-            // land the next tile's fetches before the loop latch: r0 / r1 are loop-carried, and the
-            // compiler may move or spill them there without knowing an inline-asm load is in flight
-            x3_vm_wait<0>(r0);
-            x3_vm_wait<0>(r1);
             l = ln;
         }
-        x3_vm_wait<0>(r1);
+        nps::tag_publish(a.out_tag, pmax, nps::wave_salt());
         return;
     }
 
@@ -414,6 +399,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
     // epilogue scale: undo the exact power-of-2 scales of the weights and the input
     const float inv = 1.f / (pow2_scale_for(a.wpack[packed_body(a.Cout, a.Cin, NTAPS)]) * in_scale_of(a));
     const int h = lane >> 5;
+    float amax = 0.f;  // max |stored value| over this thread's tiles (out_tag)
     for (int l = blockIdx.x; l < nwg; l += gridDim.x) {
         int cob, b, oy0, ox0;
         decode(l, cob, b, oy0, ox0);
@@ -459,7 +445,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
                     }
             }
             barrier();
-            x3_store_phase<TILE_PX>(a, b, cob, oy0, ox0, g.T, T, tid);
+            x3_store_phase<TILE_PX>(a, b, cob, oy0, ox0, g.T, T, tid, amax);
         } else {
             static_for<PB>([&](auto pbc) {  // compile-time pb: acc stays in registers
                 constexpr int pb = decltype(pbc)::value;
@@ -474,7 +460,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
                     f32x16 v = acc[cb][pb];
 #pragma unroll
                     for (int r = 0; r < 16; ++r) v[r] *= inv;
-                    store_tile(a, b, cob * 64 + cb * 32, h, v, dy, dx);
+                    store_tile(a, b, cob * 64 + cb * 32, h, v, dy, dx, amax);
                     __builtin_amdgcn_sched_barrier(0);
                 }
             });
@@ -484,6 +470,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
         X3_STAMP(3);
         X3_RSTAMP(5);
     }
+    nps::tag_publish(a.out_tag, amax, nps::wave_salt());
 }
 
 
@@ -513,7 +500,7 @@ __global__ __launch_bounds__(512) void conv1x1_x3_kernel(const nps_conv2d_t a) {
     const int npx = a.Hout * a.Wout;
     const int P0 = blockIdx.x * (PB * 32);
     const float xs = in_scale_of(a);
-    const bool scaled = a.in_scale != nullptr;  // range-scaled inputs (gradients); forward inputs are not
+    const bool scaled = has_in_scale(a);  // range-scaled input (xs != 1 possible)
     // this lane's output pixel of each pixel block -> its (circularly extended) frame position
     int fy[PB], fx[PB];
     unsigned pin = 0;
@@ -681,6 +668,7 @@ __global__ __launch_bounds__(512) void conv1x1_x3_kernel(const nps_conv2d_t a) {
         int fp = fixq ? (int)threadIdx.x / C4 : 0;
         const int fcl = fixq ? ((int)threadIdx.x - fp * C4) * 4 : 0;
         int foy = (P0 + fp) / a.Wout, fox = (P0 + fp) - ((P0 + fp) / a.Wout) * a.Wout;
+        float amax = 0.f;
         for (int i = threadIdx.x; i < PB * 32 * C4; i += blockDim.x) {
             int p, cl, oy, ox;
             if (fixq) {
@@ -721,11 +709,14 @@ __global__ __launch_bounds__(512) void conv1x1_x3_kernel(const nps_conv2d_t a) {
                 if (a.add_after_act) v = v + a0[e] + a1[e];
                 if (a.accumulate) v += ov[e];
                 r[e] = v;
+                amax = fmaxf(amax, fabsf(v));
             }
             *reinterpret_cast<f32x4*>(a.out + o) = r;
         }
+        nps::tag_publish(a.out_tag, amax, nps::wave_salt());
         return;
     }
+    float amax = 0.f;
     static_for<PB>([&](auto pbc) {  // compile-time pb: acc stays in registers
         constexpr int pb = decltype(pbc)::value;
         const int P = P0 + pb * 32 + (lane & 31);
@@ -740,9 +731,10 @@ __global__ __launch_bounds__(512) void conv1x1_x3_kernel(const nps_conv2d_t a) {
             f32x16 v = acc[cb][pb];
 #pragma unroll
             for (int r = 0; r < 16; ++r) v[r] *= inv;
-            store_tile(a, b, co, h, v, dy, dx);
+            store_tile(a, b, co, h, v, dy, dx, amax);
         }
     });
+    nps::tag_publish(a.out_tag, amax, nps::wave_salt());
 }
 
 // 1x1 with the weights staged in LDS: a wave covers ALL output channels (NCB 32-channel blocks) of its
@@ -763,7 +755,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     const int npx = a.Hout * a.Wout;
     const int P = blockIdx.x * 128 + wv * 32 + (lane & 31);
     const float xs = in_scale_of(a);
-    const bool scaled = a.in_scale != nullptr;
+    const bool scaled = has_in_scale(a);
     int fy, fx;
     bool pin;
     {
@@ -883,18 +875,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
         });
     }
     const float inv = 1.f / (pow2_scale_for(a.wpack[packed_body(a.Cout, a.Cin, 1)]) * xs);
-    if (P >= npx) return;
     const int oy = P / a.Wout, ox = P - (P / a.Wout) * a.Wout;
     const int dy = oy * a.out_os + a.out_off_y, dx = ox * a.out_os + a.out_off_x;
-    if (dy < 0 || dy >= a.out_H || dx < 0 || dx >= a.out_W) return;
+    float amax = 0.f;
+    if (P < npx && dy >= 0 && dy < a.out_H && dx >= 0 && dx < a.out_W) {
 #pragma unroll
-    for (int cb = 0; cb < NCB; ++cb) {
-        if (cb * 32 >= a.Cout) continue;
-        f32x16 v = acc[cb];
+        for (int cb = 0; cb < NCB; ++cb) {
+            if (cb * 32 >= a.Cout) continue;
+            f32x16 v = acc[cb];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) v[r] *= inv;
-        store_tile(a, b, cb * 32, h, v, dy, dx);
+            for (int r = 0; r < 16; ++r) v[r] *= inv;
+            store_tile(a, b, cb * 32, h, v, dy, dx, amax);
+        }
     }
+    nps::tag_publish(a.out_tag, amax, nps::wave_salt());
 }
 
 template <int NT, int PB, bool PRO = false>

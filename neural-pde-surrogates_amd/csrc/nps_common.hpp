@@ -64,4 +64,34 @@ __device__ __forceinline__ double block_sum(double v, double* scratch) {
     return r;
 }
 
+// ---- range tags (include/nps.h NPS_TAG_*): an upper bound of |x| over a tensor, kept as the max of
+// NPS_TAG_SUB sub-slots so the writers' atomics spread over many addresses.
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// Value of a tag (0 for NULL).  Wave-collective: all 64 lanes must be active (lane l reads sub-slot l).
+__device__ __forceinline__ float tag_read(const float* tag) {
+    if (tag == nullptr) return 0.f;
+    const int lane = threadIdx.x & 63;
+    return wave_max(tag[lane * NPS_TAG_STRIDE]);
+}
+
+// Raise a tag to cover m (>= 0) of every lane.  Wave-collective (all 64 lanes active); one atomic per
+// wave, into the sub-slot picked by `salt` (e.g. the wave's global index).  Non-negative floats order
+// like their bit patterns, so an unsigned atomic max is a float max.
+__device__ __forceinline__ void tag_publish(float* tag, float m, unsigned salt) {
+    if (tag == nullptr) return;
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0 && m > 0.f)
+        atomicMax(reinterpret_cast<unsigned int*>(tag + (salt % NPS_TAG_SUB) * NPS_TAG_STRIDE), __float_as_uint(m));
+}
+
+// a globally unique-ish wave number of the calling wave (sub-slot salt)
+__device__ __forceinline__ unsigned wave_salt() {
+    return ((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+}
+
 }  // namespace nps

@@ -218,7 +218,7 @@ __global__ void idft_h_kernel(const float2* __restrict__ Y, float2* __restrict__
 template <int KC>
 __global__ void idft_w_kernel(const float2* __restrict__ Z, float* __restrict__ out, int H, int W, int m2, int Cout,
                               int accumulate, const float* __restrict__ addend, int act, float scale_arg,
-                              int doubling) {
+                              int doubling, float* __restrict__ out_tag) {
     extern __shared__ __attribute__((aligned(16))) float2 tw[];  // [chunk][W][KC], zero past m2
     const int h = blockIdx.x, b = blockIdx.y;
     const int nch = (m2 + KC - 1) / KC;
@@ -229,6 +229,7 @@ __global__ void idft_w_kernel(const float2* __restrict__ Z, float* __restrict__ 
     }
     __syncthreads();
     const float scale = scale_arg;
+    float amax = 0.f;  // max |written value| of the final chunk (the output's range tag)
     for (int o = threadIdx.x; o < Cout; o += blockDim.x) {
         float zr[KC], zi[KC];
         for (int kb = 0; kb < m2; kb += KC) {
@@ -268,6 +269,7 @@ __global__ void idft_w_kernel(const float2* __restrict__ Z, float* __restrict__ 
                 if (last_chunk) {
                     if (addend) v += add;
                     if (act == 1) v = nps::gelu_erf(v);
+                    amax = fmaxf(amax, fabsf(v));
                 }
                 out[(rowo + w) * Cout + o] = v;
             };
@@ -295,6 +297,7 @@ __global__ void idft_w_kernel(const float2* __restrict__ Z, float* __restrict__ 
                 pixel(w0, rd_out ? out[(rowo + w0) * Cout + o] : 0.f, rd_add ? addend[(rowo + w0) * Cout + o] : 0.f);
         }
     }
+    nps::tag_publish(out_tag, amax, nps::wave_salt());
 }
 
 
@@ -396,22 +399,23 @@ void launch_dft_w(dim3 grid, int bs, size_t lds, hipStream_t s, const nps_conv2d
 
 template <int KC>
 void launch_idft_w_kc(dim3 grid, int bs, size_t lds, hipStream_t s, const float2* Z, float* out, int H, int W, int m2,
-                      int C, int accumulate, const float* addend, int act, float scale, int doubling) {
+                      int C, int accumulate, const float* addend, int act, float scale, int doubling, float* tag) {
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void*)idft_w_kernel<KC>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
         attr_set = true;
     }
-    idft_w_kernel<KC><<<grid, bs, lds, s>>>(Z, out, H, W, m2, C, accumulate, addend, act, scale, doubling);
+    idft_w_kernel<KC><<<grid, bs, lds, s>>>(Z, out, H, W, m2, C, accumulate, addend, act, scale, doubling, tag);
 }
 
 void launch_idft_w(dim3 grid, int bs, size_t lds, hipStream_t s, const float2* Z, float* out, int H, int W, int m2,
-                   int C, int accumulate, const float* addend, int act, float scale, int doubling) {
+                   int C, int accumulate, const float* addend, int act, float scale, int doubling,
+                   float* tag = nullptr) {
     switch (kc_for(m2)) {
-        case 4: launch_idft_w_kc<4>(grid, bs, lds, s, Z, out, H, W, m2, C, accumulate, addend, act, scale, doubling); break;
-        case 8: launch_idft_w_kc<8>(grid, bs, lds, s, Z, out, H, W, m2, C, accumulate, addend, act, scale, doubling); break;
-        case 12: launch_idft_w_kc<12>(grid, bs, lds, s, Z, out, H, W, m2, C, accumulate, addend, act, scale, doubling); break;
-        default: launch_idft_w_kc<16>(grid, bs, lds, s, Z, out, H, W, m2, C, accumulate, addend, act, scale, doubling); break;
+        case 4: launch_idft_w_kc<4>(grid, bs, lds, s, Z, out, H, W, m2, C, accumulate, addend, act, scale, doubling, tag); break;
+        case 8: launch_idft_w_kc<8>(grid, bs, lds, s, Z, out, H, W, m2, C, accumulate, addend, act, scale, doubling, tag); break;
+        case 12: launch_idft_w_kc<12>(grid, bs, lds, s, Z, out, H, W, m2, C, accumulate, addend, act, scale, doubling, tag); break;
+        default: launch_idft_w_kc<16>(grid, bs, lds, s, Z, out, H, W, m2, C, accumulate, addend, act, scale, doubling, tag); break;
     }
 }
 
@@ -501,14 +505,14 @@ extern "C" int nps_spectral_idft_h(const float* Y, float* Z, int B, int H, int m
 }
 
 extern "C" int nps_spectral_idft_w(const float* Z, float* out, int B, int H, int W, int m2, int Cout, int accumulate,
-                                   const float* addend, int act, void* stream) {
+                                   const float* addend, int act, float* out_tag, void* stream) {
     NPS_CHECK_ARG(Z && out && B > 0 && H > 0 && W > 0 && m2 > 0 && m2 <= W / 2 + 1 && Cout > 0,
                   "spectral_idft_w: bad args");
     const size_t lds = idft_w_lds(m2, W);
     NPS_CHECK_ARG(lds <= 96 * 1024, "spectral_idft_w: m2*W too large");
     const int bs = Cout >= 256 ? 256 : ((Cout + 63) / 64) * 64;
     launch_idft_w(dim3(H, B), bs, lds, (hipStream_t)stream, reinterpret_cast<const float2*>(Z), out, H, W, m2, Cout,
-                  accumulate, addend, act, 1.0f / ((float)H * (float)W), 1);
+                  accumulate, addend, act, 1.0f / ((float)H * (float)W), 1, out_tag);
     NPS_CHECK_LAUNCH("spectral_idft_w");
     return 0;
 }

@@ -217,7 +217,7 @@ class ResidualBlock(nn.Module):
         if isinstance(self.shortcut, nn.Identity):
             if len(srcs) != 1 or srcs[0].off_y or srcs[0].off_x or tuple(srcs[0].t.shape[1:3]) != (H, W):
                 raise RuntimeError("identity shortcut on a concatenated input")
-            out = srcs[0].t.clone()
+            out = ops.share_tag(srcs[0].t.clone(), srcs[0].t)  # conv2 accumulates into it: same bound
         else:
             out = self.shortcut.run(srcs, (H, W))
         H1, W1 = h1.shape[1:3]

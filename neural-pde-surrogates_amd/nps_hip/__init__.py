@@ -46,7 +46,8 @@ class Conv2dArgs(ctypes.Structure):
         ("addend0", ctypes.c_void_p), ("addend1", ctypes.c_void_p),
         ("act", ctypes.c_int), ("add_after_act", ctypes.c_int),
         ("TH", ctypes.c_int), ("TW", ctypes.c_int), ("lattice", ctypes.c_int), ("waves", ctypes.c_int),
-        ("precision", ctypes.c_int), ("in_scale", ctypes.c_void_p),
+        ("precision", ctypes.c_int), ("in_scale", ctypes.c_void_p), ("in_tag1", ctypes.c_void_p),
+        ("in_tag2", ctypes.c_void_p), ("out_tag", ctypes.c_void_p),
     ]
 
 
@@ -78,7 +79,7 @@ _SIGS = {
     "nps_spectral_pack_weights": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _vp]),
     "nps_spectral_mix": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _vp]),
     "nps_spectral_idft_h": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp]),
-    "nps_spectral_idft_w": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _i, _vp]),
+    "nps_spectral_idft_w": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _i, _vp, _vp]),
     "nps_pack_grid_input": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp]),
     "nps_timeconv_decode": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _vp, _i, _i, _i, _i, _i, _i,
                                  _vp]),

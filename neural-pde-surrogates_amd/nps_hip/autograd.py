@@ -400,7 +400,8 @@ class SpectralConv2dFn(torch.autograd.Function):
         check(lib.nps_spectral_dft_h(ptr(X1), ptr(X2), B, H, m1, m2, Cin, s), "spectral_dft_h")
         check(lib.nps_spectral_mix(ptr(X2), ptr(wpack), ptr(Y), B, R, m2, Cin, Cout, s), "spectral_mix")
         check(lib.nps_spectral_idft_h(ptr(Y), ptr(Z), B, H, m1, m2, Cout, s), "spectral_idft_h")
-        check(lib.nps_spectral_idft_w(ptr(Z), ptr(y), B, H, W, m2, Cout, 0, None, 0, s), "spectral_idft_w")
+        check(lib.nps_spectral_idft_w(ptr(Z), ptr(y), B, H, W, m2, Cout, 0, None, 0, ops.new_tag(y), s),
+              "spectral_idft_w")
         ctx.meta, ctx.shape = meta, (B, H, W, Cin)
         ctx.save_for_backward(X2, wpack)
         return y

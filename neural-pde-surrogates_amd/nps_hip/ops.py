@@ -41,6 +41,102 @@ class Src(NamedTuple):
     off_x: int = 0
 
 
+# ----------------------------------------------------------------- range tags ----
+# A split-fp16 conv scales its input by a power of 2 picked from an upper bound of |x| (include/nps.h,
+# nps_conv2d_t.in_scale / in_tag*), so fp32-class accuracy holds for activations of any magnitude.  The
+# bound travels with the tensor as a RANGE TAG: NPS_TAG_FLOATS floats of a per-device arena, raised by
+# the kernel that writes the tensor (conv / frame_pack / spectral epilogues: out_tag).  A tensor without
+# a live tag (model inputs, views, torch-made tensors) gets one from nps_absmax the first time a
+# split-fp16 conv reads it.  Tags are only ever raised, so a tag shared by several tensors (a clone,
+# a space-to-depth copy) or written by several kernels (accumulating convs) stays an upper bound.
+TAG_FLOATS = 64 * 64        # NPS_TAG_FLOATS
+# dev knob NPS_RANGE_TAGS: "1" (default) input + output tags, "in" / "out" one side only, "0" none
+_TAGS = os.environ.get("NPS_RANGE_TAGS", "1")
+USE_IN_TAGS, USE_OUT_TAGS = _TAGS in ("1", "in"), _TAGS in ("1", "out")
+_ARENA_TAGS = 2048          # 32 MiB per device; re-zeroed (new generation) when exhausted
+
+
+class _TagArena:
+    def __init__(self, device):
+        self.buf = torch.zeros(_ARENA_TAGS * TAG_FLOATS, dtype=torch.float32, device=device)
+        self.gen = 0
+        self.next = 0
+
+    def alloc(self):
+        if self.next == _ARENA_TAGS:
+            self.buf.zero_()        # stream-ordered after every kernel that used the old generation
+            self.gen += 1
+            self.next = 0
+        i = self.next
+        self.next += 1
+        return _Tag(self, self.gen, self.buf.data_ptr() + 4 * i * TAG_FLOATS)
+
+
+class _Tag(NamedTuple):
+    arena: "_TagArena"
+    gen: int
+    ptr: int
+
+    @property
+    def live(self):
+        return self.arena.gen == self.gen
+
+
+_arenas = {}
+
+
+def _arena(device) -> _TagArena:
+    key = (device.type, device.index if device.index is not None else torch.cuda.current_device())
+    ar = _arenas.get(key)
+    if ar is None:
+        ar = _arenas[key] = _TagArena(device)
+    return ar
+
+
+def tag_of(t: torch.Tensor):
+    """The live range tag of `t`, or None."""
+    tag = getattr(t, "_nps_tag", None)
+    return tag if (tag is not None and tag.live) else None
+
+
+def new_tag(t: torch.Tensor) -> int:
+    """Attach a fresh (zero) tag to `t`, whose writer will raise it; returns its device pointer."""
+    tag = _arena(t.device).alloc()
+    t._nps_tag = tag
+    return tag.ptr
+
+
+def out_tag(t: torch.Tensor, accumulate: bool) -> int:
+    """Tag pointer for a kernel that writes into the existing tensor `t`: its live tag, or a new one —
+    seeded with max|t| when the kernel accumulates onto (reads) the current contents.  Otherwise the
+    contents the kernel leaves unwritten must be zeros or absent (crop padding, phase outputs)."""
+    tag = tag_of(t)
+    if tag is not None:
+        return tag.ptr
+    p = new_tag(t)
+    if accumulate:
+        check(lib.nps_absmax(ptr(t), t.numel(), p, stream_ptr()), "absmax (tag seed)")
+    return p
+
+
+def share_tag(dst: torch.Tensor, src: torch.Tensor) -> torch.Tensor:
+    """dst holds a subset of src's values (and zeros): it may carry src's bound."""
+    tag = tag_of(src)
+    if tag is not None:
+        dst._nps_tag = tag
+    return dst
+
+
+def input_tag(t: torch.Tensor) -> int:
+    """Tag pointer bounding |t| for a split-fp16 conv reading t (nps_absmax when t has no live tag)."""
+    tag = tag_of(t)
+    if tag is not None:
+        return tag.ptr
+    p = new_tag(t)
+    check(lib.nps_absmax(ptr(t), t.numel(), p, stream_ptr()), "absmax (input tag)")
+    return p
+
+
 def _c_src(srcs: Sequence[Src]):
     arr = (_CSrc * 3)()
     for i, s in enumerate(srcs):
@@ -92,7 +188,7 @@ def space_to_depth(x: torch.Tensor, pad: int, Hq: int, Wq: int) -> torch.Tensor:
     B, H, W, C = x.shape
     out = torch.empty((B, Hq, Wq, 4 * C), dtype=torch.float32, device=x.device)
     check(lib.nps_space_to_depth(ptr(x), ptr(out), B, H, W, C, pad, Hq, Wq, stream_ptr()), "space_to_depth")
-    return out
+    return share_tag(out, x)
 
 
 def pack_convT_phases(w: torch.Tensor) -> List[torch.Tensor]:
@@ -164,6 +260,7 @@ def conv2d(srcs: Sequence[Src], frame_hw, wpack: torch.Tensor, bias: Optional[to
         Hout, Wout = out_hw
     if Hout <= 0 or Wout <= 0:
         raise RuntimeError(f"nps_hip conv2d: empty output {Hout}x{Wout} for input {Hin}x{Win} k={KH}")
+    out_given = out is not None
     if out is None:
         out = (torch.empty((B, Cout, Hout, Wout), dtype=torch.float32, device=t0.device) if out_nchw
                else empty_nhwc(B, Hout, Wout, Cout, t0))
@@ -192,8 +289,16 @@ def conv2d(srcs: Sequence[Src], frame_hw, wpack: torch.Tensor, bias: Optional[to
     a.addend1 = ptr(ads[1]) if len(ads) > 1 else None
     a.act, a.add_after_act = act, (1 if add_after_act else 0)
     a.precision = getattr(wpack, "nps_precision", PREC_F32)
-    if in_scale is not None and a.precision == PREC_X3F16:
-        a.in_scale = ptr(in_scale)
+    if a.precision == PREC_X3F16:
+        if in_scale is not None:  # explicit range (gradients): overrides the sources' tags
+            a.in_scale = ptr(in_scale)
+        elif USE_IN_TAGS and not (fused and gn is not None):
+            # the sources' tags (a fused GroupNorm prologue normalises the frame: its output range is not
+            # the sources', the normalised values are O(1) and run unscaled)
+            tags = [input_tag(s.t) for s in srcs] + [None, None]
+            a.in_scale, a.in_tag1, a.in_tag2 = tags[0], tags[1], tags[2]
+    if USE_OUT_TAGS:
+        a.out_tag = out_tag(out, accumulate) if out_given else new_tag(out)
     if lib.nps_conv2d_plan(ctypes_byref(a)) < 0:
         raise RuntimeError("conv2d_plan failed: " + lib.nps_last_error().decode())
     if conv_probe is not None:
@@ -210,11 +315,23 @@ def conv2d(srcs: Sequence[Src], frame_hw, wpack: torch.Tensor, bias: Optional[to
 
 
 def absmax(x: torch.Tensor) -> torch.Tensor:
-    """(1,) fp32 device tensor max|x| — the input range for a split-fp16 conv (conv2d(in_scale=...))."""
+    """Range tag (TAG_FLOATS fp32 device tensor, value max|x|) — the input range of a split-fp16 conv
+    (conv2d(in_scale=...)); tag_value() reads it back."""
     x = x.contiguous()
-    out = torch.empty(1, dtype=torch.float32, device=x.device)
+    out = torch.empty(TAG_FLOATS, dtype=torch.float32, device=x.device)
     check(lib.nps_absmax(ptr(x), x.numel(), ptr(out), stream_ptr()), "absmax")
     return out
+
+
+def tag_value(tag) -> float:
+    """Host value of a range tag (a tag tensor, or a tensor carrying a live tag) — for tests / diagnostics."""
+    if isinstance(tag, torch.Tensor) and tag.numel() == TAG_FLOATS and tag_of(tag) is None:
+        return float(tag.view(64, 64)[:, 0].max())
+    t = tag_of(tag)
+    if t is None:
+        return float("nan")
+    i = (t.ptr - t.arena.buf.data_ptr()) // 4
+    return float(t.arena.buf[i:i + TAG_FLOATS].view(64, 64)[:, 0].max())
 
 
 def frame_pack(srcs: Sequence[Src], frame_hw, gn: Optional[GN] = None, pre_act=0, pad4=False) -> torch.Tensor:
@@ -234,6 +351,7 @@ def frame_pack(srcs: Sequence[Src], frame_hw, gn: Optional[GN] = None, pre_act=0
     a.pre_act = pre_act
     a.out_C = (Cin + 3) // 4 * 4 if pad4 else Cin
     out = empty_nhwc(B, Hin, Win, a.out_C, t0)
+    a.out_tag = new_tag(out)
     check(lib.nps_frame_pack(ctypes_byref(a), ptr(out), stream_ptr()), "frame_pack")
     return out
 
@@ -261,13 +379,16 @@ def spectral_conv2d(srcs: Sequence[Src], wpack: torch.Tensor, m1: int, m2: int, 
     if out is None:
         out = empty_nhwc(B, H, W, Cout, t0)
         accumulate = False
+        tag = new_tag(out)
+    else:
+        tag = out_tag(out, accumulate)
     s = stream_ptr()
     check(lib.nps_spectral_dft_w(_c_src(srcs), len(srcs), B, H, W, Cin, m2, ptr(X1), s), "spectral_dft_w")
     check(lib.nps_spectral_dft_h(ptr(X1), ptr(X2), B, H, m1, m2, Cin, s), "spectral_dft_h")
     check(lib.nps_spectral_mix(ptr(X2), ptr(wpack), ptr(Y), B, R, m2, Cin, Cout, s), "spectral_mix")
     check(lib.nps_spectral_idft_h(ptr(Y), ptr(Z), B, H, m1, m2, Cout, s), "spectral_idft_h")
-    check(lib.nps_spectral_idft_w(ptr(Z), ptr(out), B, H, W, m2, Cout, 1 if accumulate else 0, ptr(addend), act, s),
-          "spectral_idft_w")
+    check(lib.nps_spectral_idft_w(ptr(Z), ptr(out), B, H, W, m2, Cout, 1 if accumulate else 0, ptr(addend), act,
+                                  tag, s), "spectral_idft_w")
     return out
 
 
@@ -310,7 +431,7 @@ def spectral_conv3d_stages(x4: Sequence[Src], D, H, W, Cin, wpack, m1, m2, m3, C
     check(lib.nps_spectral_idft_h(ptr(Y), ptr(Z1), B, D, m1, R2 * m3, Cout, s), "spectral3d idft_h (D)")
     check(lib.nps_spectral_idft_h(ptr(Z1), ptr(Z2), B * D, H, m2, m3, Cout, s), "spectral3d idft_h (H)")
     check(lib.nps_spectral_idft_w(ptr(Z2), ptr(out), B, D * H, W, m3, Cout, 1 if accumulate else 0, ptr(addend), act,
-                                  s), "spectral3d idft_w")
+                                  out_tag(out, accumulate), s), "spectral3d idft_w")
     return X3
 
 
@@ -356,14 +477,14 @@ def nchw_to_nhwc(x: torch.Tensor) -> torch.Tensor:
     B, C, H, W = x.shape
     out = torch.empty((B, H, W, C), dtype=torch.float32, device=x.device)
     check(lib.nps_nchw_to_nhwc(ptr(x), ptr(out), B, C, H, W, stream_ptr()), "nchw_to_nhwc")
-    return out
+    return share_tag(out, x)
 
 
 def nhwc_to_nchw(x: torch.Tensor) -> torch.Tensor:
     B, H, W, C = x.shape
     out = torch.empty((B, C, H, W), dtype=torch.float32, device=x.device)
     check(lib.nps_nhwc_to_nchw(ptr(x), ptr(out), B, C, H, W, stream_ptr()), "nhwc_to_nchw")
-    return out
+    return share_tag(out, x)
 
 
 def pack_grid_input(u, pos, cond, sc, Cp):

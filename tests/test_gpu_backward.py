@@ -304,7 +304,7 @@ def test_pushforward_train_one_epoch():
     m.train()
     # T = 50: the only valid window starts at step 25, so successive losses are comparable
     u, cond, pos, sc = twophase_batch(2, 1, 50, 32, 32, seed=3, obstacle="random", device=DEV)
-    batch = (u[:, :, :1], u, pos, cond, torch.empty(0, device=DEV), sc)
+    batch = (u[:, :, :1], u, pos, cond, torch.empty(u.shape[0], 0, device=DEV), sc)
     cfg = argparse.Namespace(time_window=25, base_resolution=(50, 32, 32), device=DEV, batch_size=2,
                              lr_step_interval=1, unrolling=2)
     opt = torch.optim.Adam(m.parameters(), lr=1e-4)
@@ -322,5 +322,5 @@ def test_pushforward_train_one_epoch():
     tr2 = AutoregressivePushforwardTrainer(model=m, data=types.SimpleNamespace(pde=m.pde, data_interface=D.sim2d),
                                            criterion=nn.MSELoss(reduction="sum"), optimizer=opt, config=cfg)
     for _ in range(3):
-        l2 = float(tr2.train_one_epoch([(u2[:, :, :1], u2, pos, cond, torch.empty(0, device=DEV), sc)], epoch=3))
+        l2 = float(tr2.train_one_epoch([(u2[:, :, :1], u2, pos, cond, torch.empty(u2.shape[0], 0, device=DEV), sc)], epoch=3))
         assert l2 == l2
