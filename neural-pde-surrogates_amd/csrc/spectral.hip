@@ -9,6 +9,8 @@
 // integer phase (k*n mod N)/N.
 #include "nps_common.hpp"
 
+#include <cstdlib>
+
 namespace {
 
 constexpr int R_CHUNK = 8;     // retained rows per pass in dft_h
@@ -131,6 +133,102 @@ __global__ void dft_h_kernel(const float2* __restrict__ X1, float2* __restrict__
         if (r < nr) X2[((size_t)(b * R + r0 + r) * m2) * C + idx] = acc[r];
 }
 
+// H-pass of the forward DFT, split over the work-group: X2[b][r][col] = sum_h X1[b][h][col] e^{-2 pi i k1(r) h / H}
+// for every column col = (k2, c).  Work-group = 64 columns x 4 h-slices (wave s sums h = s, s + 4, ...: a
+// wave reads one 512-B row segment per h, coalesced), all RC retained rows in registers (rows past R have
+// zero twiddles), partial sums reduced through LDS.  The single-thread-per-column form left ~2 waves per
+// CU each walking H serially (latency-bound, 0.5 TB/s at C3).
+template <int RC>
+__global__ __launch_bounds__(256) void dft_h2_kernel(const float2* __restrict__ X1, float2* __restrict__ X2, int H,
+                                                     int R, int m1, int NC) {
+    extern __shared__ __attribute__((aligned(16))) float2 sm[];  // tw [H][RC], then partials [4][RC][64]
+    const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, hs = tid >> 6;
+    const int col = blockIdx.x * 64 + lane;
+    for (int i = tid; i < H * RC; i += 256) {
+        const int h = i / RC, r = i - (i / RC) * RC;
+        sm[i] = r < R ? twiddle(row_k1(r, H, R, m1), h, H) : make_float2(0.f, 0.f);
+    }
+    __syncthreads();
+    float2 acc[RC];
+#pragma unroll
+    for (int r = 0; r < RC; ++r) acc[r] = make_float2(0.f, 0.f);
+    const bool ok = col < NC;
+    const float2* src = X1 + (size_t)b * H * NC + (ok ? col : 0);
+    constexpr int U = 4;  // independent row loads issued before their FMAs
+    for (int h0 = hs; h0 < H; h0 += 4 * U) {
+        float2 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int h = h0 + 4 * u;
+            v[u] = (ok && h < H) ? src[(size_t)h * NC] : make_float2(0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int h = min(h0 + 4 * u, H - 1);  // (v is 0 past H)
+            const f32x4* t4 = reinterpret_cast<const f32x4*>(sm + h * RC);
+#pragma unroll
+            for (int q = 0; q < RC / 2; ++q) {
+                const f32x4 t = t4[q];  // (c, s) of rows 2q, 2q + 1; e^{-i th} = (c, -s)
+                acc[2 * q].x = fmaf(v[u].x, t[0], fmaf(v[u].y, t[1], acc[2 * q].x));
+                acc[2 * q].y = fmaf(v[u].y, t[0], fmaf(-v[u].x, t[1], acc[2 * q].y));
+                acc[2 * q + 1].x = fmaf(v[u].x, t[2], fmaf(v[u].y, t[3], acc[2 * q + 1].x));
+                acc[2 * q + 1].y = fmaf(v[u].y, t[2], fmaf(-v[u].x, t[3], acc[2 * q + 1].y));
+            }
+        }
+    }
+    __syncthreads();  // the twiddle table is dead: its LDS takes the partial sums
+#pragma unroll
+    for (int r = 0; r < RC; ++r) sm[(hs * RC + r) * 64 + lane] = acc[r];
+    __syncthreads();
+    for (int r = hs; r < R; r += 4) {
+        float2 t = sm[r * 64 + lane];
+#pragma unroll
+        for (int k = 1; k < 4; ++k) {
+            const float2 u = sm[(k * RC + r) * 64 + lane];
+            t.x += u.x;
+            t.y += u.y;
+        }
+        if (ok) X2[((size_t)b * R + r) * NC + col] = t;
+    }
+}
+
+// H-pass of the inverse DFT: Z[b][h][col] = sum_r Y[b][r][col] e^{+2 pi i k1(r) h / H}.  Work-group = 64
+// columns x IH_HB rows h (4 waves, wave s taking h = h0 + s, + 4, ...), the column's RC retained values in
+// registers, the twiddles of the block's rows in LDS; same r order and fma form as the one-thread-per-column
+// kernel it replaces (bit-identical results, 16x the work-groups).
+constexpr int IH_HB = 64;
+template <int RC>
+__global__ __launch_bounds__(256) void idft_h2_kernel(const float2* __restrict__ Y, float2* __restrict__ Z, int H,
+                                                      int R, int m1, int NC) {
+    __shared__ __attribute__((aligned(16))) float2 tw[IH_HB][RC];
+    const int b = blockIdx.z, h0 = blockIdx.y * IH_HB, tid = threadIdx.x, lane = tid & 63, hs = tid >> 6;
+    const int col = blockIdx.x * 64 + lane;
+    const bool ok = col < NC;
+    for (int i = tid; i < IH_HB * RC; i += 256) {
+        const int hh = i / RC, r = i - (i / RC) * RC;
+        tw[hh][r] = (r < R && h0 + hh < H) ? twiddle(row_k1(r, H, R, m1), h0 + hh, H) : make_float2(0.f, 0.f);
+    }
+    float2 y[RC];
+#pragma unroll
+    for (int r = 0; r < RC; ++r) y[r] = (ok && r < R) ? Y[((size_t)b * R + r) * NC + col] : make_float2(0.f, 0.f);
+    __syncthreads();
+    for (int hh = hs; hh < IH_HB && h0 + hh < H; hh += 4) {
+        float re = 0.f, im = 0.f;
+        const f32x4* t4 = reinterpret_cast<const f32x4*>(&tw[hh][0]);
+#pragma unroll
+        for (int q = 0; q < RC / 2; ++q) {
+            const f32x4 t = t4[q];  // e^{+i th} = (c, s) of rows 2q, 2q + 1
+            re = fmaf(y[2 * q].x, t[0], fmaf(-y[2 * q].y, t[1], re));
+            im = fmaf(y[2 * q].x, t[1], fmaf(y[2 * q].y, t[0], im));
+            re = fmaf(y[2 * q + 1].x, t[2], fmaf(-y[2 * q + 1].y, t[3], re));
+            im = fmaf(y[2 * q + 1].x, t[3], fmaf(y[2 * q + 1].y, t[2], im));
+        }
+        if (ok) Z[((size_t)b * H + h0 + hh) * NC + col] = make_float2(re, im);
+    }
+}
+
+inline int rc_for(int R) { return R <= 8 ? 8 : (R <= 16 ? 16 : (R <= 24 ? 24 : 32)); }
+
 // wpack[r][k2][i][o] from weights1/weights2 [Cin][Cout][m1][m2] (complex64)
 __global__ void spec_pack_kernel(const float2* __restrict__ w1, const float2* __restrict__ w2, float2* __restrict__ wp,
                                  int Cin, int Cout, int H, int R, int m1, int m2) {
@@ -182,6 +280,119 @@ __global__ void mix_kernel(const float2* __restrict__ X2, const float2* __restri
 #pragma unroll
             for (int bb = 0; bb < MAXB; ++bb)
                 if (bb < nb) Y[((size_t)(b0 + bb) * nmodes + mode) * Cout + o] = acc[bb];
+        }
+    }
+}
+
+// Y[b][mode][o] = sum_i X2[b][mode][i] * wp[mode][i][o] on the matrix cores (v_mfma_f32_16x16x4_f32: exact
+// fp32 products, fp32 accumulation — the per-mode complex GEMM of proc_fno.py:253-255).  The complex product
+// is the real GEMM Y'^T = W'^T X'^T with (re, im) interleaved on both sides: output row 2o + p (p = 0 re,
+// 1 im), K index 2i + q (q = 0 re, 1 im of X), W'^T[2o+p][2i+q] = Re W if p == q, -Im W if (p, q) = (0, 1),
+// +Im W if (1, 0).  So a 16x16x4 MFMA covers 8 output channels x 16 batch rows x 2 input channels.
+// Work-group (256 threads) = one mode x 64 output channels; wave w owns channels [16w, 16w + 16) of them
+// (two 16x16 tiles); the batch is processed 16 * NBC rows at a time against the same LDS weight chunk, so
+// the weights stream from HBM once for any B <= 16 * NBC.  Weight chunks of MIX_IC input channels
+// ([i][64 o] complex, fp32 in LDS; WT = float2 for the fp32 path, uint32 = packed bf16 (re, im) for the
+// bf16 path) are double-buffered through registers: chunk c + 1 is in flight while chunk c is multiplied.
+constexpr int MIX_IC = 32;   // input channels per weight chunk
+constexpr int MIX_OC = 64;   // output channels per work-group
+
+__device__ __forceinline__ float2 bf16x2_to_float2(unsigned v) {
+    return make_float2(__uint_as_float(v << 16), __uint_as_float(v & 0xffff0000u));
+}
+
+template <typename WT, int NBC>
+__global__ __launch_bounds__(256) void mix_mfma_kernel(const float2* __restrict__ X2, const WT* __restrict__ wp,
+                                                       float2* __restrict__ Y, int B, int nmodes, int Cin, int Cout) {
+    constexpr int WPT = MIX_IC * MIX_OC * (int)sizeof(WT) / (256 * 16);  // 16-B weight pieces per thread
+    static_assert(WPT >= 1 && MIX_IC * MIX_OC * sizeof(WT) % (256 * 16) == 0, "weight chunk split");
+    __shared__ float2 Ws[2][MIX_IC][MIX_OC];          // weight chunk, fp32 complex
+    __shared__ float2 Xs[MIX_IC][16 * NBC + 1];       // X chunk [i][b] (+1: bank offset between rows)
+    const int mode = blockIdx.x;
+    const int o0 = blockIdx.y * MIX_OC;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nchunks = (Cin + MIX_IC - 1) / MIX_IC;
+    const WT* wmode = wp + (size_t)mode * Cin * Cout;
+    // weight piece k of this thread: chunk-local input channel ci, output channel co .. co + 16/sizeof(WT) - 1
+    constexpr int PER_ROW = MIX_OC * (int)sizeof(WT) / 16;  // 16-B pieces per chunk row
+    f32x4 wr[WPT];
+    auto wfetch = [&](int c) {
+#pragma unroll
+        for (int k = 0; k < WPT; ++k) {
+            const int piece = k * 256 + tid;
+            const int ci = piece / PER_ROW, cp = piece - ci * PER_ROW;
+            const int i = c * MIX_IC + ci;
+            const int co = o0 + cp * (16 / (int)sizeof(WT));
+            const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+            // Cout % 4 == 0 (host-checked): a piece is either wholly inside [0, Cout) or wholly outside
+            wr[k] = (i < Cin && co < Cout) ? *reinterpret_cast<const f32x4*>(wmode + (size_t)i * Cout + co) : z;
+        }
+    };
+    auto wstore = [&](int buf) {
+#pragma unroll
+        for (int k = 0; k < WPT; ++k) {
+            const int piece = k * 256 + tid;
+            const int ci = piece / PER_ROW, cp = piece - ci * PER_ROW;
+            if constexpr (sizeof(WT) == 8) {
+                *reinterpret_cast<f32x4*>(&Ws[buf][ci][cp * 2]) = wr[k];
+            } else {  // 4 packed bf16 complex -> fp32 complex
+#pragma unroll
+                for (int e = 0; e < 4; ++e) Ws[buf][ci][cp * 4 + e] = bf16x2_to_float2(__float_as_uint(wr[k][e]));
+            }
+        }
+    };
+    // MFMA lane roles (16x16x4): A row r = lane & 15 -> (o = 2 per-tile pairs: r >> 1, p = r & 1); K index
+    // k = lane >> 4 -> (input channel ic = k >> 1 of the step, q = k & 1); B column = batch b = lane & 15
+    const int r = lane & 15, p = r & 1, k = lane >> 4, ic = k >> 1, q = k & 1;
+    for (int b0 = 0; b0 < B; b0 += 16 * NBC) {
+        f32x4 acc[NBC][2];
+#pragma unroll
+        for (int n = 0; n < NBC; ++n)
+#pragma unroll
+            for (int t = 0; t < 2; ++t) acc[n][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        wfetch(0);
+        for (int c = 0; c < nchunks; ++c) {
+            const int buf = c & 1;
+            __syncthreads();  // buffer `buf` and Xs are free (their readers passed the previous chunk)
+            wstore(buf);
+            for (int e = tid; e < MIX_IC * 16 * NBC; e += 256) {  // X chunk: [i][b]
+                const int ci = e % MIX_IC, bb = e / MIX_IC;
+                const int i = c * MIX_IC + ci, b = b0 + bb;
+                Xs[ci][bb] = (i < Cin && b < B) ? X2[((size_t)b * nmodes + mode) * Cin + i] : make_float2(0.f, 0.f);
+            }
+            if (c + 1 < nchunks) wfetch(c + 1);  // next chunk in flight during this chunk's MFMAs
+            __syncthreads();
+#pragma unroll 4
+            for (int s = 0; s < MIX_IC / 2; ++s) {
+                const int ci = 2 * s + ic;
+                float a[2];
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {
+                    const float2 w = Ws[buf][ci][wave * 16 + t * 8 + (r >> 1)];
+                    a[t] = p == q ? w.x : (p == 0 ? -w.y : w.y);
+                }
+#pragma unroll
+                for (int n = 0; n < NBC; ++n) {
+                    const float2 x = Xs[ci][n * 16 + r];
+                    const float bv = q ? x.y : x.x;
+#pragma unroll
+                    for (int t = 0; t < 2; ++t) acc[n][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t], bv, acc[n][t], 0, 0, 0);
+                }
+            }
+        }
+        // D: column = batch b0 + 16n + (lane & 15); rows (lane >> 4) * 4 + reg = (re, im) of channels
+        // 2 (lane >> 4) and 2 (lane >> 4) + 1 of the tile
+#pragma unroll
+        for (int n = 0; n < NBC; ++n) {
+            const int b = b0 + n * 16 + (lane & 15);
+            if (b >= B) continue;
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const int o = o0 + wave * 16 + t * 8 + 2 * (lane >> 4);
+                float2* y = Y + ((size_t)b * nmodes + mode) * Cout;
+                if (o < Cout) y[o] = make_float2(acc[n][t][0], acc[n][t][1]);
+                if (o + 1 < Cout) y[o + 1] = make_float2(acc[n][t][2], acc[n][t][3]);
+            }
         }
     }
 }
@@ -450,11 +661,34 @@ extern "C" int nps_spectral_dft_w(const nps_src_t* src, int nsrc, int B, int H, 
 extern "C" int nps_spectral_dft_h(const float* X1, float* X2, int B, int H, int m1, int m2, int C, void* stream) {
     NPS_CHECK_ARG(X1 && X2 && B > 0 && H > 0 && m1 > 0 && m1 <= H && m2 > 0 && C > 0, "spectral_dft_h: bad args");
     const int R = H < 2 * m1 ? H : 2 * m1;
+    hipStream_t s = (hipStream_t)stream;
+    const int RC = rc_for(R);
+    const size_t lds2 = sizeof(float2) * RC * (H > 256 ? H : 256);  // max(twiddles, 4 x RC x 64 partials)
+    if (R <= 32 && lds2 <= 96 * 1024) {
+        const int NC = m2 * C;
+        const dim3 grid((NC + 63) / 64, B);
+        const auto* x = reinterpret_cast<const float2*>(X1);
+        auto* y = reinterpret_cast<float2*>(X2);
+        static bool attr = false;
+        if (!attr) {
+            (void)hipFuncSetAttribute((const void*)dft_h2_kernel<32>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+            (void)hipFuncSetAttribute((const void*)dft_h2_kernel<24>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+            attr = true;
+        }
+        switch (RC) {
+            case 8: dft_h2_kernel<8><<<grid, 256, lds2, s>>>(x, y, H, R, m1, NC); break;
+            case 16: dft_h2_kernel<16><<<grid, 256, lds2, s>>>(x, y, H, R, m1, NC); break;
+            case 24: dft_h2_kernel<24><<<grid, 256, lds2, s>>>(x, y, H, R, m1, NC); break;
+            default: dft_h2_kernel<32><<<grid, 256, lds2, s>>>(x, y, H, R, m1, NC); break;
+        }
+        NPS_CHECK_LAUNCH("spectral_dft_h");
+        return 0;
+    }
     const size_t lds = sizeof(float2) * R_CHUNK * H;
     NPS_CHECK_ARG(lds <= 64 * 1024, "spectral_dft_h: H=%d too large", H);
     dim3 grid((m2 * C + 255) / 256, (R + R_CHUNK - 1) / R_CHUNK, B);
-    dft_h_kernel<<<grid, 256, lds, (hipStream_t)stream>>>(reinterpret_cast<const float2*>(X1),
-                                                          reinterpret_cast<float2*>(X2), H, R, m1, m2, C);
+    dft_h_kernel<<<grid, 256, lds, s>>>(reinterpret_cast<const float2*>(X1), reinterpret_cast<float2*>(X2), H, R, m1,
+                                        m2, C);
     NPS_CHECK_LAUNCH("spectral_dft_h");
     return 0;
 }
@@ -475,13 +709,31 @@ extern "C" int nps_spectral_pack_weights(const float* w1, const float* w2, float
 extern "C" int nps_spectral_mix(const float* X2, const float* wpack, float* Y, int B, int R, int m2, int Cin, int Cout,
                                 void* stream) {
     NPS_CHECK_ARG(X2 && wpack && Y && B > 0 && R > 0 && m2 > 0 && Cin > 0 && Cout > 0, "spectral_mix: bad args");
+    hipStream_t s = (hipStream_t)stream;
+    static int use_valu = -1;  // dev knob NPS_MIX_VALU=1: the scalar-FMA mixer (A/B reference)
+    if (use_valu < 0) {
+        const char* e = getenv("NPS_MIX_VALU");
+        use_valu = (e != nullptr && e[0] == '1') ? 1 : 0;
+    }
+    const int nmodes = R * m2;
+    if (!use_valu && (Cout & 3) == 0) {
+        const dim3 grid(nmodes, (Cout + MIX_OC - 1) / MIX_OC);
+        const auto* x = reinterpret_cast<const float2*>(X2);
+        const auto* w = reinterpret_cast<const float2*>(wpack);
+        auto* y = reinterpret_cast<float2*>(Y);
+        if (B <= 16)
+            mix_mfma_kernel<float2, 1><<<grid, 256, 0, s>>>(x, w, y, B, nmodes, Cin, Cout);
+        else
+            mix_mfma_kernel<float2, 2><<<grid, 256, 0, s>>>(x, w, y, B, nmodes, Cin, Cout);
+        NPS_CHECK_LAUNCH("spectral_mix (MFMA)");
+        return 0;
+    }
     const size_t lds = sizeof(float2) * MAXB * Cin;
     NPS_CHECK_ARG(lds <= 64 * 1024, "spectral_mix: Cin=%d too large", Cin);
     const int bs = Cout >= 256 ? 256 : ((Cout + 63) / 64) * 64;
-    dim3 grid(R * m2, (Cout + bs - 1) / bs);
-    mix_kernel<<<grid, bs, lds, (hipStream_t)stream>>>(reinterpret_cast<const float2*>(X2),
-                                                       reinterpret_cast<const float2*>(wpack),
-                                                       reinterpret_cast<float2*>(Y), B, R * m2, Cin, Cout);
+    dim3 grid(nmodes, (Cout + bs - 1) / bs);
+    mix_kernel<<<grid, bs, lds, s>>>(reinterpret_cast<const float2*>(X2), reinterpret_cast<const float2*>(wpack),
+                                     reinterpret_cast<float2*>(Y), B, nmodes, Cin, Cout);
     NPS_CHECK_LAUNCH("spectral_mix");
     return 0;
 }
@@ -490,6 +742,21 @@ extern "C" int nps_spectral_idft_h(const float* Y, float* Z, int B, int H, int m
     NPS_CHECK_ARG(Y && Z && B > 0 && H > 0 && m1 > 0 && m1 <= H && m2 > 0 && Cout > 0, "spectral_idft_h: bad args");
     const int R = H < 2 * m1 ? H : 2 * m1;
     NPS_CHECK_ARG(R <= MAXR, "spectral_idft_h: %d retained rows > %d", R, MAXR);
+    {
+        const int NC = m2 * Cout;
+        const dim3 g2((NC + 63) / 64, (H + IH_HB - 1) / IH_HB, B);
+        hipStream_t s = (hipStream_t)stream;
+        const auto* y = reinterpret_cast<const float2*>(Y);
+        auto* z = reinterpret_cast<float2*>(Z);
+        switch (rc_for(R)) {
+            case 8: idft_h2_kernel<8><<<g2, 256, 0, s>>>(y, z, H, R, m1, NC); break;
+            case 16: idft_h2_kernel<16><<<g2, 256, 0, s>>>(y, z, H, R, m1, NC); break;
+            case 24: idft_h2_kernel<24><<<g2, 256, 0, s>>>(y, z, H, R, m1, NC); break;
+            default: idft_h2_kernel<32><<<g2, 256, 0, s>>>(y, z, H, R, m1, NC); break;
+        }
+        NPS_CHECK_LAUNCH("spectral_idft_h");
+        return 0;
+    }
     const size_t lds = sizeof(float2) * R * H;
     NPS_CHECK_ARG(lds <= 96 * 1024, "spectral_idft_h: H=%d too large", H);
     dim3 grid((m2 * Cout + 255) / 256, 1, B);
