@@ -184,18 +184,23 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--model", default="ufno", choices=list(CFGS))
+    ap.add_argument("--model", default="ufno", choices=list(CFGS) + ["fno3d"],
+                    help="fno3d = BASELINE config C5 (3-D FNO over a 16x128x128 time-bundled volume)")
     ap.add_argument("--res", type=int, default=256)
     ap.add_argument("--num-c", type=int, default=3)
     ap.add_argument("--global-batch", type=int, default=16)
     ap.add_argument("--fno-modes", type=int, default=None)
     ap.add_argument("--cpu-calls", type=int, default=2, help="CPU-baseline sample size (model calls, 0 = skip)")
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="fno3d only: activation / weight storage of the C5 3-D spectral path")
     ap.add_argument("--mode", default="rollout", choices=["rollout", "train"],
                     help="rollout = the headline metric; train = pushforward train_step + backward + RCCL "
                          "all-reduce + Adam (samples/s)")
     args = ap.parse_args()
     if args.mode == "train":
         return run_train(args)
+    if args.model == "fno3d":
+        return run_fno3d(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -269,6 +274,85 @@ def main():
             "loss_last_window": float(losses[-1].item()),
         }
         print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+# BASELINE config C5: FNO-3D processor (proc_fno.py:22-83 with SpectralConv3d :291-376) over a time-bundled
+# (D, H, W) = (16, 128, 128) volume, 64 hidden + 4 conditioning channels, modes (8, 12, 12), 4 blocks
+C5_CFG = dict(num_spatial_dims=3, n_cond=4, hidden_features=64, fno_modes=(8, 12, 12), hidden_blocks=4,
+              cond_mode="concat", fno_kernel_size=1)
+C5_VOL = (16, 128, 128)
+
+
+def run_fno3d(args):
+    """C5 throughput: one step = one FNO-3D processor forward over the batch (16 bundled timesteps per
+    sample), fp32 or bf16 storage; batch-sharded over the ranks like the rollout."""
+    from models.enc_proc_dec_components.proc_fno import FNO
+    from nps_hip import ops
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+    gb = args.global_batch if args.global_batch != 16 else 8  # C5: global batch 8 (one volume per GPU at 8)
+    lo, hi = shard_bounds(gb, world, rank)
+    B = hi - lo
+    torch.manual_seed(42)
+    m = FNO(pde=None, **C5_CFG).to(dev).eval()
+    D, H, W = C5_VOL
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    h = torch.rand(B, C5_CFG["hidden_features"], D * H, W, device=dev, generator=g) * 2 - 1
+    vb = torch.rand(B, C5_CFG["n_cond"], D * H, W, device=dev, generator=g)
+    bf16 = args.dtype == "bf16"
+    # NDHWC (viewed as (B, D*H, W, C)) resident in HBM in the storage dtype before timing
+    hn, vn = ops.nchw_to_nhwc(h), ops.nchw_to_nhwc(vb)
+    if bf16:
+        hn, vn = ops.to_bf16(hn), ops.to_bf16(vn)
+
+    def step():
+        with torch.no_grad():
+            return m.run_bf16(hn, vn, D) if bf16 else m.run(hn, vn, D)
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        y = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    elapsed = max_over_ranks(time.perf_counter() - t0, dev)
+    if rank == 0:
+        # bytes one layer must move at least: input frame read by the pointwise conv and by the W-DFT, the
+        # output written and re-read by the spectral accumulate, the per-mode weights once
+        es = 2 if bf16 else 4
+        Cin, Co = C5_CFG["hidden_features"] + C5_CFG["n_cond"], C5_CFG["hidden_features"]
+        m1, m2, m3 = C5_CFG["fno_modes"]
+        npx = B * D * H * W
+        wbytes = min(D, 2 * m1) * min(H, 2 * m2) * m3 * Cin * Co * (4 if bf16 else 8)
+        layer_bytes = npx * es * (2 * Cin + 3 * Co) + wbytes
+        ms = elapsed / args.steps * 1e3
+        print(json.dumps({
+            "metric": "C5 FNO-3D processor throughput (sample-timesteps/s, 16 time-bundled steps per volume)",
+            "value": round(gb * D * args.steps / elapsed, 3), "unit": "sample-timesteps/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None,
+            "dtype": "bf16 storage, fp32 arithmetic" if bf16 else "f32", "data": "synthetic",
+            "config": {"workload": "FNO-3D (C5) over a 16x128x128 volume, 64 hidden + 4 cond, modes (8,12,12), "
+                                   "4 blocks", "model": "fno3d", "global_batch": gb, "per_gpu_batch": B,
+                       "parallelism": f"dp{world} (batch-sharded, no collective)"},
+            "hbm_bytes_per_step_min": layer_bytes * C5_CFG["hidden_blocks"],
+            "achieved_hbm_TBps": round(layer_bytes * C5_CFG["hidden_blocks"] / (ms * 1e-3) / 1e12, 3),
+            "out_abs_mean": float(y.float().abs().mean())}), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
 

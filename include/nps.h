@@ -192,6 +192,31 @@ int nps_spectral_idft_h(const float* Y, float* Z, int B, int H, int m1, int m2, 
 int nps_spectral_idft_w(const float* Z, float* out, int B, int H, int W, int m2, int Cout, int accumulate,
                         const float* addend, int act, float* out_tag, void* stream);
 
+/* ---- bf16 storage (BASELINE config C5: the 3-D rFFT spectral conv in bf16) ----------------------------
+ * Activations in HBM as bf16 (16-bit storage of NDHWC tensors viewed as (B, D*H, W, C)), every sum in fp32:
+ * the same transforms as the fp32 entry points above.  Replaces the fp32 SpectralConv3d / FNO_Layer chain of
+ * proc_fno.py:291-376, :142-146 for a bf16 model (the reference has no bf16 path: CPU FFT rejects bf16,
+ * SURVEY.md §0.5); parity is checked against the fp32 HIP path, itself pinned to the oracle. */
+int nps_spectral_dft_w_bf16(const nps_src_t* src, int nsrc, int B, int H, int W, int C, int m2, float* X1,
+                            void* stream);
+/* wpack: the nps_spectral(3d)_pack_weights layout with every complex value as a packed bf16 (re, im) pair
+ * (nps_f32_to_bf16 of the fp32 packing) */
+int nps_spectral_mix_bf16(const float* X2, const void* wpack, float* Y, int B, int R, int m2, int Cin, int Cout,
+                          void* stream);
+/* out / addend bf16 [B][H][W][Cout]; out (= or +=) act(c2r(Z)/(H W) + addend) */
+int nps_spectral_idft_w_bf16(const float* Z, void* out, int B, int H, int W, int m2, int Cout, int accumulate,
+                             const void* addend, int act, void* stream);
+/* elementwise conversion (bf16 round-to-nearest-even) */
+int nps_f32_to_bf16(const float* x, long n, void* y, void* stream);
+int nps_bf16_to_f32(const void* x, long n, float* y, void* stream);
+/* pointwise conv (FNO_Layer `w` with kernel 1, proc_fno.py:104-107) in bf16: a->src / a->out / a->addend0 bf16
+ * NHWC (sources covering the frame, all but the last with C % 8 == 0), a->wpack from nps_pack_1x1_bf16
+ * ([Cout][nps_conv1x1_bf16_kr(Cin)] bf16), a->bias fp32, epilogue act(acc + bias + addend0) on
+ * v_mfma_f32_32x32x16_bf16 with fp32 accumulation; Cout in {32, 64, 96, 128, 192, 256}. */
+int nps_conv1x1_bf16_kr(int Cin);
+int nps_pack_1x1_bf16(const float* w, void* wp, int Cout, int Cin, void* stream);
+int nps_conv1x1_bf16(const nps_conv2d_t* a, void* stream);
+
 /* ---- grid encoder / decoder / wrapper ---------------------------------
  * Encoder input packing, enc_grid.py:41-50 + enc_proc_dec.py:127-137:
  * xin[B][H][W][Cp] = [u(B,c,tw,H,W) flattened c*tw | pos(B,H,W,2) | cond(B,K) broadcast | sc(B,S,H,W)],

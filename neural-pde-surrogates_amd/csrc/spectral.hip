@@ -29,13 +29,21 @@ __device__ __forceinline__ float2 twiddle(int k, int n, int N) {
     return make_float2(c, s);  // (cos theta, sin theta), theta = 2 pi k n / N
 }
 
+// Activation element types of the spectral passes: fp32, or bf16 stored as its 16 bits (the bf16 3-D path,
+// BASELINE config C5: bf16 storage, fp32 arithmetic).
+typedef unsigned short bf16_t;
+__device__ __forceinline__ float ld_f(float v) { return v; }
+__device__ __forceinline__ float ld_f(bf16_t v) { return __uint_as_float((unsigned)v << 16); }
+__device__ __forceinline__ void st_f(float* p, float v) { *p = v; }
+__device__ __forceinline__ void st_f(bf16_t* p, float v) { *p = __builtin_bit_cast(bf16_t, (__bf16)v); }
+
 // X1[b][h][k2][c] = sum_w x[b][h][w][c] e^{-2 pi i k2 w / W}
 // With c2r_adj != 0 this is the adjoint of the c2r synthesis (backward of idft_w): every bin is scaled
 // by `scale` and, except DC / Nyquist, doubled (torch irfft backward: rfft(g)/N, columns 1..W-(W//2+1) x2).
 // KC bins per pass (a multiple of 4 >= the retained bins where possible): the twiddle table is laid out
 // [w][KC] so one pixel's KC twiddles are KC/2 broadcast ds_read_b128, and bins past m2 carry zero
 // twiddles (no per-bin branches in the inner loop).
-template <int KC>
+template <int KC, typename TIn = float>
 __global__ void dft_w_kernel(nps_conv2d_t a, int m2, float2* __restrict__ X1, float scale, int c2r_adj) {
     extern __shared__ __attribute__((aligned(16))) float2 tw[];  // [W][KC]
     const int h = blockIdx.x, b = blockIdx.y;
@@ -50,18 +58,18 @@ __global__ void dft_w_kernel(nps_conv2d_t a, int m2, float2* __restrict__ X1, fl
         __syncthreads();
         for (int c = threadIdx.x; c < C; c += blockDim.x) {
             // locate the source of channel c
-            const float* base = nullptr;
+            const TIn* base = nullptr;
             int sc = 0, sC = 1;
             int c0 = 0;
             for (int s = 0; s < a.nsrc; ++s) {
                 if (c >= c0 && c < c0 + a.src[s].C) {
-                    base = a.src[s].ptr;
+                    base = reinterpret_cast<const TIn*>(a.src[s].ptr);
                     sc = c - c0;
                     sC = a.src[s].C;
                 }
                 c0 += a.src[s].C;
             }
-            const float* row = base + ((size_t)(b * H + h) * W) * sC + sc;
+            const TIn* row = base + ((size_t)(b * H + h) * W) * sC + sc;
             float re[KC], im[KC];
 #pragma unroll
             for (int k = 0; k < KC; ++k) re[k] = im[k] = 0.f;
@@ -82,11 +90,11 @@ __global__ void dft_w_kernel(nps_conv2d_t a, int m2, float2* __restrict__ X1, fl
             for (; w0 + WB <= W; w0 += WB) {
                 float v[WB];
 #pragma unroll
-                for (int j = 0; j < WB; ++j) v[j] = row[(size_t)(w0 + j) * sC];
+                for (int j = 0; j < WB; ++j) v[j] = ld_f(row[(size_t)(w0 + j) * sC]);
 #pragma unroll
                 for (int j = 0; j < WB; ++j) bins(v[j], w0 + j);
             }
-            for (; w0 < W; ++w0) bins(row[(size_t)w0 * sC], w0);
+            for (; w0 < W; ++w0) bins(ld_f(row[(size_t)w0 * sC]), w0);
 #pragma unroll
             for (int k = 0; k < KC; ++k) {
                 if (k < nk) {
@@ -426,9 +434,9 @@ __global__ void idft_h_kernel(const float2* __restrict__ Y, float2* __restrict__
 // out[b][h][w][o] (=|+=) act( sum_k c_k Re(Z[b][h][k][o] e^{2 pi i k w / W}) / (H W) [+ addend] )
 // doubling = 0, scale = 1 is the adjoint of the truncated real-input DFT (backward of dft_w):
 // gx[w] = sum_k Re(gX[k] e^{+2 pi i k w / W}).
-template <int KC>
-__global__ void idft_w_kernel(const float2* __restrict__ Z, float* __restrict__ out, int H, int W, int m2, int Cout,
-                              int accumulate, const float* __restrict__ addend, int act, float scale_arg,
+template <int KC, typename TOut = float>
+__global__ void idft_w_kernel(const float2* __restrict__ Z, TOut* __restrict__ out, int H, int W, int m2, int Cout,
+                              int accumulate, const TOut* __restrict__ addend, int act, float scale_arg,
                               int doubling, float* __restrict__ out_tag) {
     extern __shared__ __attribute__((aligned(16))) float2 tw[];  // [chunk][W][KC], zero past m2
     const int h = blockIdx.x, b = blockIdx.y;
@@ -482,21 +490,21 @@ __global__ void idft_w_kernel(const float2* __restrict__ Z, float* __restrict__ 
                     if (act == 1) v = nps::gelu_erf(v);
                     amax = fmaxf(amax, fabsf(v));
                 }
-                out[(rowo + w) * Cout + o] = v;
+                st_f(out + (rowo + w) * Cout + o, v);
             };
             int w0 = 0;
             for (; w0 + WB <= W; w0 += WB) {
                 float prev[WB], add[WB];
                 if (rd_out) {  // uniform branches around straight-line batches of loads
 #pragma unroll
-                    for (int j = 0; j < WB; ++j) prev[j] = out[(rowo + w0 + j) * Cout + o];
+                    for (int j = 0; j < WB; ++j) prev[j] = ld_f(out[(rowo + w0 + j) * Cout + o]);
                 } else {
 #pragma unroll
                     for (int j = 0; j < WB; ++j) prev[j] = 0.f;
                 }
                 if (rd_add) {
 #pragma unroll
-                    for (int j = 0; j < WB; ++j) add[j] = addend[(rowo + w0 + j) * Cout + o];
+                    for (int j = 0; j < WB; ++j) add[j] = ld_f(addend[(rowo + w0 + j) * Cout + o]);
                 } else {
 #pragma unroll
                     for (int j = 0; j < WB; ++j) add[j] = 0.f;
@@ -505,7 +513,8 @@ __global__ void idft_w_kernel(const float2* __restrict__ Z, float* __restrict__ 
                 for (int j = 0; j < WB; ++j) pixel(w0 + j, prev[j], add[j]);
             }
             for (; w0 < W; ++w0)
-                pixel(w0, rd_out ? out[(rowo + w0) * Cout + o] : 0.f, rd_add ? addend[(rowo + w0) * Cout + o] : 0.f);
+                pixel(w0, rd_out ? ld_f(out[(rowo + w0) * Cout + o]) : 0.f,
+                      rd_add ? ld_f(addend[(rowo + w0) * Cout + o]) : 0.f);
         }
     }
     nps::tag_publish(out_tag, amax, nps::wave_salt());
@@ -598,35 +607,38 @@ size_t idft_w_lds(int m2, int W) {
     return sizeof(float2) * ((m2 + kc - 1) / kc) * kc * W;
 }
 
+template <typename TIn = float>
 void launch_dft_w(dim3 grid, int bs, size_t lds, hipStream_t s, const nps_conv2d_t& a, int m2, float2* X1, float scale,
                   int c2r_adj) {
     switch (kc_for(m2)) {
-        case 4: dft_w_kernel<4><<<grid, bs, lds, s>>>(a, m2, X1, scale, c2r_adj); break;
-        case 8: dft_w_kernel<8><<<grid, bs, lds, s>>>(a, m2, X1, scale, c2r_adj); break;
-        case 12: dft_w_kernel<12><<<grid, bs, lds, s>>>(a, m2, X1, scale, c2r_adj); break;
-        default: dft_w_kernel<16><<<grid, bs, lds, s>>>(a, m2, X1, scale, c2r_adj); break;
+        case 4: dft_w_kernel<4, TIn><<<grid, bs, lds, s>>>(a, m2, X1, scale, c2r_adj); break;
+        case 8: dft_w_kernel<8, TIn><<<grid, bs, lds, s>>>(a, m2, X1, scale, c2r_adj); break;
+        case 12: dft_w_kernel<12, TIn><<<grid, bs, lds, s>>>(a, m2, X1, scale, c2r_adj); break;
+        default: dft_w_kernel<16, TIn><<<grid, bs, lds, s>>>(a, m2, X1, scale, c2r_adj); break;
     }
 }
 
-template <int KC>
-void launch_idft_w_kc(dim3 grid, int bs, size_t lds, hipStream_t s, const float2* Z, float* out, int H, int W, int m2,
-                      int C, int accumulate, const float* addend, int act, float scale, int doubling, float* tag) {
+template <int KC, typename TOut>
+void launch_idft_w_kc(dim3 grid, int bs, size_t lds, hipStream_t s, const float2* Z, TOut* out, int H, int W, int m2,
+                      int C, int accumulate, const TOut* addend, int act, float scale, int doubling, float* tag) {
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)idft_w_kernel<KC>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+        (void)hipFuncSetAttribute((const void*)idft_w_kernel<KC, TOut>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  96 * 1024);
         attr_set = true;
     }
-    idft_w_kernel<KC><<<grid, bs, lds, s>>>(Z, out, H, W, m2, C, accumulate, addend, act, scale, doubling, tag);
+    idft_w_kernel<KC, TOut><<<grid, bs, lds, s>>>(Z, out, H, W, m2, C, accumulate, addend, act, scale, doubling, tag);
 }
 
-void launch_idft_w(dim3 grid, int bs, size_t lds, hipStream_t s, const float2* Z, float* out, int H, int W, int m2,
-                   int C, int accumulate, const float* addend, int act, float scale, int doubling,
+template <typename TOut = float>
+void launch_idft_w(dim3 grid, int bs, size_t lds, hipStream_t s, const float2* Z, TOut* out, int H, int W, int m2,
+                   int C, int accumulate, const TOut* addend, int act, float scale, int doubling,
                    float* tag = nullptr) {
     switch (kc_for(m2)) {
-        case 4: launch_idft_w_kc<4>(grid, bs, lds, s, Z, out, H, W, m2, C, accumulate, addend, act, scale, doubling, tag); break;
-        case 8: launch_idft_w_kc<8>(grid, bs, lds, s, Z, out, H, W, m2, C, accumulate, addend, act, scale, doubling, tag); break;
-        case 12: launch_idft_w_kc<12>(grid, bs, lds, s, Z, out, H, W, m2, C, accumulate, addend, act, scale, doubling, tag); break;
-        default: launch_idft_w_kc<16>(grid, bs, lds, s, Z, out, H, W, m2, C, accumulate, addend, act, scale, doubling, tag); break;
+        case 4: launch_idft_w_kc<4, TOut>(grid, bs, lds, s, Z, out, H, W, m2, C, accumulate, addend, act, scale, doubling, tag); break;
+        case 8: launch_idft_w_kc<8, TOut>(grid, bs, lds, s, Z, out, H, W, m2, C, accumulate, addend, act, scale, doubling, tag); break;
+        case 12: launch_idft_w_kc<12, TOut>(grid, bs, lds, s, Z, out, H, W, m2, C, accumulate, addend, act, scale, doubling, tag); break;
+        default: launch_idft_w_kc<16, TOut>(grid, bs, lds, s, Z, out, H, W, m2, C, accumulate, addend, act, scale, doubling, tag); break;
     }
 }
 
@@ -784,6 +796,67 @@ extern "C" int nps_spectral_idft_w(const float* Z, float* out, int B, int H, int
     return 0;
 }
 
+// ---- bf16 storage variants (BASELINE config C5: 3-D rFFT spectral conv in bf16) ------------------------
+// Same transforms with bf16 activations in HBM (read / written as bf16, every sum in fp32) and the packed
+// weights as bf16 complex (re, im) pairs, so the dominant HBM streams — activations and, at small batch,
+// the per-mode weights — move half the bytes.
+extern "C" int nps_spectral_dft_w_bf16(const nps_src_t* src, int nsrc, int B, int H, int W, int C, int m2, float* X1,
+                                       void* stream) {
+    NPS_CHECK_ARG(src && nsrc >= 1 && nsrc <= NPS_MAX_SRC && X1 && B > 0 && H > 0 && W > 0 && m2 > 0 &&
+                      m2 <= W / 2 + 1,
+                  "spectral_dft_w_bf16: bad args (m2=%d W=%d)", m2, W);
+    nps_conv2d_t a = {};
+    a.nsrc = nsrc;
+    int cs = 0;
+    for (int i = 0; i < nsrc; ++i) {
+        NPS_CHECK_ARG(src[i].H == H && src[i].W == W && src[i].off_y == 0 && src[i].off_x == 0,
+                      "spectral_dft_w_bf16: sources must cover the frame");
+        a.src[i] = src[i];
+        cs += src[i].C;
+    }
+    NPS_CHECK_ARG(cs == C, "spectral_dft_w_bf16: channel mismatch");
+    a.Hin = H;
+    a.Win = W;
+    a.Cin = C;
+    const size_t lds = dft_w_lds(m2, W);
+    NPS_CHECK_ARG(lds <= 64 * 1024, "spectral_dft_w_bf16: W=%d too large", W);
+    const int bs = C >= 256 ? 256 : ((C + 63) / 64) * 64;
+    launch_dft_w<bf16_t>(dim3(H, B), bs, lds, (hipStream_t)stream, a, m2, reinterpret_cast<float2*>(X1), 1.f, 0);
+    NPS_CHECK_LAUNCH("spectral_dft_w_bf16");
+    return 0;
+}
+
+extern "C" int nps_spectral_idft_w_bf16(const float* Z, void* out, int B, int H, int W, int m2, int Cout,
+                                        int accumulate, const void* addend, int act, void* stream) {
+    NPS_CHECK_ARG(Z && out && B > 0 && H > 0 && W > 0 && m2 > 0 && m2 <= W / 2 + 1 && Cout > 0,
+                  "spectral_idft_w_bf16: bad args");
+    const size_t lds = idft_w_lds(m2, W);
+    NPS_CHECK_ARG(lds <= 96 * 1024, "spectral_idft_w_bf16: m2*W too large");
+    const int bs = Cout >= 256 ? 256 : ((Cout + 63) / 64) * 64;
+    launch_idft_w<bf16_t>(dim3(H, B), bs, lds, (hipStream_t)stream, reinterpret_cast<const float2*>(Z),
+                          reinterpret_cast<bf16_t*>(out), H, W, m2, Cout, accumulate,
+                          reinterpret_cast<const bf16_t*>(addend), act, 1.0f / ((float)H * (float)W), 1);
+    NPS_CHECK_LAUNCH("spectral_idft_w_bf16");
+    return 0;
+}
+
+extern "C" int nps_spectral_mix_bf16(const float* X2, const void* wpack, float* Y, int B, int R, int m2, int Cin,
+                                     int Cout, void* stream) {
+    NPS_CHECK_ARG(X2 && wpack && Y && B > 0 && R > 0 && m2 > 0 && Cin > 0 && Cout > 0 && (Cout & 3) == 0,
+                  "spectral_mix_bf16: bad args (Cout %% 4 == 0 required)");
+    const int nmodes = R * m2;
+    const dim3 grid(nmodes, (Cout + MIX_OC - 1) / MIX_OC);
+    const auto* x = reinterpret_cast<const float2*>(X2);
+    const auto* w = reinterpret_cast<const unsigned*>(wpack);
+    auto* y = reinterpret_cast<float2*>(Y);
+    if (B <= 16)
+        mix_mfma_kernel<unsigned, 1><<<grid, 256, 0, (hipStream_t)stream>>>(x, w, y, B, nmodes, Cin, Cout);
+    else
+        mix_mfma_kernel<unsigned, 2><<<grid, 256, 0, (hipStream_t)stream>>>(x, w, y, B, nmodes, Cin, Cout);
+    NPS_CHECK_LAUNCH("spectral_mix_bf16");
+    return 0;
+}
+
 // ---- SpectralConv2d backward (autograd conventions of torch.fft) ----------------
 extern "C" int nps_spectral_idft_w_bwd(const float* gy, float* gZ, int B, int H, int W, int m2, int Cout,
                                        void* stream) {
@@ -814,8 +887,8 @@ extern "C" int nps_spectral_dft_w_bwd(const float* gX1, float* gx, int B, int H,
     const size_t lds = idft_w_lds(m2, W);
     NPS_CHECK_ARG(lds <= 96 * 1024, "spectral_dft_w_bwd: m2*W too large");
     const int bs = Cin >= 256 ? 256 : ((Cin + 63) / 64) * 64;
-    launch_idft_w(dim3(H, B), bs, lds, (hipStream_t)stream, reinterpret_cast<const float2*>(gX1), gx, H, W, m2, Cin, 0,
-                  nullptr, 0, 1.0f, 0);
+    launch_idft_w<float>(dim3(H, B), bs, lds, (hipStream_t)stream, reinterpret_cast<const float2*>(gX1), gx, H, W, m2,
+                         Cin, 0, nullptr, 0, 1.0f, 0);
     NPS_CHECK_LAUNCH("spectral_dft_w_bwd");
     return 0;
 }

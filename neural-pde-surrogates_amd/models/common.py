@@ -190,6 +190,16 @@ class Conv3d(_PackedMixin, nn.Conv3d):
         pk = self._packed(lambda w: ops.pack_conv_weight(w.reshape(w.shape[0], w.shape[1], 1, 1)))
         return ops.conv2d(srcs, frame_hw, pk, self.bias, self.out_channels, 1, 1, **kw)
 
+    def run_bf16(self, srcs, act=0, addend=None):
+        """bf16-storage form (C5): bf16 NDHWC sources viewed as (B, D*H, W, C) -> bf16 (B, D*H, W, Cout)."""
+        self._check()
+        w = self.weight
+        key = ("bf16", w.data_ptr(), w._version, str(w.device))
+        if getattr(self, "_pkb_key", None) != key:
+            self._pkb = ops.pack_1x1_bf16(w)
+            self._pkb_key = key
+        return ops.conv1x1_bf16(srcs, self._pkb, self.bias, self.out_channels, act=act, addend=addend)
+
     def run_ad(self, x):
         self._check()
         return ad.Conv2dFn.apply(self.geometry(), x, self.weight.reshape(self.out_channels, self.in_channels, 1, 1),

@@ -62,11 +62,30 @@ class FNO(nn.Module):
             h = layer.run_ad(x, D) if self.num_spatial_dims == 3 else layer.run_ad(x)
         return h
 
+    def run_bf16(self, h, vb, D):
+        """bf16-storage forward of a 3-D FNO (BASELINE config C5): h (B, D*H, W, C), vb (B, D*H, W, K) bf16
+        NDHWC views; every layer in bf16 storage with fp32 arithmetic (FNO_Layer.run_bf16)."""
+        if self.num_spatial_dims != 3:
+            raise NotImplementedError("the bf16 storage path is the 3-D FNO's (config C5)")
+        if self.cond_mode == "film":
+            raise NotImplementedError("FiLM conditioning is not on the MI355X path (twophase cfgs use concat)")
+        for layer in self.fno_layers:
+            srcs = [ops.Src(h)] + ([ops.Src(vb)] if (vb is not None and self.cond_mode == "concat") else [])
+            h = layer.run_bf16(srcs, D)
+        return h
+
     def forward(self, h: torch.Tensor, variables: torch.Tensor = None, variables_broadcast: torch.Tensor = None,
                 pos=None):
         if self.num_spatial_dims == 3:  # (B, C, D, H, W): the layers run on the (B, D*H, W, C) view
             B, C, D, H, W = h.shape
             flat = lambda t: t.reshape(t.shape[0], t.shape[1], D * H, W)
+            if h.dtype == torch.bfloat16:  # bf16 storage (C5); inference only
+                if use_autograd(self):
+                    raise NotImplementedError("the bf16 3-D FNO path is inference-only (fp32 for training)")
+                tob = lambda t: ops.to_bf16(ops.nchw_to_nhwc(ops.to_f32(flat(t))))
+                vb = tob(variables_broadcast) if variables_broadcast is not None else None
+                y = ops.nhwc_to_nchw(ops.to_f32(self.run_bf16(tob(h), vb, D)))
+                return ops.to_bf16(y).reshape(B, y.shape[1], D, H, W)
             if use_autograd(self):
                 vb = ad.to_nhwc(flat(variables_broadcast)) if variables_broadcast is not None else None
                 y = ad.to_nchw(self.run_ad(ad.to_nhwc(flat(h)), vb, D))
@@ -144,6 +163,16 @@ class FNO_Layer(nn.Module):
         if self.conv_mode == "double":
             self.w2.run(srcs, (H, W), out=out, accumulate=True)
         return self.conv.run(srcs, out=out, accumulate=True, act=act)
+
+    def run_bf16(self, srcs, D, act_override=None):
+        """3-D layer in bf16 storage: act(spectral(x) + w(x)) with bf16 sources / output, fp32 sums."""
+        if self.num_spatial_dims != 3 or self.conv_mode != "single":
+            raise NotImplementedError("bf16 storage: 3-D FNO layers with conv_mode 'single' (config C5)")
+        DH, W = srcs[0].t.shape[1:3]
+        self._check_modes((D, DH // D, W))
+        act = activation_code(self.act) if act_override is None else act_override
+        out = self.w.run_bf16(srcs)
+        return self.conv.run_bf16(srcs, D, out=out, accumulate=True, act=act)
 
     def run_ad(self, x, D=None):
         """Differentiable form: x (B,H,W,Cin) materialised frame ((B, D*H, W, Cin) for 3-D layers)."""
@@ -277,6 +306,21 @@ class SpectralConv3d(nn.Module):
             self._pk_key = key
         return self._pk
 
+    def packed_bf16(self, D, H):
+        wp = self.packed(D, H)
+        if getattr(self, "_pkb_src", None) is not wp:
+            self._pkb = ops.to_bf16(wp)
+            self._pkb_src = wp
+        return self._pkb
+
+    def run_bf16(self, srcs, D, out=None, accumulate=False, addend=None, act=0):
+        """bf16-storage form: bf16 NDHWC sources viewed as (B, D*H, W, C) -> bf16 (B, D*H, W, Cout)."""
+        if self.feature_transform:
+            raise NotImplementedError("FiLM spectral conditioning is not on the MI355X path")
+        H = srcs[0].t.shape[1] // D
+        return ops.spectral_conv3d_bf16(srcs, D, self.packed_bf16(D, H), self.modes1, self.modes2, self.modes3,
+                                        self.out_channels, out=out, accumulate=accumulate, addend=addend, act=act)
+
     def run(self, srcs, D, out=None, accumulate=False, addend=None, act=0):
         """srcs: NDHWC sources viewed as (B, D*H, W, C).  Returns (B, D*H, W, Cout)."""
         if self.feature_transform:
@@ -291,6 +335,10 @@ class SpectralConv3d(nn.Module):
         B, C, D, H, W = x.shape
         ops.check_modes3d(D, H, W, self.modes1, self.modes2, self.modes3)
         x4 = x.reshape(B, C, D * H, W)
+        if x.dtype == torch.bfloat16:  # bf16 storage (C5), inference only
+            xb = ops.to_bf16(ops.nchw_to_nhwc(ops.to_f32(x4)))
+            y = ops.nhwc_to_nchw(ops.to_f32(self.run_bf16([ops.Src(xb)], D)))
+            return ops.to_bf16(y).reshape(B, self.out_channels, D, H, W)
         if use_autograd(self):
             y = ad.to_nchw(ad.spectral_conv3d(self, ad.to_nhwc(x4), D))
         else:

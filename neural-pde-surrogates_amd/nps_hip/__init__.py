@@ -110,6 +110,15 @@ _SIGS = {
                                      _i, _i, _vp]),
     "nps_plane_dot": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp]),
     "nps_volume_rescale_bwd": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp, _i, _i, _i, _i, _i, _vp]),
+    # bf16 storage (C5)
+    "nps_spectral_dft_w_bf16": (_i, [ctypes.POINTER(Src), _i, _i, _i, _i, _i, _i, _vp, _vp]),
+    "nps_spectral_mix_bf16": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _vp]),
+    "nps_spectral_idft_w_bf16": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _i, _vp]),
+    "nps_f32_to_bf16": (_i, [_vp, _l, _vp, _vp]),
+    "nps_bf16_to_f32": (_i, [_vp, _l, _vp, _vp]),
+    "nps_conv1x1_bf16_kr": (_i, [_i]),
+    "nps_pack_1x1_bf16": (_i, [_vp, _vp, _i, _i, _vp]),
+    "nps_conv1x1_bf16": (_i, [ctypes.POINTER(Conv2dArgs), _vp]),
     "nps_last_error": (ctypes.c_char_p, []),
     "nps_version": (ctypes.c_char_p, []),
 }
@@ -127,7 +136,7 @@ def check(rc, what):
 
 
 def ptr(t):
-    """Device pointer of an fp32/fp64/complex64 ROCm tensor (None -> NULL)."""
+    """Device pointer of an fp32/fp64/complex64/bf16 ROCm tensor (None -> NULL)."""
     if t is None:
         return None
     if not t.is_cuda:

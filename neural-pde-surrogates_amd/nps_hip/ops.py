@@ -451,6 +451,96 @@ def spectral_conv3d(srcs: Sequence[Src], D: int, wpack: torch.Tensor, m1: int, m
     return out
 
 
+# ------------------------------------------------------------------ bf16 storage (C5) -----
+def _c_src_bf16(srcs: Sequence[Src]):
+    arr = (_CSrc * 3)()
+    for i, s in enumerate(srcs):
+        t = s.t
+        if t.dtype != torch.bfloat16 or not t.is_contiguous() or t.dim() != 4:
+            raise RuntimeError(f"nps_hip: bf16 sources must be contiguous bf16 NHWC, got {t.dtype} {tuple(t.shape)}")
+        arr[i].ptr = ptr(t)
+        arr[i].H, arr[i].W, arr[i].C = t.shape[1], t.shape[2], t.shape[3]
+        arr[i].off_y, arr[i].off_x = int(s.off_y), int(s.off_x)
+    return arr
+
+
+def to_bf16(x: torch.Tensor) -> torch.Tensor:
+    """bf16 copy (round-to-nearest-even) of an fp32 (or complex64, as its (re, im) pairs) device tensor."""
+    x = x.contiguous()
+    xf = torch.view_as_real(x) if x.is_complex() else x
+    out = torch.empty(xf.shape, dtype=torch.bfloat16, device=x.device)
+    check(lib.nps_f32_to_bf16(ptr(xf), xf.numel(), ptr(out), stream_ptr()), "f32_to_bf16")
+    return out
+
+
+def to_f32(x: torch.Tensor) -> torch.Tensor:
+    x = x.contiguous()
+    out = torch.empty(x.shape, dtype=torch.float32, device=x.device)
+    check(lib.nps_bf16_to_f32(ptr(x), x.numel(), ptr(out), stream_ptr()), "bf16_to_f32")
+    return out
+
+
+def pack_1x1_bf16(w: torch.Tensor) -> torch.Tensor:
+    """Pointwise conv weight (Cout, Cin[, 1...]) fp32 -> the bf16 [Cout][KR] packing of nps_conv1x1_bf16."""
+    w = w.detach().reshape(w.shape[0], w.shape[1]).contiguous()
+    Cout, Cin = w.shape
+    out = torch.empty(Cout * lib.nps_conv1x1_bf16_kr(Cin), dtype=torch.bfloat16, device=w.device)
+    check(lib.nps_pack_1x1_bf16(ptr(w), ptr(out), Cout, Cin, stream_ptr()), "pack_1x1_bf16")
+    return out
+
+
+def conv1x1_bf16(srcs: Sequence[Src], wpack: torch.Tensor, bias: Optional[torch.Tensor], Cout: int, act=0,
+                 addend: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """act(w x + bias [+ addend]) of a bf16 NHWC virtual frame (sources covering it) -> bf16 (B, H, W, Cout)."""
+    t0 = srcs[0].t
+    B, H, W = t0.shape[0], t0.shape[1], t0.shape[2]
+    a = Conv2dArgs()
+    a.nsrc = len(srcs)
+    a.src = _c_src_bf16(srcs)
+    a.B, a.Hin, a.Win, a.Cin = B, H, W, sum(s.t.shape[3] for s in srcs)
+    a.KH = a.KW = a.stride = a.dil = 1
+    a.Hout, a.Wout = H, W
+    a.wpack, a.bias, a.Cout = ptr(wpack), ptr(bias), Cout
+    out = torch.empty((B, H, W, Cout), dtype=torch.bfloat16, device=t0.device)
+    a.out, a.out_C, a.out_H, a.out_W, a.out_os = ptr(out), Cout, H, W, 1
+    a.addend0 = ptr(addend)
+    a.act = act
+    check(lib.nps_conv1x1_bf16(ctypes_byref(a), stream_ptr()), "conv1x1_bf16")
+    return out
+
+
+def spectral_conv3d_bf16(srcs: Sequence[Src], D: int, wpack_bf16: torch.Tensor, m1: int, m2: int, m3: int, Cout: int,
+                         out: Optional[torch.Tensor] = None, accumulate=False, addend=None, act=0):
+    """spectral_conv3d with bf16 activations in / out and bf16 packed weights (fp32 spectra and sums)."""
+    t0 = srcs[0].t
+    B, DH, W = t0.shape[0], t0.shape[1], t0.shape[2]
+    H = DH // D
+    Cin = sum(s.t.shape[3] for s in srcs)
+    check_modes3d(D, H, W, m1, m2, m3)
+    if out is None:
+        out = torch.empty((B, DH, W, Cout), dtype=torch.bfloat16, device=t0.device)
+        accumulate = False
+    R1, R2 = min(D, 2 * m1), min(H, 2 * m2)
+    dev = t0.device
+    c64 = torch.complex64
+    X1 = torch.empty((B, D * H, m3, Cin), dtype=c64, device=dev)
+    X2 = torch.empty((B * D, R2, m3, Cin), dtype=c64, device=dev)
+    X3 = torch.empty((B, R1, R2 * m3, Cin), dtype=c64, device=dev)
+    Y = torch.empty((B, R1, R2 * m3, Cout), dtype=c64, device=dev)
+    Z1 = torch.empty((B, D, R2 * m3, Cout), dtype=c64, device=dev)
+    Z2 = torch.empty((B * D, H, m3, Cout), dtype=c64, device=dev)
+    s = stream_ptr()
+    check(lib.nps_spectral_dft_w_bf16(_c_src_bf16(srcs), len(srcs), B, D * H, W, Cin, m3, ptr(X1), s), "dft_w bf16")
+    check(lib.nps_spectral_dft_h(ptr(X1), ptr(X2), B * D, H, m2, m3, Cin, s), "spectral3d dft_h (H)")
+    check(lib.nps_spectral_dft_h(ptr(X2), ptr(X3), B, D, m1, R2 * m3, Cin, s), "spectral3d dft_h (D)")
+    check(lib.nps_spectral_mix_bf16(ptr(X3), ptr(wpack_bf16), ptr(Y), B, R1, R2 * m3, Cin, Cout, s), "mix bf16")
+    check(lib.nps_spectral_idft_h(ptr(Y), ptr(Z1), B, D, m1, R2 * m3, Cout, s), "spectral3d idft_h (D)")
+    check(lib.nps_spectral_idft_h(ptr(Z1), ptr(Z2), B * D, H, m2, m3, Cout, s), "spectral3d idft_h (H)")
+    check(lib.nps_spectral_idft_w_bf16(ptr(Z2), ptr(out), B, D * H, W, m3, Cout, 1 if accumulate else 0, ptr(addend),
+                                       act, s), "idft_w bf16")
+    return out
+
+
 # ------------------------------------------------------------------ data path -----
 def gather_windows(u: torch.Tensor, steps, tw: int, offset: int) -> torch.Tensor:
     """out[b] = u[b][:, steps[b] + offset : steps[b] + offset + tw] for a device-resident trajectory batch
