@@ -7,10 +7,11 @@ python bench.py [--gpus N --steps K --warmup W]
   * strong scaling: a fixed global batch (16) is sharded over the ranks (one process per GPU,
     torchrun); no collective inside the rollout, one barrier + max-reduction of the timings;
   * value = global samples x tw x K / max-over-ranks wall time  [sample-timesteps/s];
-  * roofline: the implicit-GEMM conv kernel (nps_conv2d_fwd = conv2d_fwd_kernel<*>), >99% of the
-    model's flops, timed live with HIP events on its stream during one extra model call after the
-    timed region: achieved = sum(algorithmic conv flops) / sum(kernel durations) vs the 157.3 TF/s
-    fp32 MFMA peak (MI355X_MICROARCH.md);
+  * roofline: the dominant conv class (the split-fp16 implicit-GEMM kernel conv2d_x3_kernel<9,*> at C3),
+    timed live with HIP events on its stream during one extra model call after the timed region:
+    achieved = sum(algorithmic fp32 conv flops) / sum(kernel durations) vs the kernel's fp32-equivalent
+    ceiling, 2.5 PF/s dense f16 MFMA / 3 products (MI355X_MICROARCH.md); traffic = PMC HBM bytes per
+    launch from the committed profiles/pmc_traffic.json (tools/pmc_traffic.sh);
   * cpu_baseline: the CPU oracle (oracle/, the reference restated in fp32 PyTorch-CPU) on a bounded
     sample (2 model calls at B=2) on rank 0 only, with the GPU-vs-CPU rel-L2 of that sample.
 """

@@ -635,21 +635,30 @@ extern "C" int nps_conv2d_plan(nps_conv2d_t* a) {
         // scored by the useful fraction of the launched pixels x the fill of the last round of
         // work-groups over the 256 CUs; 256-pixel tiles carry a 10 % penalty (half the reuse of
         // each weight fragment per global load)
-        const int cand[5][2] = {{16, 32}, {32, 16}, {8, 64}, {16, 16}, {8, 32}};
+        // Wide tiles (8x16, 4x32, 16x8 pixels x 192 channels) replace them for 2x2 / 3x3 convs with
+        // 128 < Cout <= 192: one staged patch feeds all the output channels (dev knob NPS_X3_WIDE=0: off).
+        static int wide_on = -1;
+        if (wide_on < 0) {
+            const char* e = getenv("NPS_X3_WIDE");
+            wide_on = (e != nullptr && e[0] == '0') ? 0 : 1;
+        }
+        const bool wide = wide_on && x3_wide_eligible(*a);
+        const int cand[8][2] = {{16, 32}, {32, 16}, {8, 64}, {16, 16}, {8, 32}, {8, 16}, {4, 32}, {16, 8}};
+        const long units = wide ? (a->Cout + 191) / 192 : units_co;
         int best = -1;
         double best_eff = -1.0;
-        for (int i = 0; i < 5; ++i) {
+        for (int i = wide ? 5 : 0; i < (wide ? 8 : 5); ++i) {
             nps_conv2d_t t = *a;
             t.waves = 8;
             t.TH = cand[i][0];
             t.TW = cand[i][1];
             if (x3_lds_bytes(t) > 160 * 1024) continue;
             const Geo g = make_geo(t);
-            const long wgs = (long)g.tiles_x * g.tiles_y * a->B * units_co;
-            const double useful = (double)a->Hout * a->Wout * a->B * units_co / ((double)wgs * t.TH * t.TW);
+            const long wgs = (long)g.tiles_x * g.tiles_y * a->B * units;
+            const double useful = (double)a->Hout * a->Wout * a->B * units / ((double)wgs * t.TH * t.TW);
             const long rounds = (wgs + 255) / 256;
             const double fill = (double)wgs / (double)(rounds * 256);
-            const double eff = useful * fill * (t.TH * t.TW == 512 ? 1.0 : 0.9);
+            const double eff = useful * fill * (t.TH * t.TW == 256 ? 0.9 : 1.0);
             if (eff > best_eff) {
                 best_eff = eff;
                 best = i;
@@ -782,7 +791,8 @@ extern "C" int nps_conv2d_fwd(const nps_conv2d_t* ap, void* stream) {
                   "conv2d_fwd: precision %d not available for this conv (KH=%d stride=%d dil=%d)", a.precision, a.KH,
                   a.stride, a.dil);
     NPS_CHECK_ARG(a.precision == NPS_PREC_X3F16
-                      ? (a.TH * a.TW == 512 || a.TH * a.TW == 256) && (a.TW == 16 || a.TW == 32 || a.TW == 64)
+                      ? ((a.TH * a.TW == 512 || a.TH * a.TW == 256) && (a.TW == 16 || a.TW == 32 || a.TW == 64)) ||
+                            (a.TH * a.TW == 128 && x3_wide_eligible(a) && (a.TW == 8 || a.TW == 16 || a.TW == 32))
                       : (a.waves == 8 ? (a.TH * a.TW == 256 || a.TH * a.TW == 128) && pc_eligible(a) &&
                                             (a.KH * a.KW != 1 || a.TH * a.TW == 128)
                                       : a.TH * a.TW == 64 * a.waves),

@@ -177,6 +177,21 @@ __device__ __forceinline__ float in_scale_of(const nps_conv2d_t& a) {
     if (a.in_scale == nullptr && a.in_tag1 == nullptr && a.in_tag2 == nullptr) return 1.f;
     return pow2_scale_for(fmaxf(nps::tag_read(a.in_scale), fmaxf(nps::tag_read(a.in_tag1), nps::tag_read(a.in_tag2))));
 }
+// Input scale of a split-fp16 conv whose producers apply a GroupNorm prologue: the staged values are
+// gamma x^ + beta (then GELU, which never raises |v|), and |x^| <= sqrt(N) for a group of N elements
+// (sum x^2 = N var / (var + eps)), so max|gamma| sqrt(N) + max|beta| bounds them whatever the input range.
+// Wave-collective; every wave of the launch computes the same value.
+__device__ __forceinline__ float gn_prologue_scale(const nps_conv2d_t& a) {
+    float gm = 0.f, bm = 0.f;
+    for (int c = threadIdx.x & 63; c < a.Cin; c += 64) {
+        gm = fmaxf(gm, fabsf(a.gn_gamma[c]));
+        bm = fmaxf(bm, fabsf(a.gn_beta[c]));
+    }
+    gm = nps::wave_max(gm);
+    bm = nps::wave_max(bm);
+    const float n = (float)(a.Cin / a.gn_groups) * (float)a.Hin * (float)a.Win;
+    return pow2_scale_for(gm * sqrtf(n) + bm);
+}
 __device__ __forceinline__ bool has_in_scale(const nps_conv2d_t& a) {
     return a.in_scale != nullptr || a.in_tag1 != nullptr || a.in_tag2 != nullptr;
 }
@@ -208,12 +223,22 @@ inline bool x3_sources_aligned(const nps_conv2d_t& a) {
     return true;
 }
 
-constexpr int X3_TPITCH = 68;  // floats per pixel of the LDS-staged output tile (64 channels + pad)
+// The wide split-fp16 tile (192 output channels x 128 pixels per work-group, nps_conv2d_plan): 2x2 / 3x3
+// convs with 128 < Cout <= 192 (Cout % 32 == 0), planned as 128-pixel tiles.
+inline bool x3_wide_eligible(const nps_conv2d_t& a) {
+    const int nt = a.KH * a.KW;
+    return (nt == 4 || nt == 9) && a.Cout > 128 && a.Cout <= 192 && (a.Cout & 31) == 0 && a.dil == 1 &&
+           a.stride == 1 && !a.lattice;
+}
+inline bool x3_wide_tile(const nps_conv2d_t& a) { return a.TH * a.TW == 128; }
+
+// floats per pixel of the LDS-staged output tile: the work-group's channels + 4 (pad)
+inline int x3_tpitch(const nps_conv2d_t& a) { return (x3_wide_tile(a) ? 192 : 64) + 4; }
 
 inline int x3_lds_bytes(const nps_conv2d_t& a) {
     const Geo g = make_geo(a);
     const int ring = X3_NST * ((g.PH * g.PW * X3_PIXB + 15) & ~15);
-    const int tile = a.TH * a.TW * X3_TPITCH * 4;
+    const int tile = a.TH * a.TW * x3_tpitch(a) * 4;
     return 128 + (ring > tile ? ring : tile);
 }
 

@@ -27,10 +27,12 @@ namespace {
 //     (the 3 co-blocks of a tile and neighbouring tiles read the same patch bytes from one L2).
 __host__ __device__ constexpr int x3_patch_px_max(int ntaps, int tile_px) {
     // largest (TH + k - 1) * (TW + k - 1) over the tile shapes nps_conv2d_plan uses for tile_px
-    // (25 taps: 5x5, 256-pixel tiles only — a 512-pixel 5x5 patch ring does not fit LDS)
-    return ntaps == 1    ? tile_px
-           : ntaps == 25 ? (tile_px == 512 ? 12 * 68 : 12 * 36)
-                         : (tile_px == 512 ? (ntaps == 4 ? 9 * 65 : 10 * 66) : (ntaps == 4 ? 9 * 33 : 10 * 34));
+    // (25 taps: 5x5, 256-pixel tiles only — a 512-pixel 5x5 patch ring does not fit LDS; 128-pixel tiles:
+    // the wide kernel, 8x16 / 4x32 / 16x8)
+    return ntaps == 1      ? tile_px
+           : ntaps == 25   ? (tile_px == 512 ? 12 * 68 : 12 * 36)
+           : tile_px == 128 ? (ntaps == 4 ? 5 * 33 : 6 * 34)
+                            : (tile_px == 512 ? (ntaps == 4 ? 9 * 65 : 10 * 66) : (ntaps == 4 ? 9 * 33 : 10 * 34));
 }
 
 #define X3_MFMA __builtin_amdgcn_mfma_f32_32x32x16_f16
@@ -59,22 +61,23 @@ __device__ __forceinline__ bool x3_lds_epilogue(const nps_conv2d_t& a) {
     return !a.out_nchw && (a.out_C & 3) == 0 && (a.Cout & 3) == 0;
 }
 
-// All 512 threads store the work-group's 64-channel x TILE_PX tile from LDS (T[pixel][X3_TPITCH]):
-// 16 consecutive threads cover one pixel's 64 channels (256 contiguous bytes of the NHWC output), with
+// All 512 threads store the work-group's NCO-channel x TILE_PX tile from LDS (T[pixel][NCO + 4]):
+// NCO/4 consecutive threads cover one pixel's NCO channels (one contiguous run of the NHWC output), with
 // the fused bias / addends / GELU / accumulate of store_tile, in the same float order.
-template <int TILE_PX>
+template <int TILE_PX, int NCO>
 __device__ __forceinline__ void x3_store_phase(const nps_conv2d_t& a, int b, int cob, int oy0, int ox0, int lat,
                                                const float* T, int tid, float& amax) {
+    constexpr int Q = NCO / 4;
 #pragma unroll 4
-    for (int i = tid; i < TILE_PX * 16; i += 512) {
-        const int P = i >> 4, q = i & 15;
-        const int co0 = cob * 64 + q * 4;
+    for (int i = tid; i < TILE_PX * Q; i += 512) {
+        const int P = i / Q, q = i - (i / Q) * Q;
+        const int co0 = cob * NCO + q * 4;
         const int ti = P / a.TW, tj = P - (P / a.TW) * a.TW;
         const int oy = oy0 + ti * lat, ox = ox0 + tj * lat;  // lat: dilation-lattice step (1 unless dilated)
         const int dy = oy * a.out_os + a.out_off_y, dx = ox * a.out_os + a.out_off_x;
         if (co0 >= a.Cout || oy >= a.Hout || ox >= a.Wout || dy < 0 || dy >= a.out_H || dx < 0 || dx >= a.out_W)
             continue;
-        const f32x4 acc = *reinterpret_cast<const f32x4*>(T + P * X3_TPITCH + q * 4);
+        const f32x4 acc = *reinterpret_cast<const f32x4*>(T + P * (NCO + 4) + q * 4);
         const size_t o = (((size_t)b * a.out_H + dy) * a.out_W + dx) * a.out_C + co0;
         const f32x4 z = {0.f, 0.f, 0.f, 0.f};
         const f32x4 bi = a.bias ? *reinterpret_cast<const f32x4*>(a.bias + co0) : z;
@@ -98,16 +101,22 @@ __device__ __forceinline__ void x3_store_phase(const nps_conv2d_t& a, int b, int
 
 // PRO: the frame prologue (GroupNorm affine and/or GELU, proc_unet_modern.py:62-99) is applied by the
 // producers while staging, instead of a frame_pack pass in front of the conv.
-template <int NTAPS, int PB, bool PRO>
+// WIDE: the work-group covers 192 output channels x 128 pixels instead of 64 x 4*PB*32: consumer wave w
+// owns channels [96 (w & 1), +96) (3 co blocks) x pixels [64 (w >> 1), +64) (2 pixel blocks).  The staged
+// patch then feeds all 192 channels: 3x less producer work (fetch, split, prologue) and patch traffic per
+// MFMA than three 64-channel work-groups re-staging the same patch.
+template <int NTAPS, int PB, bool PRO, bool WIDE = false>
 __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
     constexpr int KWT = NTAPS == 25 ? 5 : (NTAPS == 9 ? 3 : (NTAPS == 4 ? 2 : 1));
-    constexpr int CBW = 2;
-    constexpr int TILE_PX = 4 * PB * 32;
+    constexpr int CBW = WIDE ? 3 : 2;          // 32-channel co blocks per consumer wave
+    constexpr int PBW = WIDE ? 2 : PB;         // 32-pixel blocks per consumer wave
+    constexpr int NCO = WIDE ? 192 : 64;       // output channels per work-group
+    constexpr int TILE_PX = WIDE ? 128 : 4 * PB * 32;
     constexpr int MAXP = (x3_patch_px_max(NTAPS, TILE_PX) * 4 + 255) / 256;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const Geo g = make_geo(a);
-    const int ncob = (a.Cout + 63) / 64;
+    const int ncob = (a.Cout + NCO - 1) / NCO;
     const int ntiles = g.tiles_x * g.tiles_y;
     const int nwg = ntiles * a.B * ncob;  // work-group tiles of the launch (the grid is persistent)
     // tile l -> (co block, sample, output origin): co block fastest; consecutive tiles of one XCD's
@@ -139,7 +148,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
         // ------------------------------------------------------------------ producers: patch only
         const int ptid = tid - 256;
         const int Hext = a.Hin + 2 * a.circ, Wext = a.Win + 2 * a.circ;
-        const float xs = in_scale_of(a);
+        const float xs = (PRO && a.gn_stats != nullptr) ? gn_prologue_scale(a) : in_scale_of(a);
         // a register set: MAXP patch slots, then (PRO) the stage's GroupNorm operands gamma[4], beta[4]
         // and the group's (sum, sum of squares) as two doubles, fetched with the patch
         constexpr int NR = MAXP + (PRO ? 3 : 0);
@@ -261,7 +270,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
                             }
                             if (a.pre_act == 1) {
 #pragma unroll
-                                for (int e = 0; e < 4; ++e) v[e] = nps::gelu_erf(v[e]);
+                                for (int e = 0; e < 4; ++e) v[e] = nps::gelu_fast(v[e]);
                             }
                         } else {
                             v = z;  // the conv's own zero padding (and channels past Cin)
@@ -308,7 +317,8 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
             }
             barrier();  // the consumers' tile is in LDS
             if (lds_epi)
-                x3_store_phase<TILE_PX>(a, sb, scob, soy0, sox0, g.T, reinterpret_cast<const float*>(ring), tid, pmax);
+                x3_store_phase<TILE_PX, NCO>(a, sb, scob, soy0, sox0, g.T, reinterpret_cast<const float*>(ring), tid,
+                                             pmax);
             barrier();  // every read of the staged tile is done: the ring may be refilled
             if (!more) break;
             l = ln;
@@ -318,20 +328,22 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
     }
 
     // ---------------------------------------------------------------------- consumers
-    int boff[PB];
+    int boff[PBW];
+    const int px0 = WIDE ? (wave >> 1) * 64 : wave * 32 * PB;  // this wave's first tile pixel
+    const int cw0 = WIDE ? (wave & 1) * 96 : 0;                // this wave's first channel in the co group
 #pragma unroll
-    for (int pb = 0; pb < PB; ++pb) {
-        const int P = wave * 32 * PB + pb * 32 + (lane & 31);
+    for (int pb = 0; pb < PBW; ++pb) {
+        const int P = px0 + pb * 32 + (lane & 31);
         const int ti = P / a.TW, tj = P - (P / a.TW) * a.TW;
         boff[pb] = (ti * g.PW + tj) * X3_PIXB + (lane >> 5) * 16;
     }
-    f32x16 acc[CBW][PB];
+    f32x16 acc[CBW][PBW];
     const int ncb = packed_ncb(a.Cout);
     const size_t gstride = (size_t)ncb * 2048;  // bytes per K-group (chunk, tap) of the packed weight
     const int G = nstages * NTAPS;
     const char* wbase = nullptr;
     f16x8 Aw[2][CBW][2];
-    f16x8 Bh[2][PB], Bl[2][PB];
+    f16x8 Bh[2][PBW], Bl[2][PBW];
     auto loadA = [&](int gg, f16x8 (&d)[CBW][2]) {
         const char* p = wbase + (size_t)gg * gstride;
 #pragma unroll
@@ -344,10 +356,10 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
         const int st = gg / NTAPS, tap = gg - (gg / NTAPS) * NTAPS;
         return (st % X3_NST) * stage_b + ((tap / KWT) * g.PW + tap % KWT) * X3_PIXB;
     };
-    auto loadB = [&](int gg, f16x8 (&d)[PB], int half) {
+    auto loadB = [&](int gg, f16x8 (&d)[PBW], int half) {
         const char* p = ring + boffs(gg) + half * 32;
 #pragma unroll
-        for (int pb = 0; pb < PB; ++pb) d[pb] = *reinterpret_cast<const f16x8*>(p + boff[pb]);
+        for (int pb = 0; pb < PBW; ++pb) d[pb] = *reinterpret_cast<const f16x8*>(p + boff[pb]);
     };
     // K-group gg uses weight slot gg & 1 and patch slot gg & 1; the loads of group gg + 1 (weights from
     // global memory, patch from LDS) go to the other slots, interleaved one per MFMA gap.  Loads are
@@ -364,26 +376,26 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
 #pragma unroll
         for (int cb = 0; cb < CBW; ++cb)
 #pragma unroll
-            for (int pb = 0; pb < PB; ++pb) acc[cb][pb] = X3_MFMA(Aw[r][cb][0], Bh[r][pb], acc[cb][pb], 0, 0, 0);
+            for (int pb = 0; pb < PBW; ++pb) acc[cb][pb] = X3_MFMA(Aw[r][cb][0], Bh[r][pb], acc[cb][pb], 0, 0, 0);
 #pragma unroll
         for (int cb = 0; cb < CBW; ++cb)
 #pragma unroll
-            for (int pb = 0; pb < PB; ++pb) acc[cb][pb] = X3_MFMA(Aw[r][cb][0], Bl[r][pb], acc[cb][pb], 0, 0, 0);
+            for (int pb = 0; pb < PBW; ++pb) acc[cb][pb] = X3_MFMA(Aw[r][cb][0], Bl[r][pb], acc[cb][pb], 0, 0, 0);
 #pragma unroll
         for (int cb = 0; cb < CBW; ++cb)
 #pragma unroll
-            for (int pb = 0; pb < PB; ++pb) acc[cb][pb] = X3_MFMA(Aw[r][cb][1], Bh[r][pb], acc[cb][pb], 0, 0, 0);
+            for (int pb = 0; pb < PBW; ++pb) acc[cb][pb] = X3_MFMA(Aw[r][cb][1], Bh[r][pb], acc[cb][pb], 0, 0, 0);
 #pragma unroll
         for (int i = 0; i < 2 * CBW; ++i) {  // weights first: the longest latency gets the most cover
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
             __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // 1 VMEM read
         }
 #pragma unroll
-        for (int i = 0; i < 2 * PB; ++i) {
+        for (int i = 0; i < 2 * PBW; ++i) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
             __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
         }
-        __builtin_amdgcn_sched_group_barrier(0x008, 6 * CBW * PB - 2 * PB - 2 * CBW, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 3 * CBW * PBW - 2 * PBW - 2 * CBW, 0);
         __builtin_amdgcn_sched_barrier(0);
         if ((gg + 1) % NTAPS == 0) {
 #ifdef NPS_X3_STAMP
@@ -397,17 +409,18 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
         __builtin_amdgcn_sched_barrier(0);
     };
     // epilogue scale: undo the exact power-of-2 scales of the weights and the input
-    const float inv = 1.f / (pow2_scale_for(a.wpack[packed_body(a.Cout, a.Cin, NTAPS)]) * in_scale_of(a));
+    const float inv = 1.f / (pow2_scale_for(a.wpack[packed_body(a.Cout, a.Cin, NTAPS)]) *
+                             ((PRO && a.gn_stats != nullptr) ? gn_prologue_scale(a) : in_scale_of(a)));
     const int h = lane >> 5;
     float amax = 0.f;  // max |stored value| over this thread's tiles (out_tag)
     for (int l = blockIdx.x; l < nwg; l += gridDim.x) {
         int cob, b, oy0, ox0;
         decode(l, cob, b, oy0, ox0);
-        wbase = reinterpret_cast<const char*>(a.wpack) + (size_t)cob * CBW * 2048 + lane * 16;
+        wbase = reinterpret_cast<const char*>(a.wpack) + (size_t)(cob * (NCO / 32) + cw0 / 32) * 2048 + lane * 16;
 #pragma unroll
         for (int i = 0; i < CBW; ++i)
 #pragma unroll
-            for (int j = 0; j < PB; ++j)
+            for (int j = 0; j < PBW; ++j)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
         X3_STAMP(0);
@@ -433,23 +446,23 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
             // drop the 64 x TILE_PX tile into LDS, then all 8 waves store it with coalesced 16-B accesses
             float* T = reinterpret_cast<float*>(ring);
 #pragma unroll
-            for (int pb = 0; pb < PB; ++pb) {
-                const int P = wave * 32 * PB + pb * 32 + (lane & 31);
+            for (int pb = 0; pb < PBW; ++pb) {
+                const int P = px0 + pb * 32 + (lane & 31);
 #pragma unroll
                 for (int cb = 0; cb < CBW; ++cb)
 #pragma unroll
                     for (int m = 0; m < 4; ++m) {
                         const f32x4 v = {acc[cb][pb][4 * m] * inv, acc[cb][pb][4 * m + 1] * inv,
                                          acc[cb][pb][4 * m + 2] * inv, acc[cb][pb][4 * m + 3] * inv};
-                        *reinterpret_cast<f32x4*>(T + P * X3_TPITCH + cb * 32 + 8 * m + 4 * h) = v;
+                        *reinterpret_cast<f32x4*>(T + P * (NCO + 4) + cw0 + cb * 32 + 8 * m + 4 * h) = v;
                     }
             }
             barrier();
-            x3_store_phase<TILE_PX>(a, b, cob, oy0, ox0, g.T, T, tid, amax);
+            x3_store_phase<TILE_PX, NCO>(a, b, cob, oy0, ox0, g.T, T, tid, amax);
         } else {
-            static_for<PB>([&](auto pbc) {  // compile-time pb: acc stays in registers
+            static_for<PBW>([&](auto pbc) {  // compile-time pb: acc stays in registers
                 constexpr int pb = decltype(pbc)::value;
-                const int P = wave * 32 * PB + pb * 32 + (lane & 31);
+                const int P = px0 + pb * 32 + (lane & 31);
                 const int ti = P / a.TW, tj = P - (P / a.TW) * a.TW;
                 const int oy = oy0 + ti * g.T, ox = ox0 + tj * g.T;
                 if (oy >= a.Hout || ox >= a.Wout) return;
@@ -460,7 +473,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
                     f32x16 v = acc[cb][pb];
 #pragma unroll
                     for (int r = 0; r < 16; ++r) v[r] *= inv;
-                    store_tile(a, b, cob * 64 + cb * 32, h, v, dy, dx, amax);
+                    store_tile(a, b, cob * NCO + cw0 + cb * 32, h, v, dy, dx, amax);
                     __builtin_amdgcn_sched_barrier(0);
                 }
             });
@@ -891,22 +904,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     nps::tag_publish(a.out_tag, amax, nps::wave_salt());
 }
 
-template <int NT, int PB, bool PRO = false>
+template <int NT, int PB, bool PRO = false, bool WIDE = false>
 void launch_x3_one(const nps_conv2d_t& a, unsigned nwg, int lds, hipStream_t s) {
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)conv2d_x3_kernel<NT, PB, PRO>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
+        (void)hipFuncSetAttribute((const void*)conv2d_x3_kernel<NT, PB, PRO, WIDE>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_set = true;
     }
-    conv2d_x3_kernel<NT, PB, PRO><<<nwg, 512, lds, s>>>(a);
+    conv2d_x3_kernel<NT, PB, PRO, WIDE><<<nwg, 512, lds, s>>>(a);
 }
 
 }  // namespace
 
 int nps_launch_conv2d_x3(const nps_conv2d_t& a, int lds, hipStream_t s) {
     const Geo g = make_geo(a);
-    const long nwg = (long)g.tiles_x * g.tiles_y * a.B * ((a.Cout + 63) / 64);
+    const bool wide = x3_wide_tile(a);  // 192-channel x 128-pixel work-groups (nps_conv2d_plan)
+    const long nwg = (long)g.tiles_x * g.tiles_y * a.B * ((a.Cout + (wide ? 191 : 63)) / (wide ? 192 : 64));
     NPS_CHECK_ARG(nwg < (1L << 31), "conv2d_fwd: grid too large");
     // persistent grid: one 512-thread work-group per CU (the LDS ring takes most of a CU), each walking
     // the tiles l = blockIdx.x, + gridDim.x, ...; a multiple of 8 keeps every work-group's tiles on one XCD
@@ -977,6 +991,16 @@ int nps_launch_conv2d_x3(const nps_conv2d_t& a, int lds, hipStream_t s) {
         else
             conv1x1_x3_kernel<2, 2><<<grid1, 64 * waves, lds1, s>>>(a);
         NPS_CHECK_LAUNCH("conv2d_fwd (split-fp16 1x1)");
+        return 0;
+    }
+    if (wide) {
+        if (a.KH * a.KW == 9)
+            pro ? launch_x3_one<9, 2, true, true>(a, grid, lds, s) : launch_x3_one<9, 2, false, true>(a, grid, lds, s);
+        else if (a.KH * a.KW == 4)
+            launch_x3_one<4, 2, false, true>(a, grid, lds, s);
+        else
+            NPS_CHECK_ARG(false, "conv2d_fwd (split-fp16): wide tiles are 2x2 / 3x3 only");
+        NPS_CHECK_LAUNCH("conv2d_fwd (split-fp16, wide)");
         return 0;
     }
     switch (a.KH * a.KW) {

@@ -36,6 +36,27 @@ __device__ __forceinline__ float gelu_erf(float x) {
     return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
 }
 
+// The same GELU with a branch-free erfc (Numerical Recipes' Chebyshev-fitted erfcc: fractional error < 1.2e-7
+// for every argument, so GELU keeps ~1e-7 relative accuracy on both tails): 0.5 x erfc(|x|/sqrt 2) for x < 0,
+// x - 0.5 x erfc(x/sqrt 2) otherwise; ~15 VALU (one v_rcp, one v_exp) instead of erff's branchy polynomial —
+// for the fused GroupNorm+GELU prologue of the conv producers, which applies it to every staged element.
+__device__ __forceinline__ float gelu_fast(float x) {
+    const float z = fabsf(x) * 0.70710678118654752440f;
+    const float t = __frcp_rn(fmaf(0.5f, z, 1.0f));
+    float p = fmaf(t, 0.17087277f, -0.82215223f);
+    p = fmaf(t, p, 1.48851587f);
+    p = fmaf(t, p, -1.13520398f);
+    p = fmaf(t, p, 0.27886807f);
+    p = fmaf(t, p, -0.18628806f);
+    p = fmaf(t, p, 0.09678418f);
+    p = fmaf(t, p, 0.37409196f);
+    p = fmaf(t, p, 1.00002368f);
+    p = fmaf(t, p, -1.26551223f);
+    const float erfc = t * __expf(fmaf(-z, z, p));
+    const float h = 0.5f * x * erfc;
+    return x < 0.f ? h : x - h;
+}
+
 __device__ __forceinline__ int wrap_mod(int v, int n) {
     int r = v % n;
     return r < 0 ? r + n : r;

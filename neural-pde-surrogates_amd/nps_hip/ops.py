@@ -18,9 +18,10 @@ GELU = 1
 # Conv arithmetic (include/nps.h NPS_PREC_*): exact fp32 MFMA, or the 3-pass split-fp16 MFMA products
 # (~2^-21 relative per product, 5.3x the fp32 MFMA rate) for the stride-1 undilated 1x1 / 2x2 / 3x3 convs.
 PREC_F32, PREC_X3F16 = 0, 1
-# split-fp16 3x3 convs apply their GroupNorm / GELU prologue while staging (nps_conv2d_x3_prologue_ok);
-# — off by default (NPS_FUSE_PROLOGUE=1): the erf-GELU makes the producers the bottleneck
-FUSE_PROLOGUE = os.environ.get("NPS_FUSE_PROLOGUE", "0") == "1"
+# split-fp16 3x3 convs apply their GroupNorm / GELU prologue while staging (nps_conv2d_x3_prologue_ok)
+# instead of a frame_pack pass in front of the conv (dev knob NPS_FUSE_PROLOGUE=0: off).  Pays off on the
+# wide 192-channel tiles, whose producers stage each patch once for all output channels.
+FUSE_PROLOGUE = os.environ.get("NPS_FUSE_PROLOGUE", "1") == "1"
 CONV_PRECISION = PREC_F32 if os.environ.get("NPS_CONV_PRECISION", "x3f16") == "f32" else PREC_X3F16
 
 
@@ -294,7 +295,7 @@ def conv2d(srcs: Sequence[Src], frame_hw, wpack: torch.Tensor, bias: Optional[to
             a.in_scale = ptr(in_scale)
         elif USE_IN_TAGS and not (fused and gn is not None):
             # the sources' tags (a fused GroupNorm prologue normalises the frame: its output range is not
-            # the sources', the normalised values are O(1) and run unscaled)
+            # the sources'; the kernel bounds it from gamma, beta and the group size, gn_prologue_scale)
             tags = [input_tag(s.t) for s in srcs] + [None, None]
             a.in_scale, a.in_tag1, a.in_tag2 = tags[0], tags[1], tags[2]
     if USE_OUT_TAGS:

@@ -130,3 +130,36 @@ def test_accumulating_conv_tag_covers_prior_contents():
     out = base.clone()
     ops.conv2d([ops.Src(x)], (18, 18), wp, None, 16, 3, 3, out=out, out_off=(1, 1), accumulate=True)
     assert ops.tag_value(out) >= float(out.abs().max().cpu()) * (1 - 1e-6)
+
+
+@pytest.mark.parametrize("cout", [192, 64])  # 192: the wide 192-channel tile, 64: the 512-pixel tile
+@pytest.mark.parametrize("xscale,gscale", [(1e-4, 1.0), (7e4, 1e-3), (1.0, 3e2), (1.0, 1e-4)])
+def test_fused_groupnorm_prologue_range(cout, xscale, gscale):
+    """The 3x3 conv applying GroupNorm(8) + GELU while staging its patch (proc_unet_modern.py:62-99): the
+    normalised values do not carry the input's range tag; the kernel scales them from gamma, beta and the
+    group size (gn_prologue_scale), so a GroupNorm affine far from O(1) keeps the fp32 bar."""
+    from nps_hip import ops
+    if not ops.FUSE_PROLOGUE:
+        pytest.skip("fused prologue off (NPS_FUSE_PROLOGUE=0)")
+    torch.manual_seed(7)
+    B, Cin, H, W, G = 2, 192, 34, 30, 8
+    x = torch.randn(B, Cin, H, W) * xscale + 0.3 * xscale
+    gamma = (torch.rand(Cin) + 0.5) * gscale
+    beta = (torch.rand(Cin) - 0.5) * gscale
+    w = torch.randn(cout, Cin, 3, 3) * 0.03
+    b = torch.randn(cout) * 0.1
+    ref = F.conv2d(F.gelu(F.group_norm(x.double(), G, gamma.double(), beta.double(), 1e-5)), w.double(), b.double(),
+                   padding=1)
+    packs = []
+    real_pack = ops.frame_pack
+    try:
+        ops.frame_pack = lambda *a, **k: packs.append(1) or real_pack(*a, **k)
+        xd = ops.nchw_to_nhwc(x.to(DEV))
+        st = ops.group_norm_stats([ops.Src(xd)], (H, W), G)
+        gn = ops.GN(st, gamma.to(DEV), beta.to(DEV), G, 1e-5)
+        y = ops.conv2d([ops.Src(xd)], (H, W), ops.pack_conv_weight(w.to(DEV)), b.to(DEV), cout, 3, 3, pad=(1, 1),
+                       gn=gn, pre_act=1)
+    finally:
+        ops.frame_pack = real_pack
+    assert not packs, "GroupNorm prologue went through frame_pack"
+    assert rel_l2(ops.nhwc_to_nchw(y).cpu(), ref) < TOL, (cout, xscale, gscale)
