@@ -103,6 +103,15 @@ typedef struct {
      * non-negative float bits, one sub-slot per wave) to >= max |value| of every element it writes.
      * Zero it before the first writer (tags are allocated from a zeroed arena, see ops.py). */
     float* out_tag;
+    /* GroupNorm(1) moments of the output (NULL = none): [B][NPS_STATS_SUB][2] fp64 (sum, sum of squares;
+     * the sample's moments are the sum over the sub-slots, which spread the atomics) to which the
+     * conv ADDS, per sample, the moments of the values it stores — an accumulating conv the change of
+     * the moments (stored value minus the value it replaced).  So a zeroed buffer after convs that write
+     * every element of `out` once (a conv, the 4 phases of a transposed conv), or a buffer seeded with
+     * `out`'s moments after an accumulating conv, holds what nps_group_norm_stats(G = 1) would compute
+     * from `out`, without that pass.  Split-fp16 convs with NHWC output and Cout, out_C multiples of 4
+     * only (1x1: Cout <= 192, bias-only epilogue); nps_conv2d_fwd refuses others. */
+    double* out_stats;
 } nps_conv2d_t;
 
 /* Range tags (nps_conv2d_t.in_scale / in_tag* / out_tag): 64 sub-slots 256 B apart, so the atomics of
@@ -110,6 +119,8 @@ typedef struct {
 #define NPS_TAG_SUB 64
 #define NPS_TAG_STRIDE 64
 #define NPS_TAG_FLOATS (NPS_TAG_SUB * NPS_TAG_STRIDE)
+/* sub-slots per sample of a moments buffer (nps_conv2d_t.out_stats) */
+#define NPS_STATS_SUB 16
 
 #define NPS_PREC_F32 0
 #define NPS_PREC_X3F16 1
@@ -167,6 +178,12 @@ int nps_frame_pack(const nps_conv2d_t* a, float* out, void* stream);
  * first (the call does it when zero_first != 0). */
 int nps_group_norm_stats(const nps_src_t* src, int nsrc, int B, int Hin, int Win, int Cin, int G,
                          double* stats, int zero_first, void* stream);
+/* GroupNorm(1) moments of a virtual frame from those of its sources, each covering the frame exactly
+ * (nps_conv2d_t.out_stats) — the per-source moments of torch.cat's GroupNorm (proc_unet_modern.py:235-236):
+ * part i is [B][n_i][2] (n_i sub-slots; p1, p2 may be NULL), out is [B][n_out][2] and receives
+ * out[b][0][k] = sum over parts and sub-slots of p_i[b][s][k] (its other sub-slots are left as they are). */
+int nps_stats_sum(const double* p0, int n0, const double* p1, int n1, const double* p2, int n2, int B, double* out,
+                  int n_out, void* stream);
 
 /* ---- SpectralConv2d forward (proc_fno.py:257-288) ----------------------
  * Truncated DFTs replace rfft2 / irfft2: only the 2*m1 x m2 retained modes

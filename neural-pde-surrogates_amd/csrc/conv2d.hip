@@ -797,6 +797,9 @@ extern "C" int nps_conv2d_fwd(const nps_conv2d_t* ap, void* stream) {
                                             (a.KH * a.KW != 1 || a.TH * a.TW == 128)
                                       : a.TH * a.TW == 64 * a.waves),
                   "conv2d_fwd: tile %dx%d does not match waves=%d", a.TH, a.TW, a.waves);
+    NPS_CHECK_ARG(a.out_stats == nullptr || (a.precision == NPS_PREC_X3F16 && (a.KH * a.KW != 1 || a.Cout <= 192) &&
+                                             !a.out_nchw && (a.out_C & 3) == 0 && (a.Cout & 3) == 0),
+                  "conv2d_fwd: out_stats needs a split-fp16 conv (1x1: Cout <= 192) with an NHWC, 4-aligned output");
     const Geo g = make_geo(a);
     const int lds = lds_bytes(a);
     NPS_CHECK_ARG(lds <= 160 * 1024, "conv2d_fwd: LDS %d B too large", lds);
@@ -916,6 +919,31 @@ extern "C" int nps_group_norm_stats(const nps_src_t* src, int nsrc, int B, int H
     nblk = nblk < 1 ? 1 : (nblk > 96 ? 96 : nblk);
     gn_stats_kernel<<<dim3(nblk, G, B), 256, 0, s>>>(a, G, stats);
     NPS_CHECK_LAUNCH("group_norm_stats");
+    return 0;
+}
+
+namespace {
+__global__ void stats_sum_kernel(const double* __restrict__ p0, int n0, const double* __restrict__ p1, int n1,
+                                 const double* __restrict__ p2, int n2, int B, double* __restrict__ out, int n_out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= 2 * B) return;
+    const int b = i >> 1, k = i & 1;
+    double s = 0.0;
+    for (int j = 0; j < n0; ++j) s += p0[(b * n0 + j) * 2 + k];
+    if (p1)
+        for (int j = 0; j < n1; ++j) s += p1[(b * n1 + j) * 2 + k];
+    if (p2)
+        for (int j = 0; j < n2; ++j) s += p2[(b * n2 + j) * 2 + k];
+    out[b * n_out * 2 + k] = s;
+}
+}  // namespace
+
+extern "C" int nps_stats_sum(const double* p0, int n0, const double* p1, int n1, const double* p2, int n2, int B,
+                             double* out, int n_out, void* stream) {
+    NPS_CHECK_ARG(p0 && out && B > 0 && n0 > 0 && (!p1 || n1 > 0) && (!p2 || n2 > 0) && n_out > 0,
+                  "stats_sum: bad args");
+    stats_sum_kernel<<<(2 * B + 255) / 256, 256, 0, (hipStream_t)stream>>>(p0, n0, p1, n1, p2, n2, B, out, n_out);
+    NPS_CHECK_LAUNCH("stats_sum");
     return 0;
 }
 

@@ -92,9 +92,44 @@ __device__ __forceinline__ f32x4 fetch4(const nps_conv2d_t& a, int b, int y, int
 // any store, then 16-B stores.  Order of the float ops matches the reference:
 // act(acc + bias + addends) or act(acc + bias) + addends, then + out when accumulating.
 // `amax` is raised to max |stored value| (the output's range tag, nps_conv2d_t.out_tag).
+// nps_conv2d_t.out_stats: the GroupNorm(1) moments of the stored values — for an accumulating conv the
+// change of the moments (new value minus the value it replaced), so a buffer seeded with the moments of
+// the tensor before the conv ends with those after it
+__device__ __forceinline__ void stats_add(const nps_conv2d_t& a, float r, float old, double& s1, double& s2) {
+    s1 += (double)r;
+    s2 = fma((double)r, (double)r, s2);
+    if (a.accumulate) {
+        s1 -= (double)old;
+        s2 = fma(-(double)old, (double)old, s2);
+    }
+}
+// Wave-collective: adds the wave's moments of sample b to out_stats (no-op without out_stats), into the
+// sub-slot picked by the wave's global index
+__device__ __forceinline__ void stats_publish(const nps_conv2d_t& a, int b, double s1, double s2) {
+    if (a.out_stats == nullptr) return;
+    s1 = nps::wave_sum(s1);
+    s2 = nps::wave_sum(s2);
+    if ((threadIdx.x & 63) == 0) {
+        double* p = a.out_stats + ((size_t)b * NPS_STATS_SUB + nps::wave_salt() % NPS_STATS_SUB) * 2;
+        atomicAdd(p, s1);
+        atomicAdd(p + 1, s2);
+    }
+}
+
+// store_tile that also accumulates the stored values' moments into (s1, s2) when out_stats is set
+// (NHWC 4-aligned outputs only: nps_conv2d_fwd refuses out_stats otherwise)
+__device__ __forceinline__ void store_tile_s(const nps_conv2d_t& a, int b, int co_base, int h, const f32x16& acc,
+                                             int dy, int dx, float& amax, double& s1, double& s2);
 __device__ __forceinline__ void store_tile(const nps_conv2d_t& a, int b, int co_base, int h, const f32x16& acc,
                                            int dy, int dx, float& amax) {
+    double s1 = 0.0, s2 = 0.0;
+    store_tile_s(a, b, co_base, h, acc, dy, dx, amax, s1, s2);
+}
+__device__ __forceinline__ void store_tile_s(const nps_conv2d_t& a, int b, int co_base, int h, const f32x16& acc,
+                                             int dy, int dx, float& amax, double& s1, double& s2) {
     if (!a.out_nchw && (a.out_C & 3) == 0 && (a.Cout & 3) == 0) {
+        const bool st = a.out_stats != nullptr;
+        float f1 = 0.f, f2 = 0.f;  // this tile's 16 values: fp32 partials (rel. error ~1e-7 of a partial)
         const size_t base = (((size_t)b * a.out_H + dy) * a.out_W + dx) * a.out_C;
         f32x4 bi[4], a0[4], a1[4], o[4];
 #pragma unroll
@@ -121,8 +156,16 @@ __device__ __forceinline__ void store_tile(const nps_conv2d_t& a, int b, int co_
                 if (a.accumulate) v += o[m][e];
                 r[e] = v;
                 amax = fmaxf(amax, fabsf(v));
+                if (st) {
+                    f1 += a.accumulate ? v - o[m][e] : v;
+                    f2 += a.accumulate ? (v - o[m][e]) * (v + o[m][e]) : v * v;
+                }
             }
             *reinterpret_cast<f32x4*>(a.out + base + co0) = r;
+        }
+        if (st) {
+            s1 += (double)f1;
+            s2 += (double)f2;
         }
         return;
     }

@@ -68,6 +68,8 @@ template <int TILE_PX, int NCO>
 __device__ __forceinline__ void x3_store_phase(const nps_conv2d_t& a, int b, int cob, int oy0, int ox0, int lat,
                                                const float* T, int tid, float& amax) {
     constexpr int Q = NCO / 4;
+    const bool st = a.out_stats != nullptr;
+    double s1 = 0.0, s2 = 0.0;  // out_stats: fp64 sum / sum of squares of the stored values
 #pragma unroll 4
     for (int i = tid; i < TILE_PX * Q; i += 512) {
         const int P = i / Q, q = i - (i / Q) * Q;
@@ -96,7 +98,12 @@ __device__ __forceinline__ void x3_store_phase(const nps_conv2d_t& a, int b, int
             amax = fmaxf(amax, fabsf(v));
         }
         *reinterpret_cast<f32x4*>(a.out + o) = r;
+        if (st) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) stats_add(a, r[e], ov[e], s1, s2);
+        }
     }
+    stats_publish(a, b, s1, s2);  // the next GroupNorm(1)'s moments of this sample: one pair per wave
 }
 
 // PRO: the frame prologue (GroupNorm affine and/or GELU, proc_unet_modern.py:62-99) is applied by the
@@ -891,7 +898,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     const int oy = P / a.Wout, ox = P - (P / a.Wout) * a.Wout;
     const int dy = oy * a.out_os + a.out_off_y, dx = ox * a.out_os + a.out_off_x;
     float amax = 0.f;
-    if (P < npx && dy >= 0 && dy < a.out_H && dx >= 0 && dx < a.out_W) {
+    const bool pout = P < npx && dy >= 0 && dy < a.out_H && dx >= 0 && dx < a.out_W;
+    if (pout) {
 #pragma unroll
         for (int cb = 0; cb < NCB; ++cb) {
             if (cb * 32 >= a.Cout) continue;
@@ -902,6 +910,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
         }
     }
     nps::tag_publish(a.out_tag, amax, nps::wave_salt());
+    if (a.out_stats != nullptr) {
+        // moments of the stored values, recomputed from the accumulators (out_stats on a 1x1 conv:
+        // plain epilogue only — bias, no addends / act / accumulate, host-checked); kept out of the store
+        // loop, where the extra live values made this kernel spill
+        double s1 = 0.0, s2 = 0.0;
+        if (pout) {
+#pragma unroll
+            for (int cb = 0; cb < NCB; ++cb) {
+                if (cb * 32 >= a.Cout) continue;
+                float f1 = 0.f, f2 = 0.f;
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    const int co0 = cb * 32 + 8 * m + 4 * h;
+                    if (co0 >= a.Cout) continue;
+                    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+                    const f32x4 bi = a.bias ? *reinterpret_cast<const f32x4*>(a.bias + co0) : z;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const float r = acc[cb][4 * m + e] * inv + bi[e];
+                        f1 += r;
+                        f2 += r * r;
+                    }
+                }
+                s1 += (double)f1;
+                s2 += (double)f2;
+            }
+        }
+        stats_publish(a, b, s1, s2);
+    }
 }
 
 template <int NT, int PB, bool PRO = false, bool WIDE = false>
@@ -960,6 +997,10 @@ int nps_launch_conv2d_x3(const nps_conv2d_t& a, int lds, hipStream_t s) {
             const char* e = getenv("NPS_X3_1X1_WL");
             wl = (e != nullptr && e[0] == '0') ? 0 : 1;
         }
+        NPS_CHECK_ARG(a.out_stats == nullptr || (wl && a.Cout <= 192 && !a.accumulate && !a.addend0 && !a.addend1 &&
+                                                 a.act == 0),
+                      "conv2d_fwd (split-fp16 1x1): out_stats needs the LDS-weight kernel (Cout <= 192) and a "
+                      "plain epilogue (bias only)");
         if (wl && a.Cout <= 192) {  // (Cout 193..256 measured slower with 8 blocks per wave: co-block waves)
             const long nb = ((long)a.Hout * a.Wout + 127) / 128;
             NPS_CHECK_ARG(nb < (1L << 31) && a.B < 65536, "conv2d_fwd: grid too large");

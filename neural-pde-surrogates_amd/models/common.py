@@ -150,11 +150,12 @@ class ConvTranspose2d(_PackedMixin, nn.ConvTranspose2d):
         Ho, Wo = 2 * Hp + 2 - 2 * p, 2 * Wp + 2 - 2 * p
         out = ops.empty_nhwc(B, Ho, Wo, self.out_channels, x)
         phases = self._packed(ops.pack_convT_phases)
+        st = ops.new_stats(B, x)  # the 4 phases store every output element once: GroupNorm(1) moments of out
         for ph in range(4):
             py, px = ph >> 1, ph & 1
             ops.conv2d([ops.Src(x)], (H, W), phases[ph], self.bias, self.out_channels, 2, 2, pad=(1, 1), circ=c,
-                       out_hw=(Hp + 1, Wp + 1), out=out, out_os=2, out_off=(py - p, px - p), act=act)
-        return out
+                       out_hw=(Hp + 1, Wp + 1), out=out, out_os=2, out_off=(py - p, px - p), act=act, out_stats=st)
+        return ops.attach_stats(out, st)
 
     def forward(self, x):
         if use_autograd(self):

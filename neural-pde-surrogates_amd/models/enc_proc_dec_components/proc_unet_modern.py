@@ -213,13 +213,24 @@ class ResidualBlock(nn.Module):
         gn1 = gn2 = None
         if isinstance(self.norm1, nn.GroupNorm):
             gn1 = _gn_args(self.norm1, ops.group_norm_stats(srcs, (H, W), self.norm1.num_groups))
-        h1 = self.conv1.run(srcs, (H, W), gn=gn1, pre_act=act)
+        # conv1 adds norm2's moments of h1 as it stores it (ops.conv2d out_stats): no statistics pass
+        st1 = ops.new_stats(srcs[0].t.shape[0], srcs[0].t) if isinstance(self.norm2, nn.GroupNorm) else None
+        h1 = self.conv1.run(srcs, (H, W), gn=gn1, pre_act=act, out_stats=st1)
+        if st1 is not None:
+            ops.attach_stats(h1, st1)
+        # The block output's moments (the next block's norm1): those of the shortcut output — x's own for
+        # the identity, else added by the 1x1 conv — then conv2, accumulating at its crop offset, adds
+        # the change it makes (nps_conv2d_t.out_stats)
+        st2 = None
         if isinstance(self.shortcut, nn.Identity):
             if len(srcs) != 1 or srcs[0].off_y or srcs[0].off_x or tuple(srcs[0].t.shape[1:3]) != (H, W):
                 raise RuntimeError("identity shortcut on a concatenated input")
             out = ops.share_tag(srcs[0].t.clone(), srcs[0].t)  # conv2 accumulates into it: same bound
+            if isinstance(self.norm1, nn.GroupNorm):
+                st2 = ops.copy_stats(ops.source_stats(srcs[0].t))
         else:
-            out = self.shortcut.run(srcs, (H, W))
+            st2 = ops.new_stats(srcs[0].t.shape[0], srcs[0].t) if isinstance(self.norm1, nn.GroupNorm) else None
+            out = self.shortcut.run(srcs, (H, W), out_stats=st2)
         H1, W1 = h1.shape[1:3]
         if isinstance(self.norm2, nn.GroupNorm):
             gn2 = _gn_args(self.norm2, ops.group_norm_stats([ops.Src(h1)], (H1, W1), self.norm2.num_groups))
@@ -227,7 +238,10 @@ class ResidualBlock(nn.Module):
         H2 = (H1 + 2 * circ + lo[0] + hi[0] - d * (KH - 1) - 1) // s + 1
         W2 = (W1 + 2 * circ + lo[1] + hi[1] - d * (KW - 1) - 1) // s + 1
         oy, ox = crop_offsets((H2, W2), out.shape[1:3])
-        self.conv2.run([ops.Src(h1)], (H1, W1), gn=gn2, pre_act=act, out=out, out_off=(oy, ox), accumulate=True)
+        self.conv2.run([ops.Src(h1)], (H1, W1), gn=gn2, pre_act=act, out=out, out_off=(oy, ox), accumulate=True,
+                       out_stats=st2)
+        if st2 is not None:
+            ops.attach_stats(out, st2)
         return out
 
     def run_ad(self, srcs, frame_hw):
@@ -387,7 +401,8 @@ class Downsample(nn.Module):
                 num_spatial_dims, in_channels=n_cond, out_channels=n_cond, kernel_size=3, stride=2, **padding_kwargs)
 
     def run(self, x, vb):
-        h = self.conv.run([ops.Src(x)], x.shape[1:3])
+        st = ops.new_stats(x.shape[0], x)  # the next ResidualBlock's norm1 moments of h
+        h = ops.attach_stats(self.conv.run([ops.Src(x)], x.shape[1:3], out_stats=st), st)
         if vb is not None:
             vb = self.conv_variables_broadcast.run([ops.Src(vb)], vb.shape[1:3])
         return h, vb

@@ -47,7 +47,7 @@ class Conv2dArgs(ctypes.Structure):
         ("act", ctypes.c_int), ("add_after_act", ctypes.c_int),
         ("TH", ctypes.c_int), ("TW", ctypes.c_int), ("lattice", ctypes.c_int), ("waves", ctypes.c_int),
         ("precision", ctypes.c_int), ("in_scale", ctypes.c_void_p), ("in_tag1", ctypes.c_void_p),
-        ("in_tag2", ctypes.c_void_p), ("out_tag", ctypes.c_void_p),
+        ("in_tag2", ctypes.c_void_p), ("out_tag", ctypes.c_void_p), ("out_stats", ctypes.c_void_p),
     ]
 
 
@@ -74,6 +74,7 @@ _SIGS = {
     "nps_frame_pack": (_i, [ctypes.POINTER(Conv2dArgs), _vp, _vp]),
     "nps_space_to_depth": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp]),
     "nps_group_norm_stats": (_i, [ctypes.POINTER(Src), _i, _i, _i, _i, _i, _i, _vp, _i, _vp]),
+    "nps_stats_sum": (_i, [_vp, _i, _vp, _i, _vp, _i, _i, _vp, _i, _vp]),
     "nps_spectral_dft_w": (_i, [ctypes.POINTER(Src), _i, _i, _i, _i, _i, _i, _vp, _vp]),
     "nps_spectral_dft_h": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp]),
     "nps_spectral_pack_weights": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _vp]),

@@ -23,6 +23,7 @@ PREC_F32, PREC_X3F16 = 0, 1
 # wide 192-channel tiles, whose producers stage each patch once for all output channels.
 FUSE_PROLOGUE = os.environ.get("NPS_FUSE_PROLOGUE", "1") == "1"
 CONV_PRECISION = PREC_F32 if os.environ.get("NPS_CONV_PRECISION", "x3f16") == "f32" else PREC_X3F16
+X1_LDS_WEIGHTS = os.environ.get("NPS_X3_1X1_WL", "1")[:1] != "0"  # (libnps_hip's dev knob of the same name)
 
 
 def conv_precision(KH, KW, stride=1, dil=1):
@@ -138,6 +139,70 @@ def input_tag(t: torch.Tensor) -> int:
     return p
 
 
+# ------------------------------------------------------------ GroupNorm(1) moments ----
+# A split-fp16 2x2/3x3 conv that writes a whole tensor can add the per-sample (sum, sum of squares) of
+# the values it stores to a zeroed fp64 [B][2] buffer (nps_conv2d_t.out_stats).  The tensor then CARRIES
+# its moments (attach_stats), and the GroupNorm(1) of a frame made of such tensors (ResidualBlock.norm1 /
+# norm2, proc_unet_modern.py:235-236) is their sum — no statistics pass over the frame.  Sources without
+# moments get them from one nps_group_norm_stats pass over that source alone, kept for later frames.
+# Moments are valid while the tensor is unchanged: torch's in-place ops bump t._version, and the HIP ops
+# that write into an existing tensor drop them (drop_stats).
+STATS_SUB = 16  # NPS_STATS_SUB
+
+
+def new_stats(B: int, like: torch.Tensor, sub: int = STATS_SUB) -> torch.Tensor:
+    """A zeroed fp64 [B][sub][2] moments buffer: sub = NPS_STATS_SUB for nps_conv2d_t.out_stats, 1 for the
+    [B][G][2] statistics a GroupNorm prologue reads (G = 1)."""
+    return torch.zeros((B, sub, 2), dtype=torch.float64, device=like.device)
+
+
+def _stats_sum(parts, B, out):
+    """out[b][0] = sum of the parts' (sum, sum of squares) over their sub-slots (nps_stats_sum)."""
+    p = list(parts) + [None] * (3 - len(parts))
+    n = [t.shape[1] if t is not None else 0 for t in p]
+    check(lib.nps_stats_sum(ptr(p[0]), n[0], ptr(p[1]), n[1], ptr(p[2]), n[2], B, ptr(out), out.shape[1],
+                            stream_ptr()), "stats_sum")
+    return out
+
+
+def attach_stats(t: torch.Tensor, st: torch.Tensor) -> torch.Tensor:
+    """Record that st holds t's GroupNorm(1) moments (every element of t was added exactly once)."""
+    if not getattr(st, "_nps_incomplete", False):
+        t._nps_stats = (st, t._version)
+    return t
+
+
+def drop_stats(t: torch.Tensor):
+    if getattr(t, "_nps_stats", None) is not None:
+        t._nps_stats = None
+
+
+def stats_of(t: torch.Tensor) -> Optional[torch.Tensor]:
+    """t's live GroupNorm(1) moments, or None."""
+    rec = getattr(t, "_nps_stats", None)
+    if rec is None:
+        return None
+    st, ver = rec
+    return st if ver == t._version else None
+
+
+def source_stats(t: torch.Tensor) -> torch.Tensor:
+    """t's GroupNorm(1) moments: carried, or one nps_group_norm_stats pass (then carried).  Read-only:
+    seed a buffer of your own with copy_stats() to accumulate into."""
+    st = stats_of(t)
+    if st is None:
+        st = new_stats(t.shape[0], t, 1)
+        check(lib.nps_group_norm_stats(_c_src([Src(t)]), 1, t.shape[0], t.shape[1], t.shape[2], t.shape[3], 1,
+                                       ptr(st), 0, stream_ptr()), "group_norm_stats (source)")
+        attach_stats(t, st)
+    return st
+
+
+def copy_stats(st: torch.Tensor) -> torch.Tensor:
+    """A new out_stats buffer seeded with st's moments (to accumulate a conv's changes into)."""
+    return _stats_sum([st], st.shape[0], new_stats(st.shape[0], st))
+
+
 def _c_src(srcs: Sequence[Src]):
     arr = (_CSrc * 3)()
     for i, s in enumerate(srcs):
@@ -221,8 +286,17 @@ class GN(NamedTuple):
 
 
 def group_norm_stats(srcs: Sequence[Src], frame_hw, groups: int) -> torch.Tensor:
+    """(B, groups, 2) fp64 (sum, sum of squares) of the virtual frame's groups — the moments of
+    nn.GroupNorm.  GroupNorm(1) of sources that each lie wholly inside the frame (crop_Nd zero-pads them,
+    it does not cut them): the sum of the sources' carried moments (source_stats)."""
     t0 = srcs[0].t
     B = t0.shape[0]
+    if groups == 1 and all(0 <= s.off_y and s.off_y + s.t.shape[1] <= frame_hw[0] and
+                           0 <= s.off_x and s.off_x + s.t.shape[2] <= frame_hw[1] for s in srcs):
+        parts = [source_stats(s.t) for s in srcs]
+        if len(parts) == 1 and parts[0].shape[1] == 1:
+            return parts[0]
+        return _stats_sum(parts, B, new_stats(B, t0, 1))
     Cin = sum(s.t.shape[3] for s in srcs)
     stats = torch.empty((B, groups, 2), dtype=torch.float64, device=t0.device)
     check(lib.nps_group_norm_stats(_c_src(srcs), len(srcs), B, frame_hw[0], frame_hw[1], Cin, groups, ptr(stats), 1,
@@ -234,9 +308,11 @@ def conv2d(srcs: Sequence[Src], frame_hw, wpack: torch.Tensor, bias: Optional[to
            KW: int, stride=1, dil=1, pad=(0, 0), circ=0, out_hw=None, gn: Optional[GN] = None, pre_act=0,
            out: Optional[torch.Tensor] = None, out_nchw=False, out_os=1, out_off=(0, 0), accumulate=False,
            addends: Sequence[torch.Tensor] = (), act=0, add_after_act=False, pad_bottom=None,
-           in_scale: Optional[torch.Tensor] = None):
+           in_scale: Optional[torch.Tensor] = None, out_stats: Optional[torch.Tensor] = None):
     """One fused conv launch.  `pad` = top/left zero padding (in the circularly
-    extended frame), `pad_bottom` defaults to `pad`.  Returns `out`."""
+    extended frame), `pad_bottom` defaults to `pad`.  `out_stats`: a new_stats() buffer the launch adds
+    the GroupNorm(1) moments of its stored values to (marked incomplete when this conv's kernel cannot;
+    attach_stats then ignores it).  Returns `out`."""
     t0 = srcs[0].t
     B = t0.shape[0]
     Hin, Win = int(frame_hw[0]), int(frame_hw[1])
@@ -262,6 +338,8 @@ def conv2d(srcs: Sequence[Src], frame_hw, wpack: torch.Tensor, bias: Optional[to
     if Hout <= 0 or Wout <= 0:
         raise RuntimeError(f"nps_hip conv2d: empty output {Hout}x{Wout} for input {Hin}x{Win} k={KH}")
     out_given = out is not None
+    if out_given:
+        drop_stats(out)
     if out is None:
         out = (torch.empty((B, Cout, Hout, Wout), dtype=torch.float32, device=t0.device) if out_nchw
                else empty_nhwc(B, Hout, Wout, Cout, t0))
@@ -300,6 +378,13 @@ def conv2d(srcs: Sequence[Src], frame_hw, wpack: torch.Tensor, bias: Optional[to
             a.in_scale, a.in_tag1, a.in_tag2 = tags[0], tags[1], tags[2]
     if USE_OUT_TAGS:
         a.out_tag = out_tag(out, accumulate) if out_given else new_tag(out)
+    if out_stats is not None:
+        plain = not accumulate and not ads and act == 0
+        if (a.precision == PREC_X3F16 and (KH * KW != 1 or (Cout <= 192 and X1_LDS_WEIGHTS and plain))
+                and not out_nchw and oC % 4 == 0 and Cout % 4 == 0):
+            a.out_stats = ptr(out_stats)
+        else:
+            out_stats._nps_incomplete = True
     if lib.nps_conv2d_plan(ctypes_byref(a)) < 0:
         raise RuntimeError("conv2d_plan failed: " + lib.nps_last_error().decode())
     if conv_probe is not None:
@@ -377,6 +462,8 @@ def spectral_conv2d(srcs: Sequence[Src], wpack: torch.Tensor, m1: int, m2: int, 
     X2 = torch.empty((B, R, m2, Cin), dtype=torch.complex64, device=dev)
     Y = torch.empty((B, R, m2, Cout), dtype=torch.complex64, device=dev)
     Z = torch.empty((B, H, m2, Cout), dtype=torch.complex64, device=dev)
+    if out is not None:
+        drop_stats(out)
     if out is None:
         out = empty_nhwc(B, H, W, Cout, t0)
         accumulate = False
@@ -445,6 +532,8 @@ def spectral_conv3d(srcs: Sequence[Src], D: int, wpack: torch.Tensor, m1: int, m
     H = DH // D
     Cin = sum(s.t.shape[3] for s in srcs)
     check_modes3d(D, H, W, m1, m2, m3)
+    if out is not None:
+        drop_stats(out)
     if out is None:
         out = empty_nhwc(B, DH, W, Cout, t0)
         accumulate = False
@@ -518,6 +607,8 @@ def spectral_conv3d_bf16(srcs: Sequence[Src], D: int, wpack_bf16: torch.Tensor, 
     H = DH // D
     Cin = sum(s.t.shape[3] for s in srcs)
     check_modes3d(D, H, W, m1, m2, m3)
+    if out is not None:
+        drop_stats(out)
     if out is None:
         out = torch.empty((B, DH, W, Cout), dtype=torch.bfloat16, device=t0.device)
         accumulate = False

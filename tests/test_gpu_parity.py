@@ -129,6 +129,53 @@ def test_residual_block_fused_prologue(monkeypatch, pm):
     assert rel_l2(y, ref) < TOL
 
 
+def _moments(t):
+    """fp64 (sum, sum of squares) per sample.  The carried moments match to ~1e-8 relative: the epilogues
+    sum in fp64, nps_group_norm_stats (the seed of an identity shortcut's) sums fp32 quads first."""
+    x = t.detach().cpu().double().reshape(t.shape[0], -1)
+    return torch.stack([x.sum(1), (x * x).sum(1)], 1)
+
+
+@pytest.mark.parametrize("C", [192, 32])  # 192: wide 192-channel tiles, 32: 64-channel tiles
+def test_groupnorm_moments_carried_by_conv_epilogues(C):
+    """GroupNorm(1) moments (proc_unet_modern.py:235-236) produced by the epilogues of the convs that write
+    a tensor (ResidualBlock conv2 accumulating onto its shortcut, the 4 transposed-conv phases, the
+    space-to-depth Downsample conv) equal the fp64 sums of the stored tensor, and the next block's
+    GroupNorm reads them without a statistics pass over its frame."""
+    from models.common import ConvTranspose2d_padded
+    from models.enc_proc_dec_components.proc_unet_modern import Downsample, ResidualBlock
+    from nps_hip import ops
+    if ops.CONV_PRECISION != ops.PREC_X3F16:
+        pytest.skip("moments come from the split-fp16 epilogues")
+    torch.manual_seed(4)
+    pk = dict(padding_mode="circular")
+    rb1 = ResidualBlock(C, C, activation=_gelu(), norm=True, num_spatial_dims=2, padding_kwargs=pk).to(DEV)
+    rb2 = ResidualBlock(C + 4, C, activation=_gelu(), norm=True, num_spatial_dims=2, padding_kwargs=pk).to(DEV)
+    up = ConvTranspose2d_padded(1, C, C, kernel_size=4, stride=2).to(DEV)
+    down = Downsample(C, 2, 0, pk).to(DEV)
+    x = ops.nchw_to_nhwc(torch.randn(2, C, 18, 20, device=DEV))
+    h = rb1.run([ops.Src(x)], (18, 20))
+    assert torch.allclose(ops.stats_of(h).sum(1).cpu(), _moments(h), rtol=1e-7, atol=1e-4)
+    u = up.run(h)                                         # (2 * (18 + 2) + 2) x (2 * (20 + 2) + 2)
+    assert tuple(u.shape[1:3]) == (42, 46)
+    assert torch.allclose(ops.stats_of(u).sum(1).cpu(), _moments(u), rtol=1e-7, atol=1e-4)
+    v = ops.nchw_to_nhwc(torch.rand(2, 4, 42, 46, device=DEV))
+    passes = []
+    real = ops.lib.nps_group_norm_stats
+    try:
+        ops.lib.nps_group_norm_stats = lambda *a: passes.append(a[1]) or real(*a)
+        y = rb2.run([ops.Src(u), ops.Src(v)], (42, 46))   # norm1 over cat(u, v): u's moments + one pass over v
+    finally:
+        ops.lib.nps_group_norm_stats = real
+    assert passes == [1], passes                          # only v (untagged) was read for statistics
+    d = down.run(y, None)[0]
+    assert torch.allclose(ops.stats_of(d).sum(1).cpu(), _moments(d), rtol=1e-7, atol=1e-4)
+    # the block output against the oracle on the same inputs
+    ref = Fo.residual_block({k: t.detach().cpu() for k, t in rb2.state_dict().items()}, "",
+                            torch.cat([ops.nhwc_to_nchw(u).cpu(), ops.nhwc_to_nchw(v).cpu()], 1), True, pk)
+    assert rel_l2(ops.nhwc_to_nchw(y).cpu(), ref) < TOL
+
+
 # ------------------------------------------------------------------ spectral
 @pytest.mark.parametrize("name", ["spectral2d_a", "spectral2d_overlap", "spectral2d_nyq"])
 def test_spectral2d_golden(name):
