@@ -67,23 +67,36 @@ def build_model(kind, res, num_c, device, fno_modes=None, seed=42):
 
 # dense MFMA peaks, MI355X_MICROARCH.md: f32 (v_mfma_f32_32x32x2_f32) 157.3 TF; f16 2.5 PF.  A split-fp16
 # conv spends 3 f16 MFMA products per algorithmic fp32 product, so its fp32-equivalent ceiling is 2.5 PF / 3.
-PEAK_TFLOPS = {"f32": FP32_MFMA_PEAK_TFLOPS, "x3f16": 2500.0 / 3.0}
+PEAK_TFLOPS = {"f32": FP32_MFMA_PEAK_TFLOPS, "x3f16": 2500.0 / 3.0, "f32w": FP32_MFMA_PEAK_TFLOPS}
 KERNEL_NAMES = {("x3f16", 9): "conv2d_x3_kernel<9,*> (3x3, split-fp16 MFMA)",
                 ("x3f16", 4): "conv2d_x3_kernel<4,*> (2x2 phase / space-to-depth, split-fp16 MFMA)",
                 ("x3f16", 1): "conv2d_x3_kernel<1,*> (1x1, split-fp16 MFMA)",
                 ("x3f16", 25): "conv2d_x3_kernel<25,2> (5x5 dilated on the lattice, split-fp16 MFMA)",
-                ("f32", 1): "conv2d_pc_kernel<1,32,2,3,2> (1x1, f32 MFMA)"}
+                ("f32", 1): "conv2d_pc_kernel<1,32,2,3,2> (1x1, f32 MFMA)",
+                ("f32w", 9): "wgrad_kernel (3x3 weight gradient, f32 MFMA)",
+                ("f32w", 4): "wgrad_kernel (2x2 weight gradient, f32 MFMA)",
+                ("f32w", 1): "wgrad_kernel (1x1 weight gradient, f32 MFMA)"}
 
 
 def conv_roofline(model, x, cond, pos, sc):
     """One model call with every conv launch bracketed by HIP events on its stream; the roofline is
     reported for the conv class with the largest total time (the dominant kernel)."""
+    def call():
+        with torch.no_grad():
+            model(x, cond=cond, bc=None, pos=pos, t_cond=None, spatial_cond=sc)
+    return probe_roofline(call)
+
+
+def probe_roofline(fn):
+    """Run fn() with every conv / weight-gradient launch bracketed by HIP events on its stream
+    (ops.conv_probe); roofline of the class with the largest total time."""
     from nps_hip import ops
     ops.conv_probe = []
-    with torch.no_grad():
-        model(x, cond=cond, bc=None, pos=pos, t_cond=None, spatial_cond=sc)
-    torch.cuda.synchronize()
-    probe, ops.conv_probe = ops.conv_probe, None
+    try:
+        fn()
+        torch.cuda.synchronize()
+    finally:
+        probe, ops.conv_probe = ops.conv_probe, None
     groups = {}
     for e0, e1, f, (prec, ntaps, waves), nb in probe:
         g = groups.setdefault((prec, ntaps), [0.0, 0.0, 0, 0.0])
@@ -260,6 +273,20 @@ def main():
         roof = attach_traffic(conv_roofline(model, u_all[:, :, :tw], cond, pos, sc), headline)
         cpu = cpu_baseline(model, ocfg, opde, args.res, args.num_c, calls=args.cpu_calls) if (
             args.cpu_calls > 0 and world == 1) else None
+        if cpu is not None and B >= 2:
+            # the north star's 10x is defined at the CPU sample's batch (B = 2): the same rollout on this
+            # GPU at B = 2, timed like the headline
+            def rollout2(nsteps):
+                with torch.no_grad():
+                    return tr.simulate(u_all[:2], cond[:2], pos[:2], compute_loss=True, include_data=False,
+                                       nr_gt_steps=1, t_res=tw * (nsteps + 1), spatial_conditioning=sc[:2])
+            rollout2(1)
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            rollout2(args.steps)
+            torch.cuda.synchronize()
+            v2 = 2 * tw * args.steps / (time.perf_counter() - t2)
+            cpu["gpu_at_same_batch"] = dict(value=round(v2, 3), batch=2, gpu_over_cpu=round(v2 / cpu["value"], 1))
         line = {
             "metric": f"rollout timesteps/sec on {args.res}x{args.res} two-phase grid (sample-timesteps/s); "
                       "rel-L2 vs CPU reference",
@@ -358,6 +385,29 @@ def run_fno3d(args):
         torch.distributed.destroy_process_group()
 
 
+def cpu_baseline_train(model, args, B=1):
+    """The training step on the host: the oracle (fp32 PyTorch-CPU restatement) forward, sqrt(MSE_sum)
+    loss and autograd backward for one sample (trainers/autoregressivepushforwardtrainer.py:43-163,
+    unroll 0), plus Adam — samples/s on the host cores."""
+    import oracle
+    from trainers.synthetic import twophase_batch
+    _, ocfg, opde = build_model(args.model, args.res, args.num_c, "cpu", fno_modes=args.fno_modes)
+    threads = int(os.environ.get("OMP_NUM_THREADS", len(os.sched_getaffinity(0))))
+    torch.set_num_threads(threads)
+    om = oracle.build_oracle_model(ocfg, opde, {k: v.detach().cpu() for k, v in model.state_dict().items()})
+    om.sd = {k: v.detach().clone().requires_grad_(True) for k, v in om.sd.items()}
+    opt = torch.optim.Adam([t for t in om.sd.values() if t.is_floating_point() or t.is_complex()], lr=1e-4)
+    u, cond, pos, sc = twophase_batch(B, args.num_c, 50, args.res, args.res, seed=99, obstacle="disc")
+    t0 = time.perf_counter()
+    loss = torch.sqrt(torch.sum((om(u[:, :, :25], cond=cond, pos=pos, spatial_cond=sc) - u[:, :, 25:50]) ** 2))
+    loss.backward()
+    opt.step()
+    dt = time.perf_counter() - t0
+    return dict(value=round(B / dt, 4), unit="samples/s", cores=threads, kind="port",
+                sample=f"oracle train step (forward + sqrt(MSE_sum) + autograd backward + Adam), B={B}, "
+                       f"{args.res}x{args.res}, {args.num_c} fields, {dt:.1f} s")
+
+
 def run_train(args):
     """Training throughput: trainers/base.py:472-507 steps of the pushforward train_step (unroll 0, the
     epoch-0 case) on a fixed global batch sharded over the ranks; gradients all-reduced over RCCL
@@ -408,6 +458,8 @@ def run_train(args):
         torch.distributed.barrier()
     elapsed = max_over_ranks(time.perf_counter() - t0, dev)
     if rank == 0:
+        roof = probe_roofline(lambda: tr.train_one_epoch([batch], epoch=0))
+        cpu = cpu_baseline_train(model, args) if (args.cpu_calls > 0 and world == 1) else None
         print(json.dumps({
             "metric": "pushforward training samples/sec (train_step + backward + all-reduce + Adam)",
             "value": round(args.global_batch * args.steps / elapsed, 3), "unit": "samples/s", "n_gpus": world,
@@ -417,7 +469,7 @@ def run_train(args):
             "config": {"workload": f"{args.model.upper()} twophase cfg train_step, {args.res}x{args.res}, "
                                    f"{args.num_c} fields, tw=25", "global_batch": args.global_batch,
                        "per_gpu_batch": B, "parallelism": f"dp{world} (RCCL gradient all-reduce)"},
-            "loss_last": float(loss)}), flush=True)
+            "roofline": roof, "cpu_baseline": cpu, "loss_last": float(loss)}), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
 

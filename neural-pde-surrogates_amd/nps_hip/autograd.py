@@ -41,7 +41,15 @@ def wgrad(a: torch.Tensor, x: torch.Tensor, KH: int, KW: int, dil=1, pad=(0, 0),
     p.x, p.Hx, p.Wx, p.N = ptr(x), Hx, Wx, N
     p.KH, p.KW, p.dil, p.pad_y, p.pad_x, p.circ = KH, KW, dil, pad[0], pad[1], circ
     p.g = ptr(g)
-    check(lib.nps_conv2d_wgrad(ctypes.byref(p), stream_ptr()), "conv2d_wgrad")
+    if ops.conv_probe is not None:  # bench.py's live roofline probe (ops.conv_probe)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        check(lib.nps_conv2d_wgrad(ctypes.byref(p), stream_ptr()), "conv2d_wgrad")
+        e1.record()
+        ops.conv_probe.append((e0, e1, 2.0 * B * Ha * Wa * M * N * KH * KW, ("f32w", KH * KW, 0),
+                               4.0 * (a.numel() + x.numel() + g.numel())))
+    else:
+        check(lib.nps_conv2d_wgrad(ctypes.byref(p), stream_ptr()), "conv2d_wgrad")
     return g
 
 

@@ -25,7 +25,7 @@ def load(d, counter):
 
 
 def klass(name):
-    m = re.search(r"conv2d_x3_kernel<(\d+), \d+(?:, (?:true|false))?>", name)
+    m = re.search(r"conv2d_x3_kernel<(\d+), \d+(?:, (?:true|false))*>", name)
     if m:
         return f"x3f16_{m.group(1)}tap"
     if re.search(r"conv1x1_(?:x3|wl)_kernel<", name):
