@@ -578,6 +578,139 @@ __global__ void mix_bwd_kernel(const float2* __restrict__ X2, const float2* __re
     }
 }
 
+// The same backward on the matrix cores (v_mfma_f32_16x16x4f32, exact fp32, complex as interleaved real
+// rows / columns as in mix_mfma_kernel), for B <= 16 * NBC.  Work-group = one mode x 64 input channels
+// (wave w: channels [16w, +16), two 16-row tiles of 8 complex channels); the output channels are walked
+// in chunks of 32 with the chunk's weights [64 i][32 o] and gY [32 o][B] in LDS (weights double-buffered
+// through registers), and each chunk does both products:
+//   gX2[b][i]  += sum_o conj(W[i][o]) gY[b][o]      A = conj(W) [(i,p)][(o,q)], B = gY [(o,q)][b]
+//   gW[i][o]    = sum_b conj(X2[b][i]) gY[b][o]     A = conj(X2) [(i,p)][(b,q)] (registers), B = gY [(b,q)][o]
+// so the weights stream from HBM once and the weight gradient is written once.
+constexpr int MIXB_OC = 32;  // output channels per chunk
+template <int NBC>
+__global__ __launch_bounds__(256) void mix_bwd_mfma_kernel(const float2* __restrict__ X2, const float2* __restrict__ wp,
+                                                           const float2* __restrict__ gY, float2* __restrict__ gX2,
+                                                           float2* __restrict__ gwp, int B, int nmodes, int Cin,
+                                                           int Cout) {
+    constexpr int NB = 16 * NBC;          // batch columns
+    constexpr int WPT = 64 * MIXB_OC * 8 / (256 * 16);  // 16-B weight pieces per thread per chunk (4)
+    __shared__ float2 Ws[2][64][MIXB_OC + 1];  // [i][o] (+1: bank offset between rows)
+    __shared__ float2 Gs[MIXB_OC][NB + 1];     // [o][b]
+    const int mode = blockIdx.x;
+    const int i0 = blockIdx.y * 64;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nchunks = (Cout + MIXB_OC - 1) / MIXB_OC;
+    const float2* wmode = wp + (size_t)mode * Cin * Cout;
+    f32x4 wr[WPT];
+    auto wfetch = [&](int c) {
+#pragma unroll
+        for (int k = 0; k < WPT; ++k) {
+            const int piece = k * 256 + tid;
+            const int row = piece / (MIXB_OC / 2), cp = piece - row * (MIXB_OC / 2);
+            const int i = i0 + row, o = c * MIXB_OC + 2 * cp;
+            const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+            // Cout % 4 == 0 (host-checked): a 2-channel piece is wholly inside [0, Cout) or wholly outside
+            wr[k] = (i < Cin && o < Cout) ? *reinterpret_cast<const f32x4*>(wmode + (size_t)i * Cout + o) : z;
+        }
+    };
+    auto wstore = [&](int buf) {
+#pragma unroll
+        for (int k = 0; k < WPT; ++k) {
+            const int piece = k * 256 + tid;
+            const int row = piece / (MIXB_OC / 2), cp = piece - row * (MIXB_OC / 2);
+            Ws[buf][row][2 * cp] = make_float2(wr[k][0], wr[k][1]);
+            Ws[buf][row][2 * cp + 1] = make_float2(wr[k][2], wr[k][3]);
+        }
+    };
+    // lane roles (16x16x4): row r = lane & 15 -> (complex row r >> 1 of the tile, p = r & 1); k = lane >> 4
+    // -> (pair member k >> 1, q = k & 1)
+    const int r = lane & 15, p = r & 1, k = lane >> 4, kh = k >> 1, q = k & 1;
+    // conj(X2) A fragments of this wave's rows, one per K step of 2 batch entries
+    float xa[2][NB / 2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const int i = i0 + wave * 16 + t * 8 + (r >> 1);
+#pragma unroll
+        for (int kk = 0; kk < NB / 2; ++kk) {
+            const int b = 2 * kk + kh;
+            const float2 x = (i < Cin && b < B) ? X2[((size_t)b * nmodes + mode) * Cin + i] : make_float2(0.f, 0.f);
+            xa[t][kk] = p == q ? x.x : (p == 0 ? x.y : -x.y);
+        }
+    }
+    f32x4 gx[NBC][2];
+#pragma unroll
+    for (int n = 0; n < NBC; ++n)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) gx[n][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int nks = (B + 1) / 2;  // K steps of the weight-gradient product
+    wfetch(0);
+    for (int c = 0; c < nchunks; ++c) {
+        const int buf = c & 1;
+        __syncthreads();  // buffer `buf` and Gs are free
+        wstore(buf);
+        for (int e = tid; e < MIXB_OC * NB; e += 256) {  // gY chunk: [o][b]
+            const int oc = e % MIXB_OC, b = e / MIXB_OC;
+            const int o = c * MIXB_OC + oc;
+            Gs[oc][b] = (o < Cout && b < B) ? gY[((size_t)b * nmodes + mode) * Cout + o] : make_float2(0.f, 0.f);
+        }
+        if (c + 1 < nchunks) wfetch(c + 1);
+        __syncthreads();
+        // gX2: K = this chunk's 32 output channels, 2 per step
+#pragma unroll 4
+        for (int s2 = 0; s2 < MIXB_OC / 2; ++s2) {
+            const int oc = 2 * s2 + kh;
+            float a[2];
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const float2 w = Ws[buf][wave * 16 + t * 8 + (r >> 1)][oc];
+                a[t] = p == q ? w.x : (p == 0 ? w.y : -w.y);  // conj(W)
+            }
+#pragma unroll
+            for (int n = 0; n < NBC; ++n) {
+                const float2 g = Gs[oc][n * 16 + r];
+                const float bv = q ? g.y : g.x;
+#pragma unroll
+                for (int t = 0; t < 2; ++t) gx[n][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t], bv, gx[n][t], 0, 0, 0);
+            }
+        }
+        // gW for this chunk: 2 row tiles x 2 column tiles of 16 output channels, K = batch (2 per step)
+#pragma unroll
+        for (int cc = 0; cc < 2; ++cc) {
+            f32x4 gw[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+            for (int kk = 0; kk < nks; ++kk) {
+                const float2 g = Gs[cc * 16 + r][2 * kk + kh];
+                const float bv = q ? g.y : g.x;
+#pragma unroll
+                for (int t = 0; t < 2; ++t) gw[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[t][kk], bv, gw[t], 0, 0, 0);
+            }
+            // D: column = output channel (lane & 15); rows (lane >> 4) * 4 + reg = (re, im) of complex rows
+            // 2 (lane >> 4) and 2 (lane >> 4) + 1 of the tile
+            const int o = c * MIXB_OC + cc * 16 + (lane & 15);
+            if (o < Cout) {
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {
+                    const int i = i0 + wave * 16 + t * 8 + 2 * (lane >> 4);
+                    if (i < Cin) gwp[((size_t)mode * Cin + i) * Cout + o] = make_float2(gw[t][0], gw[t][1]);
+                    if (i + 1 < Cin) gwp[((size_t)mode * Cin + i + 1) * Cout + o] = make_float2(gw[t][2], gw[t][3]);
+                }
+            }
+        }
+    }
+    // gX2: D column = batch 16n + (lane & 15); rows = (re, im) of complex rows 2 (lane >> 4) + {0, 1}
+#pragma unroll
+    for (int n = 0; n < NBC; ++n) {
+        const int b = n * 16 + (lane & 15);
+        if (b >= B) continue;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int i = i0 + wave * 16 + t * 8 + 2 * (lane >> 4);
+            float2* g = gX2 + ((size_t)b * nmodes + mode) * Cin;
+            if (i < Cin) g[i] = make_float2(gx[n][t][0], gx[n][t][1]);
+            if (i + 1 < Cin) g[i + 1] = make_float2(gx[n][t][2], gx[n][t][3]);
+        }
+    }
+}
+
 // gw1/gw2 [Cin][Cout][m1][m2] from gwp[r][k2][i][o] (adjoint of spec_pack_kernel: a weights1 row that
 // the weights2 corner overwrites in the forward gets zero gradient)
 __global__ void spec_unpack_grad_kernel(const float2* __restrict__ gwp, float2* __restrict__ gw1,
@@ -897,6 +1030,25 @@ extern "C" int nps_spectral_mix_bwd(const float* X2, const float* wpack, const f
                                     int B, int R, int m2, int Cin, int Cout, void* stream) {
     NPS_CHECK_ARG(X2 && wpack && gY && gX2 && gwpack && B > 0 && R > 0 && m2 > 0 && Cin > 0 && Cout > 0,
                   "spectral_mix_bwd: bad args");
+    static int use_valu = -1;  // dev knob NPS_MIX_VALU=1: the scalar-FMA backward (A/B reference)
+    if (use_valu < 0) {
+        const char* e = getenv("NPS_MIX_VALU");
+        use_valu = (e != nullptr && e[0] == '1') ? 1 : 0;
+    }
+    if (!use_valu && (Cout & 3) == 0 && B <= 32) {
+        const dim3 grid(R * m2, (Cin + 63) / 64);
+        const auto* x = reinterpret_cast<const float2*>(X2);
+        const auto* w = reinterpret_cast<const float2*>(wpack);
+        const auto* gy = reinterpret_cast<const float2*>(gY);
+        auto* gx = reinterpret_cast<float2*>(gX2);
+        auto* gw = reinterpret_cast<float2*>(gwpack);
+        if (B <= 16)
+            mix_bwd_mfma_kernel<1><<<grid, 256, 0, (hipStream_t)stream>>>(x, w, gy, gx, gw, B, R * m2, Cin, Cout);
+        else
+            mix_bwd_mfma_kernel<2><<<grid, 256, 0, (hipStream_t)stream>>>(x, w, gy, gx, gw, B, R * m2, Cin, Cout);
+        NPS_CHECK_LAUNCH("spectral_mix_bwd (MFMA)");
+        return 0;
+    }
     const size_t lds = sizeof(float2) * B * Cout;
     NPS_CHECK_ARG(lds <= 64 * 1024, "spectral_mix_bwd: B*Cout=%d too large", B * Cout);
     const int ychunks = (Cin + 31) / 32;

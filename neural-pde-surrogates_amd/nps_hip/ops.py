@@ -150,10 +150,27 @@ def input_tag(t: torch.Tensor) -> int:
 STATS_SUB = 16  # NPS_STATS_SUB
 
 
+_STATS_CHUNK = 1 << 15      # doubles zeroed at once; slices are handed out and never re-zeroed
+_stats_chunks = {}
+
+
 def new_stats(B: int, like: torch.Tensor, sub: int = STATS_SUB) -> torch.Tensor:
     """A zeroed fp64 [B][sub][2] moments buffer: sub = NPS_STATS_SUB for nps_conv2d_t.out_stats, 1 for the
-    [B][G][2] statistics a GroupNorm prologue reads (G = 1)."""
-    return torch.zeros((B, sub, 2), dtype=torch.float64, device=like.device)
+    [B][G][2] statistics a GroupNorm prologue reads (G = 1).  Slices of one zero-filled chunk per device
+    (one fill launch per chunk instead of one per buffer); a chunk is never reused in place — it is freed
+    when its last slice is."""
+    n = B * sub * 2
+    d = like.device
+    key = (d.type, d.index if d.index is not None else torch.cuda.current_device())
+    ch = _stats_chunks.get(key)
+    if n > _STATS_CHUNK // 4:
+        return torch.zeros((B, sub, 2), dtype=torch.float64, device=d)
+    if ch is None or ch[1] + n > _STATS_CHUNK:
+        ch = [torch.zeros(_STATS_CHUNK, dtype=torch.float64, device=d), 0]
+        _stats_chunks[key] = ch
+    v = ch[0][ch[1]:ch[1] + n].view(B, sub, 2)
+    ch[1] += (n + 31) // 32 * 32
+    return v
 
 
 def _stats_sum(parts, B, out):

@@ -202,6 +202,32 @@ _ORACLE_PROC = {"unet_ufno_style": Fo.unet_modern, "unet_cfg": Fo.unet_modern, "
                 "drn": Fo.dilated_resnet, "ufno": Fo.ufno, "fno": Fo.fno}
 
 
+@pytest.mark.parametrize("B,Cin,Cout", [(1, 20, 12), (2, 196, 192), (5, 67, 64), (16, 64, 32), (17, 40, 44),
+                                         (32, 24, 16), (33, 20, 12)])
+def test_spectral_mix_backward_vs_fp64(B, Cin, Cout):
+    """nps_spectral_mix_bwd (MFMA for B <= 32, the scalar kernel above) vs the fp64 adjoint of the per-mode
+    contraction y[b][o] = sum_i x[b][i] W[i][o] (proc_fno.py:253-255): gX = gY W^H, gW = sum_b conj(x) gY."""
+    from nps_hip import lib, ptr, stream_ptr, check
+    g = torch.Generator().manual_seed(B * 1000 + Cin)
+    nm = 6  # modes
+
+    def crand(*sh):
+        return torch.complex(torch.randn(*sh, generator=g), torch.randn(*sh, generator=g))
+
+    X = crand(B, nm, Cin)
+    W = crand(nm, Cin, Cout)
+    gY = crand(B, nm, Cout)
+    gX = torch.einsum("bmo,mio->bmi", gY.to(torch.complex128), W.to(torch.complex128).conj())
+    gW = torch.einsum("bmi,bmo->mio", X.to(torch.complex128).conj(), gY.to(torch.complex128))
+    Xd, Wd, gYd = X.to(DEV), W.to(DEV), gY.to(DEV)
+    gXd = torch.empty_like(Xd)
+    gWd = torch.empty_like(Wd)
+    check(lib.nps_spectral_mix_bwd(ptr(Xd), ptr(Wd), ptr(gYd), ptr(gXd), ptr(gWd), B, 2, nm // 2, Cin, Cout,
+                                   stream_ptr()), "spectral_mix_bwd")
+    assert rel_l2(gXd.cpu(), gX) < 1e-6
+    assert rel_l2(gWd.cpu(), gW) < 1e-6
+
+
 @pytest.mark.parametrize("name", ["unet_ufno_style", "unet_cfg", "unet_ones", "drn", "ufno", "fno"])
 def test_processor_backward_vs_oracle(name):
     m, g, _ = _proc(name)

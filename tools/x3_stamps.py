@@ -24,12 +24,18 @@ def main():
     ap.add_argument("--k", type=int, default=3)
     ap.add_argument("--hw", type=int, default=258)
     ap.add_argument("--b", type=int, default=16)
+    ap.add_argument("--gn", type=int, default=0, help="1: fused GroupNorm(1) + GELU prologue")
     a = ap.parse_args()
     x = torch.randn(a.b, a.hw, a.hw, a.cin, device="cuda")
     w = torch.randn(a.cout, a.cin, a.k, a.k, device="cuda") * 0.05
     wp = ops.pack_conv_weight(w)
+    kw = {}
+    if a.gn:
+        st = ops.group_norm_stats([ops.Src(x)], (a.hw, a.hw), 1)
+        kw = dict(gn=ops.GN(st, torch.rand(a.cin, device="cuda") + 0.5, torch.rand(a.cin, device="cuda") - 0.5, 1,
+                            1e-5), pre_act=1)
     for _ in range(5):
-        out = ops.conv2d([ops.Src(x)], (a.hw, a.hw), wp, None, a.cout, a.k, a.k)
+        out = ops.conv2d([ops.Src(x)], (a.hw, a.hw), wp, None, a.cout, a.k, a.k, **kw)
     torch.cuda.synchronize()
     ho = out.shape[1]
     n = 1 << 20
@@ -38,13 +44,14 @@ def main():
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
     assert fn(ctypes.addressof(buf), n) == 0
     st = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 8).astype(np.int64)
-    tile = 512 if a.hw >= 64 else 256
+    wide = os.environ.get("NPS_X3_WIDE", "1") != "0" and a.k in (2, 3) and 128 < a.cout <= 192
+    tile = 128 if wide else (512 if a.hw >= 64 else 256)
     nwg = int(np.count_nonzero(st[:, 3]))
     st = st[:nwg]
     clk = (st[:, 3] - st[:, 0]) / np.maximum(st[:, 5] - st[:, 4], 1) * 100.0  # MHz
     pro, loop, epi = st[:, 1] - st[:, 0], st[:, 2] - st[:, 1], st[:, 3] - st[:, 2]
     groups = ((a.cin + 15) // 16) * a.k * a.k
-    ideal = groups * 2 * (tile // 128) * 3 * 32
+    ideal = groups * (3 * 2 if wide else 2 * (tile // 128)) * 3 * 32  # MFMAs per K-group per consumer wave
     span = (st[:, 5].max() - st[:, 4].min()) / 100.0  # us
     print(f"work-groups {nwg}, out {ho}x{ho}, span {span:.1f} us, clock median {np.median(clk):.0f} MHz")
     print(f"cycles per WG (median): prologue {np.median(pro):.0f}  loop {np.median(loop):.0f} "
