@@ -105,3 +105,13 @@ def test_fno3d_construction_matches_reference_seeded_init():
     assert list(sd) == list(g["state_dict"])
     for k, v in g["state_dict"].items():
         assert torch.equal(sd[k], v), k
+
+
+def test_3d_ufno_unconstructible_as_reference():
+    """The reference's U-FNO / UNetModern with num_spatial_dims=3 and two or more U-Net resolutions fail at
+    construction (its Upsample has no 3-D form: src/models/common.py:103-120); the mirror fails the same way,
+    so a cfg behaves identically (C5 runs the FNO-3D processor)."""
+    from models.enc_proc_dec_components.proc_ufno import UFNO
+    with pytest.raises(NotImplementedError, match="spatial dim 3"):
+        UFNO(pde=None, num_spatial_dims=3, n_cond=4, hidden_features=16, hidden_blocks=1, fno_modes=(4, 4, 4),
+             ch_mults=(1, 1), is_attn=(False, False), norm=True)
