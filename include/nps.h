@@ -178,6 +178,10 @@ int nps_frame_pack(const nps_conv2d_t* a, float* out, void* stream);
  * first (the call does it when zero_first != 0). */
 int nps_group_norm_stats(const nps_src_t* src, int nsrc, int B, int Hin, int Win, int Cin, int G,
                          double* stats, int zero_first, void* stream);
+/* Test hook: run the split-fp16 conv kernels on a persistent grid of `wgs` work-groups (> 0; 0 = one per
+ * CU, the default) so every work-group walks many tiles. */
+int nps_x3_set_grid(long wgs);
+
 /* GroupNorm(1) moments of a virtual frame from those of its sources, each covering the frame exactly
  * (nps_conv2d_t.out_stats) — the per-source moments of torch.cat's GroupNorm (proc_unet_modern.py:235-236):
  * part i is [B][n_i][2] (n_i sub-slots; p1, p2 may be NULL), out is [B][n_out][2] and receives

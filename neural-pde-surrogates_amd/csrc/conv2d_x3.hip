@@ -954,6 +954,13 @@ void launch_x3_one(const nps_conv2d_t& a, unsigned nwg, int lds, hipStream_t s) 
 
 }  // namespace
 
+// test hook (nps_x3_set_grid): persistent-grid size override (> 0)
+static long g_x3_grid_override = 0;
+extern "C" int nps_x3_set_grid(long wgs) {
+    g_x3_grid_override = wgs > 0 ? wgs : 0;
+    return 0;
+}
+
 int nps_launch_conv2d_x3(const nps_conv2d_t& a, int lds, hipStream_t s) {
     const Geo g = make_geo(a);
     const bool wide = x3_wide_tile(a);  // 192-channel x 128-pixel work-groups (nps_conv2d_plan)
@@ -975,11 +982,9 @@ int nps_launch_conv2d_x3(const nps_conv2d_t& a, int lds, hipStream_t s) {
         const char* e = getenv("NPS_X3_GRID");  // dev knob: work-groups of the persistent grid
         if (e != nullptr && atol(e) > 0) per = atol(e);
     }
-    // The register-store epilogue (NCHW or channel counts not a multiple of 4) runs one tile per
-    // work-group: looped over tiles it gave wrong co-block-1 rows after the first tile (only there;
-    // the PB=4 kernels spill under the persistent loop), so that rare layout keeps the plain grid.
+    const long pw = g_x3_grid_override > 0 ? g_x3_grid_override : per;
     const bool lds_epi = !a.out_nchw && (a.out_C & 3) == 0 && (a.Cout & 3) == 0;  // == x3_lds_epilogue
-    const unsigned grid = (unsigned)(lds_epi && per < nwg ? per : nwg);
+    const unsigned grid = (unsigned)(pw < nwg ? pw : nwg);  // either epilogue walks tiles (tests: many per WG)
     const bool p512 = a.TH * a.TW == 512;
     const bool pro = a.gn_stats != nullptr || a.pre_act != 0;  // fused frame prologue: 3x3 only (host-checked)
     // 1x1 convs (never with a prologue: x3_eligible) run on the ring-free kernel, whose 32-channel

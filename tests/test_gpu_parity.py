@@ -129,6 +129,31 @@ def test_residual_block_fused_prologue(monkeypatch, pm):
     assert rel_l2(y, ref) < TOL
 
 
+@pytest.mark.parametrize("cout", [192, 64])     # 192: wide tiles, 64: 512-pixel tiles (PB=4 kernels)
+@pytest.mark.parametrize("nchw", [False, True])  # LDS-staged vs register-store epilogue
+def test_split_fp16_persistent_tiles(cout, nchw):
+    """Every work-group walks many tiles (persistent grid of 8 work-groups, nps_x3_set_grid) for both
+    epilogue layouts — the register-store one walks tiles too since the producer fetches became
+    compiler-visible loads (round 1 kept it on one tile per work-group): bias + GELU epilogue vs fp64."""
+    from nps_hip import lib, ops
+    import torch.nn.functional as F
+    torch.manual_seed(2)
+    B, Cin, H, W = 2, 48, 66, 70
+    x = torch.randn(B, Cin, H, W)
+    w = torch.randn(cout, Cin, 3, 3) * 0.05
+    b = torch.randn(cout) * 0.1
+    ref = F.gelu(F.conv2d(x.double(), w.double(), b.double()))
+    lib.nps_x3_set_grid(8)
+    try:
+        y = ops.conv2d([ops.Src(ops.nchw_to_nhwc(x.to(DEV)))], (H, W), ops.pack_conv_weight(w.to(DEV)), b.to(DEV),
+                       cout, 3, 3, act=ops.GELU, out_nchw=nchw)
+        torch.cuda.synchronize()
+    finally:
+        lib.nps_x3_set_grid(0)
+    y = y.cpu() if nchw else ops.nhwc_to_nchw(y).cpu()
+    assert rel_l2(y, ref) < TOL
+
+
 def _moments(t):
     """fp64 (sum, sum of squares) per sample.  The carried moments match to ~1e-8 relative: the epilogues
     sum in fp64, nps_group_norm_stats (the seed of an identity shortcut's) sums fp32 quads first."""
