@@ -67,7 +67,8 @@ def build_model(kind, res, num_c, device, fno_modes=None, seed=42):
 
 # dense MFMA peaks, MI355X_MICROARCH.md: f32 (v_mfma_f32_32x32x2_f32) 157.3 TF; f16 2.5 PF.  A split-fp16
 # conv spends 3 f16 MFMA products per algorithmic fp32 product, so its fp32-equivalent ceiling is 2.5 PF / 3.
-PEAK_TFLOPS = {"f32": FP32_MFMA_PEAK_TFLOPS, "x3f16": 2500.0 / 3.0, "f32w": FP32_MFMA_PEAK_TFLOPS}
+PEAK_TFLOPS = {"f32": FP32_MFMA_PEAK_TFLOPS, "x3f16": 2500.0 / 3.0, "f32w": FP32_MFMA_PEAK_TFLOPS,
+               "x3w": 2500.0 / 3.0}
 KERNEL_NAMES = {("x3f16", 9): "conv2d_x3_kernel<9,*> (3x3, split-fp16 MFMA)",
                 ("x3f16", 4): "conv2d_x3_kernel<4,*> (2x2 phase / space-to-depth, split-fp16 MFMA)",
                 ("x3f16", 1): "conv2d_x3_kernel<1,*> (1x1, split-fp16 MFMA)",
@@ -75,7 +76,10 @@ KERNEL_NAMES = {("x3f16", 9): "conv2d_x3_kernel<9,*> (3x3, split-fp16 MFMA)",
                 ("f32", 1): "conv2d_pc_kernel<1,32,2,3,2> (1x1, f32 MFMA)",
                 ("f32w", 9): "wgrad_kernel (3x3 weight gradient, f32 MFMA)",
                 ("f32w", 4): "wgrad_kernel (2x2 weight gradient, f32 MFMA)",
-                ("f32w", 1): "wgrad_kernel (1x1 weight gradient, f32 MFMA)"}
+                ("f32w", 1): "wgrad_kernel (1x1 weight gradient, f32 MFMA)",
+                ("x3w", 9): "wgrad_x3_kernel<3,3> (3x3 weight gradient, split-fp16 MFMA)",
+                ("x3w", 4): "wgrad_x3_kernel<2,2> (2x2 weight gradient, split-fp16 MFMA)",
+                ("x3w", 1): "wgrad_x3_kernel<1,1> (1x1 weight gradient, split-fp16 MFMA)"}
 
 
 def conv_roofline(model, x, cond, pos, sc):
@@ -155,12 +159,33 @@ def shard_bounds(global_batch, world, rank):
     return rank * per, (rank + 1) * per
 
 
+def init_ranks():
+    """(world, rank, device) of this process: one process per GPU (torchrun env), RCCL process group.
+
+    NPS_BENCH_REHEARSAL=1 (dev only, never a reported number): every rank on cuda:0 over gloo, so the
+    N > 1 code path (sharding, barriers, max-over-ranks) can run on a one-GPU box."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        if os.environ.get("NPS_BENCH_REHEARSAL") == "1":
+            local_rank = 0
+            torch.cuda.set_device(0)
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local_rank)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    return world, rank, torch.device("cuda", local_rank)
+
+
 def max_over_ranks(elapsed, device):
     """The job's wall time: the slowest rank's (one all-reduce MAX; identity in a single process)."""
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return elapsed
-    t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+    on_cpu = dist.get_backend() == "gloo"
+    t = torch.tensor([elapsed], device="cpu" if on_cpu else device, dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return t.item()
 
@@ -216,14 +241,7 @@ def main():
     if args.model == "fno3d":
         return run_fno3d(args)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cuda", local_rank)
+    world, rank, dev = init_ranks()
     lo, hi = shard_bounds(args.global_batch, world, rank)
     B = hi - lo
     tw = 25
@@ -318,14 +336,7 @@ def run_fno3d(args):
     sample), fp32 or bf16 storage; batch-sharded over the ranks like the rollout."""
     from models.enc_proc_dec_components.proc_fno import FNO
     from nps_hip import ops
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cuda", local_rank)
+    world, rank, dev = init_ranks()
     gb = args.global_batch if args.global_batch != 16 else 8  # C5: global batch 8 (one volume per GPU at 8)
     lo, hi = shard_bounds(gb, world, rank)
     B = hi - lo
@@ -416,15 +427,8 @@ def run_train(args):
     from common.interfaces import D
     from trainers.autoregressivepushforwardtrainer import AutoregressivePushforwardTrainer
     from trainers.synthetic import twophase_batch
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, dev = init_ranks()
     sync = None
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cuda", local_rank)
     lo, hi = shard_bounds(args.global_batch, world, rank)
     B = hi - lo
     tw = 25

@@ -29,8 +29,12 @@ def _c(t):
 
 # ------------------------------------------------------------------------- weight gradient
 def wgrad(a: torch.Tensor, x: torch.Tensor, KH: int, KW: int, dil=1, pad=(0, 0), circ=0,
-          g: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """G[m][n][KH*KW] (+)= sum_pix a[pix][m] * Xext[pix + tap*dil - pad][n]  (nps_conv2d_wgrad)."""
+          g: Optional[torch.Tensor] = None, a_range: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """G[m][n][KH*KW] (+)= sum_pix a[pix][m] * Xext[pix + tap*dil - pad][n].
+
+    Split-fp16 MFMA (nps_conv2d_wgrad_x3) under ops.CONV_PRECISION == PREC_X3F16 for undilated square
+    kernels up to 3x3 — a and x range-scaled from their max |.| (a_range: a's range tag when the caller
+    already has it) — else exact fp32 MFMA (nps_conv2d_wgrad)."""
     a, x = _c(a), _c(x)
     B, Ha, Wa, M = a.shape
     _, Hx, Wx, N = x.shape
@@ -41,15 +45,27 @@ def wgrad(a: torch.Tensor, x: torch.Tensor, KH: int, KW: int, dil=1, pad=(0, 0),
     p.x, p.Hx, p.Wx, p.N = ptr(x), Hx, Wx, N
     p.KH, p.KW, p.dil, p.pad_y, p.pad_x, p.circ = KH, KW, dil, pad[0], pad[1], circ
     p.g = ptr(g)
+    if ops.CONV_PRECISION == ops.PREC_X3F16 and KH == KW and KH <= 3 and dil == 1:
+        ar = a_range if a_range is not None else ops.absmax(a)
+        xr = ops.absmax(x)
+        arith = "x3w"
+
+        def launch():
+            check(lib.nps_conv2d_wgrad_x3(ctypes.byref(p), ptr(ar), ptr(xr), stream_ptr()), "conv2d_wgrad_x3")
+    else:
+        arith = "f32w"
+
+        def launch():
+            check(lib.nps_conv2d_wgrad(ctypes.byref(p), stream_ptr()), "conv2d_wgrad")
     if ops.conv_probe is not None:  # bench.py's live roofline probe (ops.conv_probe)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        check(lib.nps_conv2d_wgrad(ctypes.byref(p), stream_ptr()), "conv2d_wgrad")
+        launch()
         e1.record()
-        ops.conv_probe.append((e0, e1, 2.0 * B * Ha * Wa * M * N * KH * KW, ("f32w", KH * KW, 0),
+        ops.conv_probe.append((e0, e1, 2.0 * B * Ha * Wa * M * N * KH * KW, (arith, KH * KW, 0),
                                4.0 * (a.numel() + x.numel() + g.numel())))
     else:
-        check(lib.nps_conv2d_wgrad(ctypes.byref(p), stream_ptr()), "conv2d_wgrad")
+        launch()
     return g
 
 
@@ -197,7 +213,7 @@ class Conv2dFn(torch.autograd.Function):
         H, W = ctx.in_hw
         B, Ho, Wo, Cout = gy.shape
         Cin = w.shape[1]
-        dx = dw = db = None
+        dx = dw = db = rng = None
         if ctx.needs_input_grad[1]:
             rng = ops.absmax(gy) if ops.CONV_PRECISION == ops.PREC_X3F16 else None  # gradients: any magnitude
             if s == 1:
@@ -221,12 +237,12 @@ class Conv2dFn(torch.autograd.Function):
                                    in_scale=rng)
         if ctx.needs_input_grad[2]:
             if s == 1:
-                dw = wgrad(gy, xs, KH, KW, dil=d, pad=lo, circ=circ)
+                dw = wgrad(gy, xs, KH, KW, dil=d, pad=lo, circ=circ, a_range=rng)
                 if dw.shape[1] != Cin:      # input carried zero padding channels (packed encoder input)
                     dw = dw[:, :Cin].contiguous()
             else:
                 C = Cin
-                G = wgrad(gy, xs, 2, 2)                                    # [Cout][4C][2][2]
+                G = wgrad(gy, xs, 2, 2, a_range=rng)                       # [Cout][4C][2][2]
                 G = G.view(Cout, 2, 2, C, 2, 2).permute(0, 3, 4, 1, 5, 2).reshape(Cout, C, 4, 4)
                 dw = G[:, :, :3, :3].contiguous()
         if ctx.has_bias and ctx.needs_input_grad[3]:

@@ -91,6 +91,41 @@ def test_conv2d_backward_vs_torch(case):
     assert rel_l2(m.bias.grad, b.grad) < TOL
 
 
+WGRAD_X3_CASES = [
+    # (B, M, N, k, pad, circ, Ha, Wa, a_scale, x_scale)
+    (2, 192, 196, 3, 1, 0, 33, 35, 1.0, 1.0),       # U-FNO shape: channel tails, ragged pixel tiles
+    (2, 64, 64, 3, 0, 1, 40, 36, 1.0, 1.0),         # circular 'same' (frame extended by 1)
+    (1, 20, 96, 2, 0, 0, 17, 19, 1.0, 1.0),         # space-to-depth / phase form
+    (2, 75, 81, 1, 0, 0, 19, 23, 1.0, 1.0),         # 1x1, channel counts % 4 != 0
+    (2, 64, 48, 3, 1, 0, 64, 64, 1e-4, 1e3),        # range: tiny gradients x large activations
+    (2, 32, 40, 3, 1, 0, 24, 24, 1.5e5, 1e-3),      # range: gradients past fp16's max
+    (3, 128, 128, 3, 0, 1, 96, 96, 1.0, 1.0),       # many pixel tiles per split
+]
+
+
+@pytest.mark.parametrize("case", WGRAD_X3_CASES)
+def test_wgrad_x3_vs_fp64(case):
+    """nps_conv2d_wgrad_x3 (split-fp16 MFMA) against the fp64 weight gradient of the same geometry:
+    G[m][n][ky][kx] = sum_{b,p} a[b][p][m] Xext[b][p + (ky, kx) - pad][n], Xext circularly extended by circ
+    and zero outside; range-scaled operands must keep the fp32 bar at any magnitude."""
+    from nps_hip import autograd as ad
+    from nps_hip import ops
+    B, M, N, k, pad, circ, Ha, Wa, sa, sx = case
+    Hx, Wx = Ha + k - 1 - 2 * pad - 2 * circ, Wa + k - 1 - 2 * pad - 2 * circ
+    torch.manual_seed(1)
+    a = torch.randn(B, M, Ha, Wa, dtype=torch.float64) * sa
+    x = torch.randn(B, N, Hx, Wx, dtype=torch.float64) * sx
+    xe = F.pad(x, (circ,) * 4, mode="circular") if circ else x
+    xe = F.pad(xe, (pad,) * 4)
+    ref = torch.nn.grad.conv2d_weight(xe, (M, N, k, k), a)
+    assert ops.CONV_PRECISION == ops.PREC_X3F16
+    ad_a = a.float().permute(0, 2, 3, 1).contiguous().to(DEV)
+    ad_x = x.float().permute(0, 2, 3, 1).contiguous().to(DEV)
+    got = ad.wgrad(ad_a, ad_x, k, k, pad=(pad, pad), circ=circ)
+    got32 = torch.nn.grad.conv2d_weight(xe.float(), (M, N, k, k), a.float())  # fp32 CPU: the reference class
+    assert rel_l2(got, ref) < TOL, (rel_l2(got, ref), rel_l2(got32, ref))
+
+
 @pytest.mark.parametrize("circ", [True, False])
 def test_conv_transpose_backward_vs_torch(circ):
     from models.common import ConvTranspose2d, ConvTranspose2d_padded
