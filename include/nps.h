@@ -290,10 +290,13 @@ typedef struct {
 size_t nps_wgrad_lds_bytes(int KH, int KW);
 int nps_conv2d_wgrad(const nps_wgrad_t* p, void* stream);
 /* The same weight gradient in the split-fp16 arithmetic of NPS_PREC_X3F16 (3 fp16 MFMA products per
- * fp32 product, fp32 accumulation) for undilated 1x1 / 2x2 / 3x3 kernels (KH == KW): a and x are
- * scaled by exact powers of two from their range tags a_range / x_range (NPS_TAG_FLOATS floats,
- * e.g. from nps_absmax) before the split.  Same geometry and += semantics as nps_conv2d_wgrad. */
-int nps_conv2d_wgrad_x3(const nps_wgrad_t* p, const float* a_range, const float* x_range, void* stream);
+ * fp32 product, fp32 accumulation) for undilated 1x1 / 2x2 / 3x3 kernels (KH == KW) over channel
+ * counts M, N that are multiples of 4: a and x are scaled by exact powers of two from their range tags
+ * a_range / x_range (NPS_TAG_FLOATS floats, e.g. from nps_absmax) before the split.  ws: a device
+ * workspace of nps_wgrad_x3_ws_floats(M, N, KH, KW) floats (the split-K partials accumulate there
+ * tap-major, then fold into g).  Same geometry and += semantics as nps_conv2d_wgrad. */
+size_t nps_wgrad_x3_ws_floats(int M, int N, int KH, int KW);
+int nps_conv2d_wgrad_x3(const nps_wgrad_t* p, const float* a_range, const float* x_range, float* ws, void* stream);
 /* out[c] += sum over `rows` rows of x[row][c] (conv bias gradients; parameter-partial reductions) */
 int nps_channel_sums(const float* x, long rows, int C, float* out, void* stream);
 

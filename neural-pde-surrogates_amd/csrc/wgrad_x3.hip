@@ -27,7 +27,7 @@ __host__ __device__ constexpr int wx_prows(int KH) { return WX_TH + KH - 1; }
 // halves per patch channel: rows x 24 (+8 so consecutive channels start 16 B apart mod 256 B: conflict-free)
 __host__ __device__ constexpr int wx_bpitch(int KH) { return wx_prows(KH) * WX_PROW + 8; }
 __host__ __device__ constexpr size_t wx_lds_bytes(int KH) {
-    return (size_t)2 * 2 * (64 * WX_APITCH + 64 * wx_bpitch(KH));  // [hi | lo] x (A + patch), fp16
+    return (size_t)2 * 2 * 2 * (64 * WX_APITCH + 64 * wx_bpitch(KH));  // 2 buffers x [hi | lo] x (A + patch)
 }
 
 template <int N, typename F>
@@ -55,87 +55,117 @@ __device__ __forceinline__ f16x8 shifted_run(const unsigned (&d)[6]) {
     return __builtin_bit_cast(f16x8, r);
 }
 
-__device__ __forceinline__ f32x4 ld4c(const float* p, int C, int c) {  // channels [c, c+4) of one pixel row
-    if ((C & 3) == 0 && c + 4 <= C) return *reinterpret_cast<const f32x4*>(p + c);
-    f32x4 v = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-        if (c + e < C) v[e] = p[c + e];
-    return v;
-}
+// 16 zero bytes: the fetch address of every slot outside the tile / frame / channel range, so the producers'
+// loads are unconditional and the compiler's in-order vmcnt waits stay exact (a load skipped on one path
+// makes them drain the newest loads too)
+__device__ __attribute__((aligned(16))) float wx_zero4[4];
 
-// Work-group (4 waves, 256 threads) = 64 m x 64 n x KH*KW taps over a range of pixel tiles (split K);
-// wave (wm, wn) owns 32 m x 32 n x taps, one 32x32 accumulator per tap.  Per tile every thread fetches
-// 2 pixels x 4 channels of A (pixel pairs along a row) and of the patch into registers, then splits them
-// into the LDS planes with packed 2-pixel writes.
+// Work-group (8 waves, 512 threads, one per CU) = 64 m x 64 n x KH*KW taps over a range of pixel tiles
+// (split K).  Wave w owns 32 m x 32 n (wm = w & 1, wn = (w >> 1) & 1) and half the taps: waves 0-3 taps
+// [0, NT0), waves 4-7 taps [NT0, NT) — one 32x32 accumulator per tap; waves w and w + 4 share a SIMD, so
+// every SIMD carries all the taps of one (m, n) block.  A 1x1 conv splits the tile's pixel rows instead
+// (both halves add into the same G entries).  Every wave also stages: each lane fetches pixel pairs (2
+// pixels along a row x 4 channels per slot) two tiles ahead into one of two register sets, and after its
+// MFMAs of tile i splits tile i + 1 into the other LDS buffer (VALU beside the partner wave's MFMAs); one
+// barrier per tile.  Lanes 0-15 of a wave-quarter take 16 consecutive pixel pairs, so the packed 2-pixel
+// b32 writes of one instruction hit distinct banks.
 template <int KH, int KW>
-__global__ __launch_bounds__(256, 2) void wgrad_x3_kernel(const nps_wgrad_t p, const float* a_range,
-                                                          const float* x_range, int ntiles, int tiles_per_split,
-                                                          int n_nt) {
+__global__ __launch_bounds__(512) void wgrad_x3_kernel(const nps_wgrad_t p, const float* a_range,
+                                                       const float* x_range, float* __restrict__ ws, int ntiles,
+                                                       int tiles_per_split, int n_nt) {
     constexpr int NT = KH * KW;
+    constexpr bool ROWSPLIT = NT == 1;
+    constexpr int NT0 = ROWSPLIT ? 1 : (NT + 1) / 2;       // taps of waves 0-3
+    constexpr int NTW = NT0;                                 // accumulators per wave (max over the halves)
     constexpr int PR = wx_prows(KH), PC = WX_TW + KW - 1;  // patch rows / useful columns
     constexpr int PCE = (PC + 1) & ~1;                       // fetched columns (pixel pairs)
+    constexpr int PPR = PCE / 2;                             // pixel pairs per patch row
     constexpr int BP = wx_bpitch(KH);
-    constexpr int NA = WX_PX / 2 * 16 / 256;                 // A pixel-pair quads per thread (2)
-    constexpr int NB = (PR * PCE / 2 * 16 + 255) / 256;      // patch pixel-pair quads per thread
+    constexpr int NPA = WX_PX / 2;                           // A pixel pairs (32)
+    constexpr int NPB = PR * PPR;                            // patch pixel pairs
+    constexpr int GA = (NPA + 15) / 16, GB = (NPB + 15) / 16;  // groups of 16 pixel pairs
+    constexpr int NA = (GA * 4 * 64 + 511) / 512;            // slots per lane (x 4 channel quads)
+    constexpr int NB = (GB * 4 * 64 + 511) / 512;
+    constexpr int BUF = 2 * (64 * WX_APITCH + 64 * BP);      // halves per LDS buffer
     extern __shared__ __attribute__((aligned(16))) _Float16 wsm[];
-    _Float16* Ah = wsm;
-    _Float16* Al = Ah + 64 * WX_APITCH;
-    _Float16* Bh = Al + 64 * WX_APITCH;
-    _Float16* Bl = Bh + 64 * BP;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wm = wave & 1, wn = wave >> 1, h = lane >> 5;
     const int nt = blockIdx.x % n_nt, mt = blockIdx.x / n_nt;
     const int m0 = mt * 64, n0 = nt * 64;
     const int tiles_x = (p.Wa + WX_TW - 1) / WX_TW, tiles_y = (p.Ha + WX_TH - 1) / WX_TH;
-    const int Hext = p.Hx + 2 * p.circ, Wext = p.Wx + 2 * p.circ;
     const int t_begin = blockIdx.y * tiles_per_split;
     const int t_end = min(ntiles, t_begin + tiles_per_split);
     if (t_begin >= t_end) return;
+    const int nloc = t_end - t_begin;
     const float sa = pow2_scale_for(nps::tag_read(a_range));
     const float sx = pow2_scale_for(nps::tag_read(x_range));
+    const int Hext = p.Hx + 2 * p.circ, Wext = p.Wx + 2 * p.circ;
 
-    f32x4 ra[NA][2], rb[NB][2];
-    auto issue = [&](int t) {
+    // ---- staging: per-slot geometry, fixed for the work-group (only the tile origin changes): slot k of
+    // this lane is group-of-16 g = (tid + 512 k) >> 6 — pair block g % G, channel block g / G — so the
+    // per-tile address arithmetic is a few adds and compares (no integer division)
+    int a_r[NA], a_c[NA], a_m[NA], a_lds[NA];
+    bool a_ok[NA];
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+        const int idx = tid + k * 512, l = idx & 63, g = idx >> 6;
+        const int pp = (l & 15) + 16 * (g % GA), mq = (l >> 4) + 4 * (g / GA);
+        const bool in = g < GA * 4 && pp < NPA;
+        a_r[k] = (2 * pp) / WX_TW;
+        a_c[k] = (2 * pp) % WX_TW;
+        a_m[k] = m0 + mq * 4;
+        a_ok[k] = in && a_m[k] < p.M;
+        a_lds[k] = in ? mq * 4 * WX_APITCH + 2 * pp : -1;
+    }
+    int b_r[NB], b_c[NB], b_n[NB], b_lds[NB];
+    bool b_ok[NB];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+        const int idx = tid + k * 512, l = idx & 63, g = idx >> 6;
+        const int pp = (l & 15) + 16 * (g % GB), nq = (l >> 4) + 4 * (g / GB);
+        const bool in = g < GB * 4 && pp < NPB;
+        b_r[k] = pp / PPR;
+        b_c[k] = 2 * (pp % PPR);
+        b_n[k] = n0 + nq * 4;
+        b_ok[k] = in && b_n[k] < p.N;
+        b_lds[k] = in ? nq * 4 * BP + b_r[k] * WX_PROW + b_c[k] : -1;
+    }
+    // frame coordinate of an extended-frame coordinate e (0 <= e < H + 2 circ), without a division
+    auto wrap = [&](int e, int H) {
+        int v = e - p.circ;
+        v = v < 0 ? v + H : v;
+        return v >= H ? v - H : v;
+    };
+    auto issue = [&](int t, f32x4 (&ra)[NA][2], f32x4 (&rb)[NB][2]) {
         const int b = t / (tiles_y * tiles_x);
         const int rr = t - b * tiles_y * tiles_x;
         const int oy0 = (rr / tiles_x) * WX_TH, ox0 = (rr % tiles_x) * WX_TW;
+        const float* ab = p.a + (size_t)b * p.Ha * p.Wa * p.M;
+        const float* xb = p.x + (size_t)b * p.Hx * p.Wx * p.N;
 #pragma unroll
         for (int k = 0; k < NA; ++k) {
-            const int idx = tid + k * 256;
-            const int pp = idx >> 4, mq = idx & 15;  // pixel pair pp: pixels 2pp, 2pp + 1 (one row)
-            const int oy = oy0 + (2 * pp) / WX_TW, ox = ox0 + (2 * pp) % WX_TW;
-            const int m = m0 + mq * 4;
+            const int oy = oy0 + a_r[k], ox = ox0 + a_c[k];
+            const bool ok = a_ok[k] && oy < p.Ha;
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                f32x4 v = {0.f, 0.f, 0.f, 0.f};
-                if (oy < p.Ha && ox + j < p.Wa && m < p.M)
-                    v = ld4c(p.a + ((size_t)(b * p.Ha + oy) * p.Wa + ox + j) * p.M, p.M, m);
-                ra[k][j] = v;
+            for (int j = 0; j < 2; ++j) {  // unconditional loads (zero page outside): exact vmcnt waits
+                const float* src = (ok && ox + j < p.Wa) ? ab + ((size_t)oy * p.Wa + ox + j) * p.M + a_m[k] : wx_zero4;
+                ra[k][j] = *reinterpret_cast<const f32x4*>(src);
             }
         }
 #pragma unroll
         for (int k = 0; k < NB; ++k) {
-            const int idx = tid + k * 256;
-            const int pp = idx >> 4, nq = idx & 15;
-            const int pr = (2 * pp) / PCE, pc = (2 * pp) % PCE;
-            const int n = n0 + nq * 4;
-            const int ye = oy0 + pr - p.pad_y;
-            const bool rok = pr < PR && ye >= 0 && ye < Hext && n < p.N;
-            const int y = p.circ ? nps::wrap_mod(ye - p.circ, p.Hx) : ye;
+            const int ye = oy0 + b_r[k] - p.pad_y;
+            const bool rok = b_ok[k] && ye >= 0 && ye < Hext;
+            const int y = wrap(ye, p.Hx);
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
-                const int xe = ox0 + pc + j - p.pad_x;
-                f32x4 v = {0.f, 0.f, 0.f, 0.f};
-                if (rok && pc + j < PC && xe >= 0 && xe < Wext) {
-                    const int x = p.circ ? nps::wrap_mod(xe - p.circ, p.Wx) : xe;
-                    v = ld4c(p.x + ((size_t)(b * p.Hx + y) * p.Wx + x) * p.N, p.N, n);
-                }
-                rb[k][j] = v;
+                const int xe = ox0 + b_c[k] + j - p.pad_x;
+                const bool ok = rok && b_c[k] + j < PC && xe >= 0 && xe < Wext;
+                const float* src = ok ? xb + ((size_t)y * p.Wx + wrap(xe, p.Wx)) * p.N + b_n[k] : wx_zero4;
+                rb[k][j] = *reinterpret_cast<const f32x4*>(src);
             }
         }
     };
-    // split a pixel pair's 4 channels into (hi, lo) fp16 and write each channel's 2 pixels as one b32
+    // split a pixel pair's 4 channels into (hi, lo) fp16; each channel's 2 pixels are one b32 write
     auto put = [&](_Float16* H, _Float16* L, int base, int pitch, const f32x4& v0, const f32x4& v1, float s) {
         f16x4 h0, l0, h1, l1;
         split4(v0 * s, h0, l0);
@@ -146,45 +176,41 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3_kernel(const nps_wgrad_t p, c
             *reinterpret_cast<h2f*>(L + base + e * pitch) = h2f{l0[e], l1[e]};
         }
     };
-    auto commit = [&]() {
+    auto commit = [&](int i, const f32x4 (&ra)[NA][2], const f32x4 (&rb)[NB][2]) {
+        _Float16* Ah = wsm + (i & 1) * BUF;
+        _Float16* Al = Ah + 64 * WX_APITCH;
+        _Float16* Bh = Al + 64 * WX_APITCH;
+        _Float16* Bl = Bh + 64 * BP;
 #pragma unroll
-        for (int k = 0; k < NA; ++k) {
-            const int idx = tid + k * 256;
-            const int pp = idx >> 4, mq = idx & 15;
-            put(Ah, Al, mq * 4 * WX_APITCH + 2 * pp, WX_APITCH, ra[k][0], ra[k][1], sa);
-        }
+        for (int k = 0; k < NA; ++k)
+            if (a_lds[k] >= 0) put(Ah, Al, a_lds[k], WX_APITCH, ra[k][0], ra[k][1], sa);
 #pragma unroll
-        for (int k = 0; k < NB; ++k) {
-            const int idx = tid + k * 256;
-            const int pp = idx >> 4, nq = idx & 15;
-            const int pr = (2 * pp) / PCE, pc = (2 * pp) % PCE;
-            if (pr < PR) put(Bh, Bl, nq * 4 * BP + pr * WX_PROW + pc, BP, rb[k][0], rb[k][1], sx);
-        }
+        for (int k = 0; k < NB; ++k)
+            if (b_lds[k] >= 0) put(Bh, Bl, b_lds[k], BP, rb[k][0], rb[k][1], sx);
     };
 
-    f32x16 acc[NT];
+    // ---- MFMA part
+    const int wm = wave & 1, wn = (wave >> 1) & 1, half = wave >> 2, h = lane >> 5;
+    f32x16 acc[NTW];
 #pragma unroll
-    for (int i = 0; i < NT; ++i)
+    for (int i = 0; i < NTW; ++i)
 #pragma unroll
         for (int j = 0; j < 16; ++j) acc[i][j] = 0.f;
     const int arow = (wm * 32 + (lane & 31)) * WX_APITCH + h * 8;
     const int brow = (wn * 32 + (lane & 31)) * BP + h * 8;
-
-    // the fetch registers are dead during the MFMA loop (register budget: 144 accumulators); the second
-    // work-group of the CU computes while this one fetches
-    for (int t = t_begin; t < t_end; ++t) {
-        issue(t);
-        __syncthreads();  // the previous tile's reads of the LDS planes are done
-        commit();
-        __syncthreads();
-#pragma unroll
-        for (int r = 0; r < WX_TH; ++r) {
+    // tap (ky, kx) of this wave's half -> its accumulator; the half's taps are a compile-time range per branch
+    auto compute_half = [&](const _Float16* Ah, const _Float16* Al, const _Float16* Bh, const _Float16* Bl,
+                            auto T0c, auto T1c, auto R0c, auto R1c) {
+        constexpr int T0 = decltype(T0c)::value, T1 = decltype(T1c)::value;
+        constexpr int R0 = decltype(R0c)::value, R1 = decltype(R1c)::value;
+        static_for<R1 - R0>([&](auto rc) {
+            constexpr int r = R0 + decltype(rc)::value;
             const f16x8 ah = *reinterpret_cast<const f16x8*>(Ah + arow + r * WX_TW);
             const f16x8 al = *reinterpret_cast<const f16x8*>(Al + arow + r * WX_TW);
-#pragma unroll
-            for (int ky = 0; ky < KH; ++ky) {
-                unsigned dh[6], dl[6];
-                {
+            static_for<KH>([&](auto kyc) {
+                constexpr int ky = decltype(kyc)::value;
+                if constexpr (ky * KW + KW > T0 && ky * KW < T1) {  // this row of taps meets [T0, T1)
+                    unsigned dh[6], dl[6];
                     const _Float16* ph = Bh + brow + (r + ky) * WX_PROW;
                     const _Float16* pl = Bl + brow + (r + ky) * WX_PROW;
                     const u32x4 h4 = *reinterpret_cast<const u32x4*>(ph);
@@ -204,41 +230,102 @@ __global__ __launch_bounds__(256, 2) void wgrad_x3_kernel(const nps_wgrad_t p, c
                     } else {
                         dh[4] = dh[5] = dl[4] = dl[5] = 0u;
                     }
+                    static_for<KW>([&](auto kxc) {
+                        constexpr int kx = decltype(kxc)::value;
+                        constexpr int tap = ky * KW + kx;
+                        if constexpr (tap >= T0 && tap < T1) {
+                            const f16x8 bh = shifted_run<kx>(dh), bl = shifted_run<kx>(dl);
+                            f32x16& c = acc[tap - T0];
+                            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, c, 0, 0, 0);
+                            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, c, 0, 0, 0);
+                            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, c, 0, 0, 0);
+                        }
+                    });
                 }
-                static_for<KW>([&](auto kxc) {
-                    constexpr int kx = decltype(kxc)::value;
-                    const f16x8 bh = shifted_run<kx>(dh), bl = shifted_run<kx>(dl);
-                    f32x16& c = acc[ky * KW + kx];
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, c, 0, 0, 0);
-                });
-            }
+            });
+        });
+    };
+    auto compute = [&](int i) {
+        const _Float16* Ah = wsm + (i & 1) * BUF;
+        const _Float16* Al = Ah + 64 * WX_APITCH;
+        const _Float16* Bh = Al + 64 * WX_APITCH;
+        const _Float16* Bl = Bh + 64 * BP;
+        using I = std::integral_constant<int, 0>;
+        if constexpr (ROWSPLIT) {
+            if (half == 0)
+                compute_half(Ah, Al, Bh, Bl, I{}, std::integral_constant<int, 1>{}, I{},
+                             std::integral_constant<int, WX_TH / 2>{});
+            else
+                compute_half(Ah, Al, Bh, Bl, I{}, std::integral_constant<int, 1>{},
+                             std::integral_constant<int, WX_TH / 2>{}, std::integral_constant<int, WX_TH>{});
+        } else {
+            if (half == 0)
+                compute_half(Ah, Al, Bh, Bl, I{}, std::integral_constant<int, NT0>{}, I{},
+                             std::integral_constant<int, WX_TH>{});
+            else
+                compute_half(Ah, Al, Bh, Bl, std::integral_constant<int, NT0>{}, std::integral_constant<int, NT>{},
+                             I{}, std::integral_constant<int, WX_TH>{});
         }
+    };
+
+    // ---- pipeline: local tile i is fetched into set i & 1 two tiles ahead, split into buffer i & 1 after
+    // the MFMAs of tile i - 1 (buffer (i - 1) & 1), computed after the next barrier
+    f32x4 a0[NA][2], b0[NB][2], a1[NA][2], b1[NB][2];
+    issue(t_begin, a0, b0);
+    if (nloc > 1) issue(t_begin + 1, a1, b1);
+    commit(0, a0, b0);
+    __syncthreads();  // tile 0 staged
+    for (int i = 0; i < nloc; i += 2) {
+        if (i + 2 < nloc) issue(t_begin + i + 2, a0, b0);
+        compute(i);
+        if (i + 1 < nloc) commit(i + 1, a1, b1);
+        __syncthreads();  // tile i read (buffer free), tile i + 1 staged
+        if (i + 1 >= nloc) break;
+        if (i + 3 < nloc) issue(t_begin + i + 3, a1, b1);
+        compute(i + 1);
+        if (i + 2 < nloc) commit(i + 2, a0, b0);
+        __syncthreads();
     }
 
-    // this split's partial into G: lane holds rows (r/4)*8 + h*4 + r%4, column lane%32
+    // this split's partial into the tap-major workspace W[tap][m][n]: lane holds rows (r/4)*8 + h*4 + r%4,
+    // column lane%32, so one atomic wave-instruction covers two 128-B runs (the full-rate shape; the
+    // [m][n][tap] order of G would scatter the 64 lanes 36 B apart)
     const float inv = 1.f / (sa * sx);
     const int n = n0 + wn * 32 + (lane & 31);
+    const int tbase = ROWSPLIT ? 0 : half * NT0;
+    const int ntw = ROWSPLIT ? 1 : (half == 0 ? NT0 : NT - NT0);
 #pragma unroll
-    for (int i = 0; i < NT; ++i) {
+    for (int i = 0; i < NTW; ++i) {
+        if (i >= ntw) continue;
+        float* wt = ws + (size_t)(tbase + i) * p.M * p.N;
 #pragma unroll
         for (int rr = 0; rr < 16; ++rr) {
             const int m = m0 + wm * 32 + (rr >> 2) * 8 + h * 4 + (rr & 3);
-            if (m < p.M && n < p.N) atomicAdd(p.g + ((size_t)m * p.N + n) * NT + i, acc[i][rr] * inv);
+            if (m < p.M && n < p.N) atomicAdd(wt + (size_t)m * p.N + n, acc[i][rr] * inv);
         }
     }
 }
 
+// G[m][n][tap] += W[tap][m][n]
+__global__ void wgrad_fold_kernel(const float* __restrict__ w, float* __restrict__ g, int MN, int nt) {
+    const long total = (long)MN * nt;
+    for (long o = (long)blockIdx.x * blockDim.x + threadIdx.x; o < total; o += (long)gridDim.x * blockDim.x) {
+        const long mn = o / nt;
+        const int t = (int)(o - mn * nt);
+        g[o] += w[(size_t)t * MN + mn];
+    }
+}
+
 template <int KH, int KW>
-int launch_wgrad_x3(const nps_wgrad_t& p, const float* ar, const float* xr, hipStream_t s) {
+int launch_wgrad_x3(const nps_wgrad_t& p, const float* ar, const float* xr, float* ws, hipStream_t s) {
     const long tiles_x = (p.Wa + WX_TW - 1) / WX_TW, tiles_y = (p.Ha + WX_TH - 1) / WX_TH;
     const long ntiles = (long)p.B * tiles_y * tiles_x;
     NPS_CHECK_ARG(ntiles < (1L << 30), "conv2d_wgrad_x3: too many tiles");
     const int n_mt = (p.M + 63) / 64, n_nt = (p.N + 63) / 64;
     const long base = (long)n_mt * n_nt;
-    // split K (pixel tiles) so the grid puts ~4 work-groups on each of the 256 CUs, >= 8 tiles each
-    long splits = (1024 + base - 1) / base;
+    // split K (pixel tiles): at most 2 work-groups in turn per CU (the first one's atomics overlap the
+    // second one's tiles; a grid just past a multiple of 256 would add a nearly empty round), >= 8 tiles each
+    long splits = 512 / base;
     const long max_splits = (ntiles + 7) / 8;
     if (splits > max_splits) splits = max_splits;
     if (splits < 1) splits = 1;
@@ -252,24 +339,40 @@ int launch_wgrad_x3(const nps_wgrad_t& p, const float* ar, const float* xr, hipS
                                   (int)lds);
         attr_set = true;
     }
-    wgrad_x3_kernel<KH, KW><<<dim3((unsigned)base, (unsigned)splits), 256, lds, s>>>(p, ar, xr, (int)ntiles, per, n_nt);
+    const size_t MN = (size_t)p.M * p.N;
+    if (hipMemsetAsync(ws, 0, sizeof(float) * MN * KH * KW, s) != hipSuccess) {
+        nps::set_error("conv2d_wgrad_x3: workspace memset failed");
+        return -2;
+    }
+    wgrad_x3_kernel<KH, KW><<<dim3((unsigned)base, (unsigned)splits), 512, lds, s>>>(p, ar, xr, ws, (int)ntiles, per,
+                                                                                    n_nt);
     NPS_CHECK_LAUNCH("conv2d_wgrad_x3");
+    const long total = (long)MN * KH * KW;
+    const long nb = (total + 255) / 256;
+    wgrad_fold_kernel<<<(unsigned)(nb < 2048 ? nb : 2048), 256, 0, s>>>(ws, p.g, (int)MN, KH * KW);
+    NPS_CHECK_LAUNCH("conv2d_wgrad_x3 (fold)");
     return 0;
 }
 
 }  // namespace
 
-extern "C" int nps_conv2d_wgrad_x3(const nps_wgrad_t* pp, const float* a_range, const float* x_range, void* stream) {
-    NPS_CHECK_ARG(pp != nullptr && a_range != nullptr && x_range != nullptr, "conv2d_wgrad_x3: null");
+extern "C" size_t nps_wgrad_x3_ws_floats(int M, int N, int KH, int KW) { return (size_t)M * N * KH * KW; }
+
+extern "C" int nps_conv2d_wgrad_x3(const nps_wgrad_t* pp, const float* a_range, const float* x_range, float* ws,
+                                   void* stream) {
+    NPS_CHECK_ARG(pp != nullptr && a_range != nullptr && x_range != nullptr && ws != nullptr, "conv2d_wgrad_x3: null");
     const nps_wgrad_t& p = *pp;
     NPS_CHECK_ARG(p.a && p.x && p.g && p.B > 0 && p.Ha > 0 && p.Wa > 0 && p.M > 0 && p.Hx > 0 && p.Wx > 0 && p.N > 0,
                   "conv2d_wgrad_x3: bad shape");
     NPS_CHECK_ARG(p.dil == 1 && p.circ >= 0 && p.KH == p.KW && (p.KH == 1 || p.KH == 2 || p.KH == 3),
                   "conv2d_wgrad_x3: kernel %dx%d dil %d unsupported (1x1 / 2x2 / 3x3, undilated)", p.KH, p.KW, p.dil);
+    NPS_CHECK_ARG((p.M & 3) == 0 && (p.N & 3) == 0 && (reinterpret_cast<size_t>(p.a) & 15) == 0 &&
+                      (reinterpret_cast<size_t>(p.x) & 15) == 0,
+                  "conv2d_wgrad_x3: channel counts %d, %d must be multiples of 4 (16-B pixel quads)", p.M, p.N);
     hipStream_t s = (hipStream_t)stream;
     switch (p.KH) {
-        case 1: return launch_wgrad_x3<1, 1>(p, a_range, x_range, s);
-        case 2: return launch_wgrad_x3<2, 2>(p, a_range, x_range, s);
-        default: return launch_wgrad_x3<3, 3>(p, a_range, x_range, s);
+        case 1: return launch_wgrad_x3<1, 1>(p, a_range, x_range, ws, s);
+        case 2: return launch_wgrad_x3<2, 2>(p, a_range, x_range, ws, s);
+        default: return launch_wgrad_x3<3, 3>(p, a_range, x_range, ws, s);
     }
 }

@@ -93,7 +93,8 @@ _SIGS = {
     # backward (training)
     "nps_wgrad_lds_bytes": (_sz, [_i, _i]),
     "nps_conv2d_wgrad": (_i, [ctypes.POINTER(WgradArgs), _vp]),
-    "nps_conv2d_wgrad_x3": (_i, [ctypes.POINTER(WgradArgs), _vp, _vp, _vp]),
+    "nps_wgrad_x3_ws_floats": (_sz, [_i, _i, _i, _i]),
+    "nps_conv2d_wgrad_x3": (_i, [ctypes.POINTER(WgradArgs), _vp, _vp, _vp, _vp]),
     "nps_channel_sums": (_i, [_vp, _l, _i, _vp, _vp]),
     "nps_frame_pack_bwd": (_i, [ctypes.POINTER(Conv2dArgs), _vp, ctypes.POINTER(ctypes.c_void_p), _vp, _vp, _vp, _vp]),
     "nps_gelu": (_i, [_vp, _vp, _l, _vp]),

@@ -33,8 +33,9 @@ def wgrad(a: torch.Tensor, x: torch.Tensor, KH: int, KW: int, dil=1, pad=(0, 0),
     """G[m][n][KH*KW] (+)= sum_pix a[pix][m] * Xext[pix + tap*dil - pad][n].
 
     Split-fp16 MFMA (nps_conv2d_wgrad_x3) under ops.CONV_PRECISION == PREC_X3F16 for undilated square
-    kernels up to 3x3 — a and x range-scaled from their max |.| (a_range: a's range tag when the caller
-    already has it) — else exact fp32 MFMA (nps_conv2d_wgrad)."""
+    kernels up to 3x3 over channel counts that are multiples of 4 — a and x range-scaled from their
+    max |.| (a_range: a's range tag when the caller already has it) — else exact fp32 MFMA
+    (nps_conv2d_wgrad)."""
     a, x = _c(a), _c(x)
     B, Ha, Wa, M = a.shape
     _, Hx, Wx, N = x.shape
@@ -45,13 +46,14 @@ def wgrad(a: torch.Tensor, x: torch.Tensor, KH: int, KW: int, dil=1, pad=(0, 0),
     p.x, p.Hx, p.Wx, p.N = ptr(x), Hx, Wx, N
     p.KH, p.KW, p.dil, p.pad_y, p.pad_x, p.circ = KH, KW, dil, pad[0], pad[1], circ
     p.g = ptr(g)
-    if ops.CONV_PRECISION == ops.PREC_X3F16 and KH == KW and KH <= 3 and dil == 1:
+    if ops.CONV_PRECISION == ops.PREC_X3F16 and KH == KW and KH <= 3 and dil == 1 and M % 4 == 0 and N % 4 == 0:
         ar = a_range if a_range is not None else ops.absmax(a)
         xr = ops.absmax(x)
+        ws = torch.empty(lib.nps_wgrad_x3_ws_floats(M, N, KH, KW), dtype=torch.float32, device=a.device)
         arith = "x3w"
 
         def launch():
-            check(lib.nps_conv2d_wgrad_x3(ctypes.byref(p), ptr(ar), ptr(xr), stream_ptr()), "conv2d_wgrad_x3")
+            check(lib.nps_conv2d_wgrad_x3(ctypes.byref(p), ptr(ar), ptr(xr), ptr(ws), stream_ptr()), "conv2d_wgrad_x3")
     else:
         arith = "f32w"
 
