@@ -276,13 +276,22 @@ __global__ void transpose_kernel(const float* __restrict__ in, float* __restrict
 // (dec_grid.py:126-146 + add_delta :8-31 + tanh + mask), then back-propagated:
 //   gpre[b][ci*L + j][pix]  (planar, like the forward's pre-decoder output)
 //   ws[block][w1 | b1 | w2 | b2]  per-block parameter-gradient partials (summed by nps_channel_sums).
+// NC_ > 0: the loop bounds (num_c, tw and the derived kernel sizes) are compile-time, so the inner
+// reductions unroll (their LDS reads issue back to back instead of one latency per FMA) and the weights
+// become scalar loads; NC_ == 0 is the generic form (the arguments decide).
+template <int NC_, int TW_>
 __global__ __launch_bounds__(64) void timeconv_bwd_kernel(
     const float* __restrict__ pre, const float* __restrict__ u, const float* __restrict__ w1,
     const float* __restrict__ b1, const float* __restrict__ w2, const float* __restrict__ b2,
     const float* __restrict__ dtcum, const float* __restrict__ mask, int mask_S, int mask_ch,
-    const float* __restrict__ gout, float* __restrict__ gpre, float* __restrict__ ws, int nc, int tw, int HW, int ka,
-    int kb, int L1, int act_tanh, int nparams) {
+    const float* __restrict__ gout, float* __restrict__ gpre, float* __restrict__ ws, int nc_, int tw_, int HW,
+    int ka_, int kb_, int L1_, int act_tanh, int nparams) {
     extern __shared__ float lds[];
+    constexpr bool CT = NC_ > 0;
+    constexpr int KA_C = (TW_ + 1) / 2, KB_C = (TW_ + 3) / 4 + 1 + (TW_ % 4 == 0 ? 1 : 0);
+    constexpr int L1_C = (3 * TW_ - KA_C) / 2 + 1;
+    const int nc = CT ? NC_ : nc_, tw = CT ? TW_ : tw_;
+    const int ka = CT ? KA_C : ka_, kb = CT ? KB_C : kb_, L1 = CT ? L1_C : L1_;
     const int C2 = 2 * nc, L = 3 * tw;
     float* d1 = lds;                       // [C2*L1][64]  GELU(conv1)
     float* gd = lds + C2 * L1 * 64;        // [C2*L1][64]  GELU'(conv1) -> grad of conv1 pre-activation
@@ -297,7 +306,9 @@ __global__ __launch_bounds__(64) void timeconv_bwd_kernel(
     for (int o = 0; o < C2; ++o)
         for (int t1 = 0; t1 < L1; ++t1) {
             float acc = b1[o];
+#pragma unroll
             for (int ci = 0; ci < nc; ++ci)
+#pragma unroll
                 for (int k = 0; k < ka; ++k) acc = fmaf(w1[(o * nc + ci) * ka + k], xb[(size_t)(ci * L + 2 * t1 + k) * HW], acc);
             const float z = acc;
             d1[(o * L1 + t1) * 64 + p] = nps::gelu_erf(z);
@@ -310,7 +321,9 @@ __global__ __launch_bounds__(64) void timeconv_bwd_kernel(
         const float ulast = u[(((size_t)b * nc + o2) * tw + (tw - 1)) * HW + pc];
         for (int t = 0; t < tw; ++t) {
             float acc = b2[o2];
+#pragma unroll
             for (int o = 0; o < C2; ++o)
+#pragma unroll
                 for (int k = 0; k < kb; ++k) acc = fmaf(w2[(o2 * C2 + o) * kb + k], d1[(o * L1 + t + k) * 64 + p], acc);
             float g = valid ? gout[(((size_t)b * nc + o2) * tw + t) * HW + pix] : 0.f;
             if (mask) g = g - m * g;
@@ -325,12 +338,14 @@ __global__ __launch_bounds__(64) void timeconv_bwd_kernel(
     const int ow1 = 0, ob1 = C2 * nc * ka, ow2 = ob1 + C2, ob2 = ow2 + nc * C2 * kb;
     for (int o2 = 0; o2 < nc; ++o2) {
         float sb = 0.f;
+#pragma unroll
         for (int t = 0; t < tw; ++t) sb += gd2[(o2 * tw + t) * 64 + p];
         sb = nps::wave_sum((double)sb);
         if (p == 0) ws[blk * nparams + ob2 + o2] = sb;
         for (int o = 0; o < C2; ++o)
             for (int k = 0; k < kb; ++k) {
                 float s2 = 0.f;
+#pragma unroll
                 for (int t = 0; t < tw; ++t) s2 = fmaf(gd2[(o2 * tw + t) * 64 + p], d1[(o * L1 + t + k) * 64 + p], s2);
                 s2 = (float)nps::wave_sum((double)s2);
                 if (p == 0) ws[blk * nparams + ow2 + (o2 * C2 + o) * kb + k] = s2;
@@ -340,7 +355,9 @@ __global__ __launch_bounds__(64) void timeconv_bwd_kernel(
     for (int o = 0; o < C2; ++o)
         for (int t1 = 0; t1 < L1; ++t1) {
             float g = 0.f;
+#pragma unroll
             for (int o2 = 0; o2 < nc; ++o2)
+#pragma unroll
                 for (int k = 0; k < kb; ++k) {
                     const int t = t1 - k;
                     if (t >= 0 && t < tw) g = fmaf(gd2[(o2 * tw + t) * 64 + p], w2[(o2 * C2 + o) * kb + k], g);
@@ -350,12 +367,14 @@ __global__ __launch_bounds__(64) void timeconv_bwd_kernel(
     // 5. parameter partials of conv1: w1[o][ci][k], b1[o]
     for (int o = 0; o < C2; ++o) {
         float sb = 0.f;
+#pragma unroll
         for (int t1 = 0; t1 < L1; ++t1) sb += gd[(o * L1 + t1) * 64 + p];
         sb = (float)nps::wave_sum((double)sb);
         if (p == 0) ws[blk * nparams + ob1 + o] = sb;
         for (int ci = 0; ci < nc; ++ci)
             for (int k = 0; k < ka; ++k) {
                 float s1 = 0.f;
+#pragma unroll
                 for (int t1 = 0; t1 < L1; ++t1)
                     s1 = fmaf(gd[(o * L1 + t1) * 64 + p], xb[(size_t)(ci * L + 2 * t1 + k) * HW], s1);
                 s1 = (float)nps::wave_sum((double)s1);
@@ -368,9 +387,11 @@ __global__ __launch_bounds__(64) void timeconv_bwd_kernel(
     for (int ci = 0; ci < nc; ++ci)
         for (int j = 0; j < L; ++j) {
             float g = 0.f;
-            for (int k = (j & 1); k < ka; k += 2) {   // 2 t1 + k = j
+#pragma unroll
+            for (int k = 0; k < ka; ++k) {   // 2 t1 + k = j
                 const int t1 = (j - k) >> 1;
-                if (j - k < 0 || t1 >= L1) continue;
+                if (((j - k) & 1) || j - k < 0 || t1 >= L1) continue;
+#pragma unroll
                 for (int o = 0; o < C2; ++o) g = fmaf(gd[(o * L1 + t1) * 64 + p], w1[(o * nc + ci) * ka + k], g);
             }
             gb[(size_t)(ci * L + j) * HW] = g;
@@ -562,14 +583,26 @@ extern "C" int nps_timeconv_decode_bwd(const float* pre, const float* u, const f
     NPS_CHECK_ARG(lds <= 160 * 1024, "timeconv_decode_bwd: num_c=%d tw=%d too large", num_c, tw);
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)timeconv_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void*)timeconv_bwd_kernel<0, 0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        (void)hipFuncSetAttribute((const void*)timeconv_bwd_kernel<3, 25>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        (void)hipFuncSetAttribute((const void*)timeconv_bwd_kernel<1, 25>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   160 * 1024);
         attr_set = true;
     }
     const int HW = H * W;
-    timeconv_bwd_kernel<<<dim3((HW + 63) / 64, B), 64, lds, (hipStream_t)stream>>>(
-        pre, u, w1, b1, w2, b2, dtcum, mask, mask_S, mask_ch, gout, gpre, ws, num_c, tw, HW, ka, kb, L1, act_tanh,
-        nparams);
+    const dim3 grid((HW + 63) / 64, B);
+    hipStream_t s = (hipStream_t)stream;
+    if (num_c == 3 && tw == 25)  // the twophase cfgs (3 fields / 1 field, time_window 25)
+        timeconv_bwd_kernel<3, 25><<<grid, 64, lds, s>>>(pre, u, w1, b1, w2, b2, dtcum, mask, mask_S, mask_ch, gout,
+                                                         gpre, ws, num_c, tw, HW, ka, kb, L1, act_tanh, nparams);
+    else if (num_c == 1 && tw == 25)
+        timeconv_bwd_kernel<1, 25><<<grid, 64, lds, s>>>(pre, u, w1, b1, w2, b2, dtcum, mask, mask_S, mask_ch, gout,
+                                                         gpre, ws, num_c, tw, HW, ka, kb, L1, act_tanh, nparams);
+    else
+        timeconv_bwd_kernel<0, 0><<<grid, 64, lds, s>>>(pre, u, w1, b1, w2, b2, dtcum, mask, mask_S, mask_ch, gout,
+                                                        gpre, ws, num_c, tw, HW, ka, kb, L1, act_tanh, nparams);
     NPS_CHECK_LAUNCH("timeconv_decode_bwd");
     return 0;
 }
