@@ -199,6 +199,29 @@ __global__ void channel_sums_kernel(const float* __restrict__ x, long rows, int 
     for (int c = threadIdx.x; c < C; c += blockDim.x) atomicAdd(&out[c], part[c]);
 }
 
+// The same for C % 4 == 0, C <= 1024: thread = one channel quad (fixed) x rows lr, lr + per, ... of the
+// block's range, summed in registers from 16-B loads; one LDS add per channel per thread at the end.
+__global__ void channel_sums4_kernel(const float* __restrict__ x, long rows, int C, int rows_per_block,
+                                     float* __restrict__ out) {
+    extern __shared__ float part[];  // [C]
+    for (int c = threadIdx.x; c < C; c += blockDim.x) part[c] = 0.f;
+    __syncthreads();
+    const int Q = C >> 2, per = blockDim.x / Q;
+    const int q = threadIdx.x % Q, lr = threadIdx.x / Q;
+    const long r0 = (long)blockIdx.x * rows_per_block;
+    const long r1 = min(rows, r0 + rows_per_block);
+    if (lr < per) {
+        f32x4 s = {0.f, 0.f, 0.f, 0.f};
+        const f32x4* xp = reinterpret_cast<const f32x4*>(x) + q;
+#pragma unroll 4
+        for (long rr = r0 + lr; rr < r1; rr += per) s += xp[rr * Q];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) atomicAdd(&part[4 * q + e], s[e]);
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += blockDim.x) atomicAdd(&out[c], part[c]);
+}
+
 // ------------------------------------------------------------------------------ element-wise
 __device__ __forceinline__ float gelu_grad(float z) {
     // d/dz [0.5 z (1 + erf(z/sqrt2))] = Phi(z) + z phi(z)
@@ -403,6 +426,185 @@ __global__ void frame_bwd_apply_kernel(nps_conv2d_t a, const float* __restrict__
     }
 }
 
+// Quad forms of the frame backward (every source's C, Cin and the GroupNorm group size multiples of 4, so
+// a channel quad lies in one source and one group): thread = one fixed channel quad x pixels lr, lr + per,
+// ... of the block's pixel range (row / column stepped, no per-element division), 16-B loads and stores,
+// the reduce pass's sums in registers until one LDS add per channel per thread.
+struct FrameQuad {  // the source, GroupNorm operands and source origin of a thread's channel quad
+    const float* ptr;
+    int C, H, W, oy, ox, cs;
+    f32x4 gam, bet;
+    float2 mr;
+};
+__device__ __forceinline__ FrameQuad frame_quad(const nps_conv2d_t& a, int c0, const float2* tab, int cpg) {
+    FrameQuad f;
+    int lo = 0, si = 0, base = 0;
+#pragma unroll
+    for (int k = 0; k < NPS_MAX_SRC; ++k)
+        if (k < a.nsrc) {
+            const int C = k == 0 ? a.src[0].C : (k == 1 ? a.src[1].C : a.src[2].C);
+            if (c0 >= lo && c0 < lo + C) {
+                si = k;
+                base = lo;
+            }
+            lo += C;
+        }
+    const nps_src_t S = si == 0 ? a.src[0] : (si == 1 ? a.src[1] : a.src[2]);
+    f.ptr = S.ptr;
+    f.C = S.C;
+    f.H = S.H;
+    f.W = S.W;
+    f.oy = S.off_y;
+    f.ox = S.off_x;
+    f.cs = c0 - base;
+    if (a.gn_stats) {
+        f.gam = *reinterpret_cast<const f32x4*>(a.gn_gamma + c0);
+        f.bet = *reinterpret_cast<const f32x4*>(a.gn_beta + c0);
+        f.mr = tab[c0 / cpg];
+    } else {
+        f.gam = f32x4{1.f, 1.f, 1.f, 1.f};
+        f.bet = f32x4{0.f, 0.f, 0.f, 0.f};
+        f.mr = make_float2(0.f, 1.f);
+    }
+    return f;
+}
+
+__global__ void frame_bwd_reduce4_kernel(nps_conv2d_t a, const float* __restrict__ gy, double* __restrict__ PQ,
+                                         int px_per_block) {
+    extern __shared__ float part[];  // [2][Cin]
+    __shared__ float2 tab[16];
+    const int b = blockIdx.y;
+    gn_tab_fill(a, b, tab);
+    for (int c = threadIdx.x; c < 2 * a.Cin; c += blockDim.x) part[c] = 0.f;
+    __syncthreads();
+    const int Q = a.Cin >> 2, per = blockDim.x / Q;
+    const int q = threadIdx.x % Q, lr = threadIdx.x / Q;
+    const int npix = a.Hin * a.Win;
+    const int p0 = blockIdx.x * px_per_block, p1 = min(npix, p0 + px_per_block);
+    if (lr < per && p0 + lr < p1) {
+        const int cpg = a.gn_stats ? a.Cin / a.gn_groups : 1;
+        const FrameQuad f = frame_quad(a, 4 * q, tab, cpg);
+        const float* sb = f.ptr + (size_t)b * f.H * f.W * f.C + f.cs;
+        const float* g = gy + (size_t)b * npix * a.Cin + 4 * q;
+        f32x4 P = {0.f, 0.f, 0.f, 0.f}, Qs = {0.f, 0.f, 0.f, 0.f};
+        int pix = p0 + lr;
+        int y = pix / a.Win, x = pix - y * a.Win;
+        const int dy = per / a.Win, dx = per - dy * a.Win;
+        for (; pix < p1; pix += per) {
+            const int yy = y - f.oy, xx = x - f.ox;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if (yy >= 0 && yy < f.H && xx >= 0 && xx < f.W) v = *reinterpret_cast<const f32x4*>(sb + ((size_t)yy * f.W + xx) * f.C);
+            f32x4 gz = *reinterpret_cast<const f32x4*>(g + (size_t)pix * a.Cin);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float xh = a.gn_stats ? (v[e] - f.mr.x) * f.mr.y : v[e];
+                const float z = a.gn_stats ? xh * f.gam[e] + f.bet[e] : v[e];
+                if (a.pre_act == 1) gz[e] *= gelu_grad(z);
+                P[e] += gz[e];
+                Qs[e] = fmaf(gz[e], xh, Qs[e]);
+            }
+            x += dx;
+            y += dy;
+            if (x >= a.Win) {
+                x -= a.Win;
+                ++y;
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            atomicAdd(&part[4 * q + e], P[e]);
+            atomicAdd(&part[a.Cin + 4 * q + e], Qs[e]);
+        }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < a.Cin; c += blockDim.x) {
+        atomicAdd(&PQ[(b * 2) * a.Cin + c], (double)part[c]);
+        atomicAdd(&PQ[(b * 2 + 1) * a.Cin + c], (double)part[a.Cin + c]);
+    }
+}
+
+__global__ void frame_bwd_apply4_kernel(nps_conv2d_t a, const float* __restrict__ gy, const double* __restrict__ PQ,
+                                        float* d0, float* d1, float* d2, float* __restrict__ dgamma,
+                                        float* __restrict__ dbeta, int px_per_block) {
+    __shared__ float2 tab[16];
+    __shared__ float s12[16][2];
+    const int b = blockIdx.y, si = blockIdx.z;
+    gn_tab_fill(a, b, tab);
+    const int cpg = a.gn_stats ? a.Cin / a.gn_groups : 1;
+    if (a.gn_stats && threadIdx.x < a.gn_groups) {
+        double s1 = 0.0, s2 = 0.0;
+        for (int c = threadIdx.x * cpg; c < (threadIdx.x + 1) * cpg; ++c) {
+            s1 += (double)a.gn_gamma[c] * PQ[(b * 2) * a.Cin + c];
+            s2 += (double)a.gn_gamma[c] * PQ[(b * 2 + 1) * a.Cin + c];
+        }
+        const double N = (double)cpg * a.Hin * a.Win;
+        s12[threadIdx.x][0] = (float)(s1 / N);
+        s12[threadIdx.x][1] = (float)(s2 / N);
+    }
+    if (a.gn_stats && b == 0 && si == 0 && blockIdx.x == 0 && dgamma) {
+        for (int c = threadIdx.x; c < a.Cin; c += blockDim.x) {
+            double sg = 0.0, sb = 0.0;
+            for (int bb = 0; bb < a.B; ++bb) {
+                sb += PQ[(bb * 2) * a.Cin + c];
+                sg += PQ[(bb * 2 + 1) * a.Cin + c];
+            }
+            dgamma[c] = (float)sg;
+            dbeta[c] = (float)sb;
+        }
+    }
+    __syncthreads();
+    float* dst = si == 0 ? d0 : (si == 1 ? d1 : d2);
+    if (dst == nullptr) return;
+    const nps_src_t S = si == 0 ? a.src[0] : (si == 1 ? a.src[1] : a.src[2]);
+    const int lo = si == 0 ? 0 : (si == 1 ? a.src[0].C : a.src[0].C + a.src[1].C);
+    const int Q = S.C >> 2, per = blockDim.x / Q;
+    const int q = threadIdx.x % Q, lr = threadIdx.x / Q;
+    const int npix = S.H * S.W;
+    const int p0 = blockIdx.x * px_per_block, p1 = min(npix, p0 + px_per_block);
+    if (lr >= per || p0 + lr >= p1) return;
+    const int c0 = lo + 4 * q;
+    const int gidx = c0 / cpg;
+    const float2 mr = a.gn_stats ? tab[gidx] : make_float2(0.f, 1.f);
+    const float t1 = a.gn_stats ? s12[gidx][0] : 0.f, t2 = a.gn_stats ? s12[gidx][1] : 0.f;
+    f32x4 gam = {1.f, 1.f, 1.f, 1.f}, bet = {0.f, 0.f, 0.f, 0.f};
+    if (a.gn_stats) {
+        gam = *reinterpret_cast<const f32x4*>(a.gn_gamma + c0);
+        bet = *reinterpret_cast<const f32x4*>(a.gn_beta + c0);
+    }
+    const float* sp = S.ptr + (size_t)b * npix * S.C + 4 * q;
+    float* dp = dst + (size_t)b * npix * S.C + 4 * q;
+    const float* g = gy + (size_t)b * a.Hin * a.Win * a.Cin + c0;
+    int pix = p0 + lr;
+    int ys = pix / S.W, xs = pix - ys * S.W;
+    const int dy = per / S.W, dx = per - dy * S.W;
+    for (; pix < p1; pix += per) {
+        const int y = ys + S.off_y, x = xs + S.off_x;
+        f32x4 d = {0.f, 0.f, 0.f, 0.f};
+        if (y >= 0 && y < a.Hin && x >= 0 && x < a.Win) {
+            const f32x4 v = *reinterpret_cast<const f32x4*>(sp + (size_t)pix * S.C);
+            f32x4 gz = *reinterpret_cast<const f32x4*>(g + ((size_t)y * a.Win + x) * a.Cin);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                if (a.gn_stats) {
+                    const float xh = (v[e] - mr.x) * mr.y;
+                    if (a.pre_act == 1) gz[e] *= gelu_grad(xh * gam[e] + bet[e]);
+                    d[e] = mr.y * (gam[e] * gz[e] - t1 - xh * t2);
+                } else {
+                    if (a.pre_act == 1) gz[e] *= gelu_grad(v[e]);
+                    d[e] = gz[e];
+                }
+            }
+        }
+        *reinterpret_cast<f32x4*>(dp + (size_t)pix * S.C) = d;
+        xs += dx;
+        ys += dy;
+        if (xs >= S.W) {
+            xs -= S.W;
+            ++ys;
+        }
+    }
+}
+
 inline int grid_for(long n, int per_block = 256 * 8, int cap = 4096) {
     long nb = (n + per_block - 1) / per_block;
     return (int)(nb < 1 ? 1 : (nb > cap ? cap : nb));
@@ -455,7 +657,10 @@ extern "C" int nps_channel_sums(const float* x, long rows, int C, float* out, vo
     const int rpb = 256;
     const long nb = (rows + rpb - 1) / rpb;
     NPS_CHECK_ARG(nb < (1L << 31), "channel_sums: too many rows");
-    channel_sums_kernel<<<(unsigned)nb, 256, sizeof(float) * C, (hipStream_t)stream>>>(x, rows, C, rpb, out);
+    if ((C & 3) == 0 && C <= 1024 && (reinterpret_cast<size_t>(x) & 15) == 0)
+        channel_sums4_kernel<<<(unsigned)nb, 256, sizeof(float) * C, (hipStream_t)stream>>>(x, rows, C, rpb, out);
+    else
+        channel_sums_kernel<<<(unsigned)nb, 256, sizeof(float) * C, (hipStream_t)stream>>>(x, rows, C, rpb, out);
     NPS_CHECK_LAUNCH("channel_sums");
     return 0;
 }
@@ -520,22 +725,41 @@ extern "C" int nps_frame_pack_bwd(const nps_conv2d_t* ap, const float* gy, float
                                   a.gn_beta && work),
                   "frame_pack_bwd: bad GroupNorm");
     hipStream_t s = (hipStream_t)stream;
+    // quad kernels: every channel count a multiple of 4 (so is the GroupNorm group), 16-B aligned tensors
+    bool quad = (a.Cin & 3) == 0 && a.Cin <= 1024 && (reinterpret_cast<size_t>(gy) & 15) == 0 &&
+                (!a.gn_stats || ((a.Cin / a.gn_groups) & 3) == 0);
+    for (int i = 0; i < a.nsrc; ++i)
+        quad = quad && (a.src[i].C & 3) == 0 && (reinterpret_cast<size_t>(a.src[i].ptr) & 15) == 0 &&
+               (dsrc[i] == nullptr || (reinterpret_cast<size_t>(dsrc[i]) & 15) == 0);
+    const int npix = a.Hin * a.Win;
+    const int PXB = 256;  // pixels per block of the quad kernels
     if (a.gn_stats) {
         NPS_CHECK_ARG(a.Cin <= 4096, "frame_pack_bwd: Cin too large");
         if (hipMemsetAsync(work, 0, sizeof(double) * 2 * a.B * a.Cin, s) != hipSuccess) {
             nps::set_error("frame_pack_bwd: memset failed");
             return -2;
         }
-        const long n = (long)a.Hin * a.Win * a.Cin;
-        frame_bwd_reduce_kernel<<<dim3(grid_for(n, 256 * 16, 1024), a.B), 256, sizeof(float) * 2 * a.Cin, s>>>(a, gy,
-                                                                                                            work);
+        const long n = (long)npix * a.Cin;
+        if (quad)
+            frame_bwd_reduce4_kernel<<<dim3((npix + PXB - 1) / PXB, a.B), 256, sizeof(float) * 2 * a.Cin, s>>>(
+                a, gy, work, PXB);
+        else
+            frame_bwd_reduce_kernel<<<dim3(grid_for(n, 256 * 16, 1024), a.B), 256, sizeof(float) * 2 * a.Cin, s>>>(
+                a, gy, work);
         NPS_CHECK_LAUNCH("frame_pack_bwd reduce");
     }
-    long nmax = 1;
-    for (int i = 0; i < a.nsrc; ++i) nmax = std::max(nmax, (long)a.src[i].H * a.src[i].W * a.src[i].C);
+    long nmax = 1, pmax = 1;
+    for (int i = 0; i < a.nsrc; ++i) {
+        nmax = std::max(nmax, (long)a.src[i].H * a.src[i].W * a.src[i].C);
+        pmax = std::max(pmax, (long)a.src[i].H * a.src[i].W);
+    }
     float* d[3] = {dsrc[0], a.nsrc > 1 ? dsrc[1] : nullptr, a.nsrc > 2 ? dsrc[2] : nullptr};
-    frame_bwd_apply_kernel<<<dim3(grid_for(nmax, 256 * 8, 2048), a.B, a.nsrc), 256, 0, s>>>(a, gy, work, d[0], d[1],
-                                                                                           d[2], dgamma, dbeta);
+    if (quad)
+        frame_bwd_apply4_kernel<<<dim3((unsigned)((pmax + PXB - 1) / PXB), a.B, a.nsrc), 256, 0, s>>>(
+            a, gy, work, d[0], d[1], d[2], dgamma, dbeta, PXB);
+    else
+        frame_bwd_apply_kernel<<<dim3(grid_for(nmax, 256 * 8, 2048), a.B, a.nsrc), 256, 0, s>>>(a, gy, work, d[0], d[1],
+                                                                                               d[2], dgamma, dbeta);
     NPS_CHECK_LAUNCH("frame_pack_bwd apply");
     return 0;
 }
