@@ -36,6 +36,23 @@ __host__ __device__ constexpr int x3_patch_px_max(int ntaps, int tile_px) {
 }
 
 #define X3_MFMA __builtin_amdgcn_mfma_f32_32x32x16_f16
+#ifndef NPS_X3_PRIO
+#define NPS_X3_PRIO 1
+#endif
+#ifndef NPS_X3_REMAP
+#define NPS_X3_REMAP 0
+#endif
+// Producer slot -> (patch pixel, channel quad).  REMAP: the 16 lanes of one ds_write_b64 group take
+// pixels {0, 2, 4, 6} (lanes 16-31: {1, 3, 5, 7}) of a run of 8, whose 32-B [hi] / [lo] runs at the 80-B
+// pixel pitch land on disjoint banks (consecutive pixels collide: 20 p mod 32 repeats within 4).
+__device__ __forceinline__ int x3_slot_px(int idx) {
+#if NPS_X3_REMAP
+    const int j = idx & 31;
+    return ((idx >> 5) << 3) + ((j >> 2) & 3) * 2 + (j >> 4);
+#else
+    return idx >> 2;
+#endif
+}
 
 #ifdef NPS_X3_STAMP  // dev diagnostic: per-work-group s_memtime stamps of consumer wave 0
 __device__ unsigned long long x3_stamps[1 << 20];
@@ -143,7 +160,6 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
         ox0 = (tx % g.T) + (tx / g.T) * a.TW * g.T;
     };
     const int npix = g.PH * g.PW;
-    const int NG = npix * 4;                              // float4 slots of a 16-channel patch stage
     const int stage_b = (npix * X3_PIXB + 15) & ~15;
     char* ring = reinterpret_cast<char*>(smem) + 128;
     const int nstages = (a.Cin + CK - 1) / CK;
@@ -151,6 +167,14 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
     const bool lds_epi = x3_lds_epilogue(a);
     auto barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
 
+    // static priority for the producer half (MI355X_MICROARCH 'Two waves per SIMD' item 4): they win the
+    // VALU arbitration against their SIMD partner's MFMA stream; same-box A/B: 3x3 class -1.7 % per call
+    // (tools/ab_prio.sh; NPS_X3_PRIO=0 / 2: none / the consumers instead)
+#if NPS_X3_PRIO == 1
+    if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+#elif NPS_X3_PRIO == 2
+    if (wave < 4) __builtin_amdgcn_s_setprio(1);
+#endif
     if (wave >= 4) {
         // ------------------------------------------------------------------ producers: patch only
         const int ptid = tid - 256;
@@ -184,10 +208,10 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
 #pragma unroll
             for (int k = 0; k < MAXP; ++k) {
                 const int idx = ptid + k * 256;
-                const int p = idx >> 2;
+                const int p = x3_slot_px(idx);
                 const int pr = p / g.PW, pc = p - pr * g.PW;
                 const int ye = ybase + pr * g.rstep, xe = xbase + pc * g.rstep;
-                bool ok = idx < NG && ye >= 0 && ye < Hext && xe >= 0 && xe < Wext;
+                bool ok = p < npix && ye >= 0 && ye < Hext && xe >= 0 && xe < Wext;
                 finm = ok ? (finm | (1u << k)) : finm;
                 const int fy = a.circ ? nps::wrap_mod(ye - a.circ, a.Hin) : ye;
                 const int fx = a.circ ? nps::wrap_mod(xe - a.circ, a.Win) : xe;
@@ -264,7 +288,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
 #pragma unroll
             for (int k = 0; k < MAXP; ++k) {
                 const int idx = ptid + k * 256;
-                if (idx < NG) {
+                if (x3_slot_px(idx) < npix) {
                     const f32x4 z = {0.f, 0.f, 0.f, 0.f};
                     f16x4 hi, lo;
                     f32x4 v = ((okm >> k) & 1u) ? rp[k] : z;
@@ -284,7 +308,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
                         }
                     }
                     split4(v * xs, hi, lo);
-                    char* base = Pt + (idx >> 2) * X3_PIXB + (idx & 3) * 8;
+                    char* base = Pt + x3_slot_px(idx) * X3_PIXB + (idx & 3) * 8;
                     *reinterpret_cast<f16x4*>(base) = hi;
                     *reinterpret_cast<f16x4*>(base + 32) = lo;
                 }
