@@ -635,7 +635,7 @@ extern "C" int nps_conv2d_plan(nps_conv2d_t* a) {
         // scored by the useful fraction of the launched pixels x the fill of the last round of
         // work-groups over the 256 CUs; 256-pixel tiles carry a 10 % penalty (half the reuse of
         // each weight fragment per global load)
-        // Wide tiles (8x16, 4x32, 16x8 pixels x 192 channels) replace them for 2x2 / 3x3 convs with
+        // Wide tiles (16x8, 8x16, 4x32 pixels x 192 channels) replace them for 2x2 / 3x3 convs with
         // 128 < Cout <= 192: one staged patch feeds all the output channels (dev knob NPS_X3_WIDE=0: off).
         static int wide_on = -1;
         if (wide_on < 0) {
@@ -643,11 +643,19 @@ extern "C" int nps_conv2d_plan(nps_conv2d_t* a) {
             wide_on = (e != nullptr && e[0] == '0') ? 0 : 1;
         }
         const bool wide = wide_on && x3_wide_eligible(*a);
-        const int cand[8][2] = {{16, 32}, {32, 16}, {8, 64}, {16, 16}, {8, 32}, {8, 16}, {4, 32}, {16, 8}};
+        // wide candidates in preference order: 16x8 first (same-box A/B at C3: 3x3 class -1.7 % against 8x16,
+        // equal FETCH_SIZE; profiles/r2s2/tile_ab)
+        const int cand[8][2] = {{16, 32}, {32, 16}, {8, 64}, {16, 16}, {8, 32}, {16, 8}, {8, 16}, {4, 32}};
         const long units = wide ? (a->Cout + 191) / 192 : units_co;
+        static int wide_tile = -2;  // dev knob NPS_X3_WIDE_TILE=0/1/2: force 16x8 / 8x16 / 4x32 wide tiles
+        if (wide_tile == -2) {
+            const char* e = getenv("NPS_X3_WIDE_TILE");
+            wide_tile = (e != nullptr && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : -1;
+        }
         int best = -1;
         double best_eff = -1.0;
         for (int i = wide ? 5 : 0; i < (wide ? 8 : 5); ++i) {
+            if (wide && wide_tile >= 0 && i != 5 + wide_tile) continue;
             nps_conv2d_t t = *a;
             t.waves = 8;
             t.TH = cand[i][0];
