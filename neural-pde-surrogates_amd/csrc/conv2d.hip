@@ -645,16 +645,16 @@ extern "C" int nps_conv2d_plan(nps_conv2d_t* a) {
         const bool wide = wide_on && x3_wide_eligible(*a);
         // wide candidates in preference order: 16x8 first (same-box A/B at C3: 3x3 class -1.7 % against 8x16,
         // equal FETCH_SIZE; profiles/r2s2/tile_ab)
-        const int cand[8][2] = {{16, 32}, {32, 16}, {8, 64}, {16, 16}, {8, 32}, {16, 8}, {8, 16}, {4, 32}};
+        const int cand[9][2] = {{16, 32}, {32, 16}, {8, 64}, {16, 16}, {8, 32}, {16, 8}, {8, 16}, {4, 32}, {32, 4}};
         const long units = wide ? (a->Cout + 191) / 192 : units_co;
-        static int wide_tile = -2;  // dev knob NPS_X3_WIDE_TILE=0/1/2: force 16x8 / 8x16 / 4x32 wide tiles
+        static int wide_tile = -2;  // dev knob NPS_X3_WIDE_TILE=0/1/2/3: force 16x8 / 8x16 / 4x32 / 32x4 wide tiles
         if (wide_tile == -2) {
             const char* e = getenv("NPS_X3_WIDE_TILE");
-            wide_tile = (e != nullptr && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : -1;
+            wide_tile = (e != nullptr && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : -1;
         }
         int best = -1;
         double best_eff = -1.0;
-        for (int i = wide ? 5 : 0; i < (wide ? 8 : 5); ++i) {
+        for (int i = wide ? 5 : 0; i < (wide ? (wide_tile == 3 ? 9 : 8) : 5); ++i) {
             if (wide && wide_tile >= 0 && i != 5 + wide_tile) continue;
             nps_conv2d_t t = *a;
             t.waves = 8;
@@ -800,7 +800,7 @@ extern "C" int nps_conv2d_fwd(const nps_conv2d_t* ap, void* stream) {
                   a.stride, a.dil);
     NPS_CHECK_ARG(a.precision == NPS_PREC_X3F16
                       ? ((a.TH * a.TW == 512 || a.TH * a.TW == 256) && (a.TW == 16 || a.TW == 32 || a.TW == 64)) ||
-                            (a.TH * a.TW == 128 && x3_wide_eligible(a) && (a.TW == 8 || a.TW == 16 || a.TW == 32))
+                            (a.TH * a.TW == 128 && x3_wide_eligible(a) && (a.TW == 4 || a.TW == 8 || a.TW == 16 || a.TW == 32))
                       : (a.waves == 8 ? (a.TH * a.TW == 256 || a.TH * a.TW == 128) && pc_eligible(a) &&
                                             (a.KH * a.KW != 1 || a.TH * a.TW == 128)
                                       : a.TH * a.TW == 64 * a.waves),
