@@ -115,9 +115,15 @@ __device__ __forceinline__ void x3_store_phase(const nps_conv2d_t& a, int b, int
             amax = fmaxf(amax, fabsf(v));
         }
         *reinterpret_cast<f32x4*>(a.out + o) = r;
-        if (st) {
+        if (st) {  // fp32 partials of the quad (as store_tile_s), one pair of fp64 adds per quad
+            float f1 = 0.f, f2 = 0.f;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) stats_add(a, r[e], ov[e], s1, s2);
+            for (int e = 0; e < 4; ++e) {
+                f1 += a.accumulate ? r[e] - ov[e] : r[e];
+                f2 += a.accumulate ? (r[e] - ov[e]) * (r[e] + ov[e]) : r[e] * r[e];
+            }
+            s1 += (double)f1;
+            s2 += (double)f2;
         }
     }
     stats_publish(a, b, s1, s2);  // the next GroupNorm(1)'s moments of this sample: one pair per wave
