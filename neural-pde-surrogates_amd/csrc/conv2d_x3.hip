@@ -801,6 +801,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     extern __shared__ __attribute__((aligned(16))) char wl[];  // [2][2 chunks][NCB][hi|lo][64][16 B]
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int b = blockIdx.y;
+#ifdef NPS_X3_STAMP  // dev diagnostic (tools/x1_stamps.py): per-work-group stamps of wave 0
+    const int l = blockIdx.y * gridDim.x + blockIdx.x;
+    const int wave = wv;
+    X3_STAMP(0);
+    X3_RSTAMP(4);
+#endif
     const int h = lane >> 5;
     const int npx = a.Hout * a.Wout;
     const int P = blockIdx.x * 128 + wv * 32 + (lane & 31);
@@ -887,6 +893,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     wstore(0);
     wfetch(min(1, last));
     __syncthreads();
+#ifdef NPS_X3_STAMP
+    X3_STAMP(1);
+#endif
     const int npad = (nstages + D - 1) / D * D;
     for (int s0 = 0; s0 < npad; s0 += D) {
         static_for<D>([&](auto jc) {
@@ -924,6 +933,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
             __syncthreads();
         });
     }
+#ifdef NPS_X3_STAMP
+    X3_STAMP(2);
+#endif
     const float inv = 1.f / (pow2_scale_for(a.wpack[packed_body(a.Cout, a.Cin, 1)]) * xs);
     const int oy = P / a.Wout, ox = P - (P / a.Wout) * a.Wout;
     const int dy = oy * a.out_os + a.out_off_y, dx = ox * a.out_os + a.out_off_x;
@@ -939,6 +951,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
             store_tile(a, b, cb * 32, h, v, dy, dx, amax);
         }
     }
+#ifdef NPS_X3_STAMP
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the stores have left this wave
+    X3_STAMP(3);
+    X3_RSTAMP(5);
+#endif
     nps::tag_publish(a.out_tag, amax, nps::wave_salt());
     if (a.out_stats != nullptr) {
         // moments of the stored values, recomputed from the accumulators (out_stats on a 1x1 conv:
