@@ -11,7 +11,8 @@ python bench.py [--gpus N --steps K --warmup W]
     timed live with HIP events on its stream during one extra model call after the timed region:
     achieved = sum(algorithmic fp32 conv flops) / sum(kernel durations) vs the kernel's fp32-equivalent
     ceiling, 2.5 PF/s dense f16 MFMA / 3 products (MI355X_MICROARCH.md); traffic = PMC HBM bytes per
-    launch from the committed profiles/pmc_traffic.json (tools/pmc_traffic.sh);
+    launch from the committed profiles/pmc_traffic.json (tools/pmc_traffic.sh; FETCH_SIZE scaled per access
+    shape as calibrated by tools/calib/pmc_calib.hip: x1 for the conv producers' 64-B reads);
   * cpu_baseline: the CPU oracle (oracle/, the reference restated in fp32 PyTorch-CPU) on a bounded
     sample (2 model calls at B=2) on rank 0 only, with the GPU-vs-CPU rel-L2 of that sample.
 """
