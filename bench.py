@@ -133,11 +133,19 @@ def _dtype():
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
 
-def attach_traffic(roof, headline):
+# the workload the committed PMC passes profiled (one process, the default command): the launches of a
+# rank carry these per-launch bytes only when the rank runs this exact per-GPU workload
+PMC_WORKLOAD = dict(model="ufno", res=256, num_c=3, per_gpu_batch=16, fno_modes=None)
+
+
+def attach_traffic(roof, workload):
     """roofline.traffic: HBM bytes per launch of the dominant kernel from the committed rocprofv3 --pmc
-    passes (tools/pmc_traffic.sh; FETCH_SIZE doubled per MI355X_MICROARCH.md § HBM, + WRITE_SIZE).
-    Those passes profile the headline workload only; other workloads report traffic null."""
-    if not headline:
+    passes (tools/pmc_traffic.sh: separate FETCH_SIZE and WRITE_SIZE passes; FETCH_SIZE x1 for the conv
+    producers' 64-B-per-line reads as calibrated by tools/calib/pmc_calib.hip, x2 for 16 B/lane sweeps;
+    see profiles/pmc_traffic.json's note).  Those passes profiled PMC_WORKLOAD; a rank running any other
+    per-GPU workload (another model / size, or a per-GPU batch of 16/N at N > 1) reports traffic null."""
+    if workload != PMC_WORKLOAD:
+        roof["traffic_note"] = "null: no PMC pass for this per-GPU workload " + json.dumps(workload)
         return roof
     try:
         with open(PMC_FILE) as f:
@@ -189,6 +197,32 @@ def max_over_ranks(elapsed, device):
     t = torch.tensor([elapsed], device="cpu" if on_cpu else device, dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return t.item()
+
+
+def per_rank_times(elapsed, device):
+    """Every rank's elapsed seconds (all-gather; [elapsed] in a single process)."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [elapsed]
+    on_cpu = dist.get_backend() == "gloo"
+    t = torch.tensor([elapsed], device="cpu" if on_cpu else device, dtype=torch.float64)
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [float(x.item()) for x in out]
+
+
+def dist_info(world):
+    """What the process group actually is (read back from torch.distributed, not from the arguments)."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        return dict(backend=str(dist.get_backend()), world_size=dist.get_world_size(), launcher_world=world,
+                    rehearsal=os.environ.get("NPS_BENCH_REHEARSAL") == "1")
+    return dict(backend=None, world_size=1, launcher_world=world, rehearsal=False)
+
+
+def timing_fields(elapsed, times, steps):
+    return dict(ms_per_step=round(elapsed / steps * 1e3, 3),
+                ms_per_step_per_rank=[round(t / steps * 1e3, 3) for t in times])
 
 
 def cpu_baseline(model, ocfg, opde, res, num_c, calls=2, B=2):
@@ -284,12 +318,14 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
-    elapsed = max_over_ranks(time.perf_counter() - t0, dev)
+    mine = time.perf_counter() - t0
+    elapsed = max_over_ranks(mine, dev)
+    times = per_rank_times(mine, dev)
     value = args.global_batch * tw * args.steps / elapsed
 
     if rank == 0:
-        headline = (args.model, args.res, args.num_c, args.global_batch, args.fno_modes) == ("ufno", 256, 3, 16, None)
-        roof = attach_traffic(conv_roofline(model, u_all[:, :, :tw], cond, pos, sc), headline)
+        workload = dict(model=args.model, res=args.res, num_c=args.num_c, per_gpu_batch=B, fno_modes=args.fno_modes)
+        roof = attach_traffic(conv_roofline(model, u_all[:, :, :tw], cond, pos, sc), workload)
         cpu = cpu_baseline(model, ocfg, opde, args.res, args.num_c, calls=args.cpu_calls) if (
             args.cpu_calls > 0 and world == 1) else None
         if cpu is not None and B >= 2:
@@ -310,8 +346,9 @@ def main():
             "metric": f"rollout timesteps/sec on {args.res}x{args.res} two-phase grid (sample-timesteps/s); "
                       "rel-L2 vs CPU reference",
             "value": round(value, 3), "unit": "sample-timesteps/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "warmup": args.warmup, **timing_fields(elapsed, times, args.steps), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": _dtype(), "data": "synthetic",
+            "dist": dist_info(world),
             "config": {"workload": f"{args.model.upper()} twophase cfg rollout (simulate), {args.res}x{args.res}, "
                                    f"{args.num_c} fields, obstacle mask, tw=25", "model": args.model,
                        "global_batch": args.global_batch, "per_gpu_batch": B, "res": args.res,
@@ -370,7 +407,9 @@ def run_fno3d(args):
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
-    elapsed = max_over_ranks(time.perf_counter() - t0, dev)
+    mine = time.perf_counter() - t0
+    elapsed = max_over_ranks(mine, dev)
+    times = per_rank_times(mine, dev)
     if rank == 0:
         # bytes one layer must move at least: input frame read by the pointwise conv and by the W-DFT, the
         # output written and re-read by the spectral accumulate, the per-mode weights once
@@ -384,9 +423,9 @@ def run_fno3d(args):
         print(json.dumps({
             "metric": "C5 FNO-3D processor throughput (sample-timesteps/s, 16 time-bundled steps per volume)",
             "value": round(gb * D * args.steps / elapsed, 3), "unit": "sample-timesteps/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
-            "scaling": "strong", "vs_baseline": None,
-            "dtype": "bf16 storage, fp32 arithmetic" if bf16 else "f32", "data": "synthetic",
+            "steps": args.steps, "warmup": args.warmup, **timing_fields(elapsed, times, args.steps),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+            "dtype": "bf16 storage, fp32 arithmetic" if bf16 else "f32", "data": "synthetic", "dist": dist_info(world),
             "config": {"workload": "FNO-3D (C5) over a 16x128x128 volume, 64 hidden + 4 cond, modes (8,12,12), "
                                    "4 blocks", "model": "fno3d", "global_batch": gb, "per_gpu_batch": B,
                        "parallelism": f"dp{world} (batch-sharded, no collective)"},
@@ -422,23 +461,19 @@ def cpu_baseline_train(model, args, B=1):
 
 def run_train(args):
     """Training throughput: trainers/base.py:472-507 steps of the pushforward train_step (unroll 0, the
-    epoch-0 case) on a fixed global batch sharded over the ranks; gradients all-reduced over RCCL
-    (trainers.distributed.GradAllReducer, overlapped with backward), Adam(lr=1e-4) as in the cfgs."""
+    epoch-0 case) on a fixed global batch sharded over the ranks; under a process group the trainer wires
+    data parallelism itself (parameter broadcast, global sqrt(MSE_sum) loss, summed RCCL gradient
+    all-reduce overlapped with backward: trainers/distributed.py), Adam(lr=1e-4) as in the cfgs."""
     import types
     from common.interfaces import D
     from trainers.autoregressivepushforwardtrainer import AutoregressivePushforwardTrainer
     from trainers.synthetic import twophase_batch
     world, rank, dev = init_ranks()
-    sync = None
     lo, hi = shard_bounds(args.global_batch, world, rank)
     B = hi - lo
     tw = 25
     model, _, _ = build_model(args.model, args.res, args.num_c, dev, fno_modes=args.fno_modes)
     model.train()
-    if world > 1:
-        from trainers.distributed import GradAllReducer
-        sync = GradAllReducer(model.parameters())
-        sync.broadcast_parameters(0)
     u, cond, pos, sc = twophase_batch(B, args.num_c, 2 * tw, args.res, args.res, seed=1234 + rank,
                                       obstacle="disc", device=dev)
     batch = (u[:, :, :1], u, pos, cond, torch.empty(B, 0, device=dev), sc)  # collated layout (B, 0)
@@ -447,8 +482,8 @@ def run_train(args):
     opt = torch.optim.Adam(model.parameters(), lr=1e-4)
     tr = AutoregressivePushforwardTrainer(model=model, data=types.SimpleNamespace(pde=model.pde,
                                                                                   data_interface=D.sim2d),
-                                          criterion=nn.MSELoss(reduction="sum"), optimizer=opt, config=cfg,
-                                          grad_sync=sync)
+                                          criterion=nn.MSELoss(reduction="sum"), optimizer=opt, config=cfg)
+    assert (tr.grad_sync is not None) == (world > 1)
     for _ in range(max(1, args.warmup)):
         tr.train_one_epoch([batch], epoch=0)
     torch.cuda.synchronize()
@@ -461,16 +496,18 @@ def run_train(args):
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
-    elapsed = max_over_ranks(time.perf_counter() - t0, dev)
+    mine = time.perf_counter() - t0
+    elapsed = max_over_ranks(mine, dev)
+    times = per_rank_times(mine, dev)
     if rank == 0:
         roof = probe_roofline(lambda: tr.train_one_epoch([batch], epoch=0))
         cpu = cpu_baseline_train(model, args) if (args.cpu_calls > 0 and world == 1) else None
         print(json.dumps({
             "metric": "pushforward training samples/sec (train_step + backward + all-reduce + Adam)",
             "value": round(args.global_batch * args.steps / elapsed, 3), "unit": "samples/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "steps": args.steps, "warmup": args.warmup, **timing_fields(elapsed, times, args.steps),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": _dtype(),
-            "data": "synthetic",
+            "data": "synthetic", "dist": dist_info(world),
             "config": {"workload": f"{args.model.upper()} twophase cfg train_step, {args.res}x{args.res}, "
                                    f"{args.num_c} fields, tw=25", "global_batch": args.global_batch,
                        "per_gpu_batch": B, "parallelism": f"dp{world} (RCCL gradient all-reduce)"},

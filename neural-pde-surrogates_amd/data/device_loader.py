@@ -40,15 +40,19 @@ class DeviceLoader:
       * single process: each epoch draws the iterator's base seed and then RandomSampler's seed from
         `generator` (torch's global RNG when None), exactly as DataLoader + RandomSampler do, and permutes
         with randperm on a generator seeded by the latter;
+        With an explicit `generator`, a fully iterated epoch also draws the trailing randperm RandomSampler
+        makes for its empty remainder slice (torch 2.10 sampler.py), so later epochs stay in step;
       * num_replicas > 1 (one process per GPU): the samples of `rank` under DistributedSampler semantics
          — a permutation seeded by `seed + epoch` (set_epoch), padded by wrapping (or cut
         with drop_last) to a multiple of num_replicas, rank r taking positions r, r + R, ...; the shards
         of one epoch are disjoint and cover the split once when its size divides by num_replicas.
+        pad=False (evaluation): no wrap-around duplicates — rank r takes positions r, r + R, ... < n, so
+        the shards differ in length by at most one sample and together are the split exactly once.
     prefetch: batches read / in flight ahead of the consumer."""
 
     def __init__(self, dataset, batch_size: int, shuffle: bool = False, drop_last: bool = False,
                  device="cuda", prefetch: int = 2, generator: Optional[torch.Generator] = None,
-                 num_replicas: int = 1, rank: int = 0, seed: int = 0):
+                 num_replicas: int = 1, rank: int = 0, seed: int = 0, pad: bool = True):
         self.base, self.indices = _base_and_indices(dataset)
         self.batch_size = int(batch_size)
         self.shuffle = shuffle
@@ -59,6 +63,7 @@ class DeviceLoader:
         if not (num_replicas >= 1 and 0 <= rank < num_replicas):
             raise ValueError(f"invalid rank {rank} of {num_replicas} replicas")
         self.num_replicas, self.rank, self.seed = int(num_replicas), int(rank), int(seed)
+        self.pad = bool(pad)
         self.epoch = 0
 
     def set_epoch(self, epoch: int):
@@ -69,6 +74,8 @@ class DeviceLoader:
         n, R = len(self.indices), self.num_replicas
         if R == 1:
             return n
+        if not self.pad:
+            return len(range(self.rank, n, R))
         # DistributedSampler: with drop_last the tail that does not fill every replica is cut
         return (n - R) // R + 1 if (self.drop_last and n % R != 0) else -(-n // R)
 
@@ -99,6 +106,8 @@ class DeviceLoader:
             order = torch.randperm(n, generator=g)
         else:
             order = torch.arange(n)
+        if not self.pad:
+            return order[self.rank:n:self.num_replicas]
         total = self._num_samples() * self.num_replicas
         if total > n:
             order = order.repeat(-(-total // n))  # wrap-around padding
@@ -109,6 +118,10 @@ class DeviceLoader:
         order = self.indices[self.shard_positions().numpy()]
         for i in range(len(self)):
             yield order[i * self.batch_size:(i + 1) * self.batch_size]
+        if self.num_replicas == 1 and self.shuffle and self.generator is not None:
+            # RandomSampler.__iter__'s trailing randperm (num_samples % n == 0 remainder slice), drawn
+            # when the epoch's iteration runs to its end
+            torch.randperm(len(self.indices), generator=self.generator)
 
     def __iter__(self):
         if self.device.type != "cuda":

@@ -82,7 +82,9 @@ class FNO(nn.Module):
             if h.dtype == torch.bfloat16:  # bf16 storage (C5); inference only
                 if use_autograd(self):
                     raise NotImplementedError("the bf16 3-D FNO path is inference-only (fp32 for training)")
-                tob = lambda t: ops.to_bf16(ops.nchw_to_nhwc(ops.to_f32(flat(t))))
+                # (an fp32 variables_broadcast next to bf16 h is converted as fp32)
+                tob = lambda t: ops.to_bf16(ops.nchw_to_nhwc(ops.to_f32(flat(t)) if t.dtype == torch.bfloat16
+                                                             else flat(t).float()))
                 vb = tob(variables_broadcast) if variables_broadcast is not None else None
                 y = ops.nhwc_to_nchw(ops.to_f32(self.run_bf16(tob(h), vb, D)))
                 return ops.to_bf16(y).reshape(B, y.shape[1], D, H, W)
@@ -336,7 +338,7 @@ class SpectralConv3d(nn.Module):
         ops.check_modes3d(D, H, W, self.modes1, self.modes2, self.modes3)
         x4 = x.reshape(B, C, D * H, W)
         if x.dtype == torch.bfloat16:  # bf16 storage (C5), inference only
-            xb = ops.to_bf16(ops.nchw_to_nhwc(ops.to_f32(x4)))
+            xb = ops.to_bf16(ops.nchw_to_nhwc(ops.to_f32(x4.contiguous())))
             y = ops.nhwc_to_nchw(ops.to_f32(self.run_bf16([ops.Src(xb)], D)))
             return ops.to_bf16(y).reshape(B, self.out_channels, D, H, W)
         if use_autograd(self):

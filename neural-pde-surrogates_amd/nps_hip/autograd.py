@@ -634,3 +634,27 @@ class SqrtMseSumFn(torch.autograd.Function):
 
 def sqrt_mse_sum(pred, labels):
     return SqrtMseSumFn.apply(pred, labels)
+
+
+class MseSumFn(torch.autograd.Function):
+    """nn.MSELoss(reduction='sum')(pred, labels) as an fp64 device scalar with a HIP backward — a rank's
+    part S_r of the global sum under data parallelism (trainers.distributed.global_sqrt_loss)."""
+
+    @staticmethod
+    def forward(ctx, pred, labels):
+        pred, labels = _c(pred), _c(labels)
+        ctx.save_for_backward(pred, labels)
+        return ops.sq_err_sum(pred, labels)     # fp64
+
+    @staticmethod
+    def backward(ctx, g):
+        pred, labels = ctx.saved_tensors
+        scale = (2.0 * g.double()).reshape(1)     # d S / d pred = 2 (pred - labels)
+        out = torch.empty_like(pred)
+        check(lib.nps_scaled_diff(ptr(pred), ptr(labels), ptr(scale), ptr(out), pred.numel(), stream_ptr()),
+              "scaled_diff")
+        return out, None
+
+
+def mse_sum(pred, labels):
+    return MseSumFn.apply(pred, labels)

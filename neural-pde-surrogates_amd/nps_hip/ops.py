@@ -64,11 +64,17 @@ class _TagArena:
         self.gen = 0
         self.next = 0
 
-    def alloc(self):
-        if self.next == _ARENA_TAGS:
+    def reserve(self, k: int):
+        """Start a new generation now unless k more tags fit in this one: a launch that needs several
+        tags reserves them all before it reads any tag pointer, so no wrap (which zeroes the buffer)
+        can happen between reading an input tag and launching the kernel that reads it."""
+        if self.next + k > _ARENA_TAGS:
             self.buf.zero_()        # stream-ordered after every kernel that used the old generation
             self.gen += 1
             self.next = 0
+
+    def alloc(self):
+        self.reserve(1)
         i = self.next
         self.next += 1
         return _Tag(self, self.gen, self.buf.data_ptr() + 4 * i * TAG_FLOATS)
@@ -95,16 +101,30 @@ def _arena(device) -> _TagArena:
     return ar
 
 
+def reserve_tags(device, k: int):
+    """Guarantee that the next k tag allocations on `device` do not wrap the arena (see _TagArena.reserve)."""
+    _arena(device).reserve(k)
+
+
 def tag_of(t: torch.Tensor):
-    """The live range tag of `t`, or None."""
-    tag = getattr(t, "_nps_tag", None)
-    return tag if (tag is not None and tag.live) else None
+    """The live range tag of `t`, or None.  A tag is recorded with the tensor's version counter: a torch
+    in-place write (add_, mul_, slice assignment) bumps t._version and so invalidates the bound; the HIP
+    kernels that write into an existing tensor raise its tag instead."""
+    rec = getattr(t, "_nps_tag", None)
+    if rec is None:
+        return None
+    tag, ver = rec
+    return tag if (tag.live and ver == t._version) else None
+
+
+def _attach_tag(t: torch.Tensor, tag):
+    t._nps_tag = (tag, t._version)
 
 
 def new_tag(t: torch.Tensor) -> int:
     """Attach a fresh (zero) tag to `t`, whose writer will raise it; returns its device pointer."""
     tag = _arena(t.device).alloc()
-    t._nps_tag = tag
+    _attach_tag(t, tag)
     return tag.ptr
 
 
@@ -125,7 +145,7 @@ def share_tag(dst: torch.Tensor, src: torch.Tensor) -> torch.Tensor:
     """dst holds a subset of src's values (and zeros): it may carry src's bound."""
     tag = tag_of(src)
     if tag is not None:
-        dst._nps_tag = tag
+        _attach_tag(dst, tag)
     return dst
 
 
@@ -385,6 +405,7 @@ def conv2d(srcs: Sequence[Src], frame_hw, wpack: torch.Tensor, bias: Optional[to
     a.addend1 = ptr(ads[1]) if len(ads) > 1 else None
     a.act, a.add_after_act = act, (1 if add_after_act else 0)
     a.precision = getattr(wpack, "nps_precision", PREC_F32)
+    reserve_tags(out.device, len(srcs) + 1)  # every tag this launch reads or writes, before any pointer
     if a.precision == PREC_X3F16:
         if in_scale is not None:  # explicit range (gradients): overrides the sources' tags
             a.in_scale = ptr(in_scale)
@@ -573,6 +594,8 @@ def _c_src_bf16(srcs: Sequence[Src]):
 
 def to_bf16(x: torch.Tensor) -> torch.Tensor:
     """bf16 copy (round-to-nearest-even) of an fp32 (or complex64, as its (re, im) pairs) device tensor."""
+    if x.dtype not in (torch.float32, torch.complex64):
+        raise TypeError(f"nps_hip to_bf16: expected float32 or complex64, got {x.dtype}")
     x = x.contiguous()
     xf = torch.view_as_real(x) if x.is_complex() else x
     out = torch.empty(xf.shape, dtype=torch.bfloat16, device=x.device)
@@ -581,6 +604,9 @@ def to_bf16(x: torch.Tensor) -> torch.Tensor:
 
 
 def to_f32(x: torch.Tensor) -> torch.Tensor:
+    """fp32 copy of a bf16 device tensor."""
+    if x.dtype != torch.bfloat16:
+        raise TypeError(f"nps_hip to_f32: expected bfloat16, got {x.dtype}")
     x = x.contiguous()
     out = torch.empty(x.shape, dtype=torch.float32, device=x.device)
     check(lib.nps_bf16_to_f32(ptr(x), x.numel(), ptr(out), stream_ptr()), "bf16_to_f32")

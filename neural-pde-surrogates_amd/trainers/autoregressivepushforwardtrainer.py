@@ -7,9 +7,11 @@ resident on the device (windows are views, no per-step host copies) and the
 MSE_sum criterion computed by a HIP fp64 reduction.  `train_step` /
 `train_one_epoch` are the pushforward training loop (:43-163,
 trainers/base.py:472-507) whose backward runs the HIP backward kernels
-(nps_hip.autograd); with a `grad_sync` (trainers.distributed.GradAllReducer)
-the gradients are all-reduced over RCCL between backward and optimizer step.
-Grid models only.
+(nps_hip.autograd).  Under a process group each rank draws the global batch's
+random steps, takes its slice, and backpropagates its share of the global
+sqrt(MSE_sum) (trainers.distributed.global_sqrt_loss); the summed RCCL
+all-reduce between backward and optimizer step then gives the 1-process
+gradient of the concatenated batch.  Grid models only.
 """
 import argparse
 import math
@@ -84,17 +86,34 @@ class AutoregressivePushforwardTrainer(TrainInterface):
 
     def _loss(self, pred, labels):
         c = self.criterion
-        if isinstance(c, nn.MSELoss) and c.reduction == "sum":
+        if isinstance(c, nn.MSELoss) and c.reduction == "sum" and pred.is_cuda:
             return ops.sq_err_sum(pred, labels)
         return c(pred, labels)
 
     def _train_loss(self, pred, labels):
         """torch.sqrt(criterion(pred, labels)) (:158-162); MSELoss(sum) runs as a HIP fp64 reduction with a
-        HIP backward."""
+        HIP backward.  Under a process group the loss is that of the global batch: S_r all-reduced before
+        backward, gradient ∇S_r / (2·sqrt(S)) (distributed.global_sqrt_loss)."""
         c = self.criterion
-        if isinstance(c, nn.MSELoss) and c.reduction == "sum":
+        mse = isinstance(c, nn.MSELoss) and c.reduction in ("sum", "mean")
+        if self.world > 1:
+            if not mse:
+                raise NotImplementedError("data-parallel training reproduces the global-batch loss for "
+                                          "nn.MSELoss(reduction='sum' | 'mean') criteria only")
+            from trainers.distributed import global_sqrt_loss
+            s_local = ad.mse_sum(pred, labels) if pred.is_cuda else torch.sum((pred - labels) ** 2)
+            return global_sqrt_loss(s_local, pred.numel() if c.reduction == "mean" else None)
+        if isinstance(c, nn.MSELoss) and c.reduction == "sum" and pred.is_cuda:
             return ad.sqrt_mse_sum(pred, labels)
         return torch.sqrt(c(pred, labels))
+
+    def _random_steps(self, steps, batch_size):
+        """random.choices(steps, k=batch_size) (:95); under a process group the draw is for the global
+        batch (every rank holds rank 0's Python RNG state) and this rank takes its slice."""
+        if self.world == 1:
+            return random.choices(steps, k=batch_size)
+        allsteps = random.choices(steps, k=batch_size * self.world)
+        return allsteps[self.rank * batch_size:(self.rank + 1) * batch_size]
 
     def train_step(self, batch: Tuple, epoch, batch_idx, loader=None):
         """Pushforward training step, autoregressivepushforwardtrainer.py:43-163 (grid models, static time):
@@ -116,7 +135,7 @@ class AutoregressivePushforwardTrainer(TrainInterface):
         unrolled_graphs = random.choice(list(range(max_unrolling + 1)))
         steps = [t for t in range(self.data_creator.tw,
                                   t_res - self.data_creator.tw - (self.data_creator.tw * unrolled_graphs) + 1)]
-        random_steps = random.choices(steps, k=batch_size)                             # :95
+        random_steps = self._random_steps(steps, batch_size)                           # :95
         data, labels = self.data_creator.create_data(u_super, random_steps)
         data, labels = data.to(device), labels.to(device)
         t_cond = self.data_creator.create_data(t_conditioning, random_steps, mode="labels") \

@@ -37,6 +37,26 @@ def _dist():
     return 1, 0
 
 
+class _UnpaddedShardSampler(torch.utils.data.Sampler):
+    """Evaluation shard of a CPU DataLoader under a process group: positions rank, rank + R, ... of a
+    per-epoch permutation (DistributedSampler's seed + epoch), without wrap-around duplicates."""
+
+    def __init__(self, n, num_replicas, rank, shuffle=True, seed=0):
+        self.n, self.R, self.rank, self.shuffle, self.seed, self.epoch = n, num_replicas, rank, shuffle, seed, 0
+
+    def set_epoch(self, epoch):
+        self.epoch = epoch
+
+    def __iter__(self):
+        g = torch.Generator()
+        g.manual_seed(self.seed + self.epoch)
+        order = torch.randperm(self.n, generator=g) if self.shuffle else torch.arange(self.n)
+        return iter(order[self.rank::self.R].tolist())
+
+    def __len__(self):
+        return len(range(self.rank, self.n, self.R))
+
+
 class TrainInterface:
     """Base trainer; subclasses define train_step / test_step / simulate and the supported interfaces."""
     model_interface: list = []
@@ -60,7 +80,14 @@ class TrainInterface:
         self.max_train_batches = max_train_batches
         self.max_test_batches = max_test_batches
         self.epoch_callback = epoch_callback
-        self.grad_sync = grad_sync
+        self.world, self.rank = _dist()
+        if self.world > 1 and grad_sync is None:
+            # data parallelism wired here, so an unchanged train.py under torchrun trains one model
+            from trainers.distributed import GradAllReducer, sync_python_random
+            grad_sync = GradAllReducer(self.model.parameters())
+            grad_sync.broadcast_parameters(0)
+            sync_python_random()
+        self.grad_sync = grad_sync if grad_sync is not False else None
         self.print_setting = getattr(self.config, "print_setting", dict(print_per_step=False))
         self.use_wandb = bool(use_wandb) and WANDB_AVAILABLE
         if use_wandb and not WANDB_AVAILABLE:
@@ -87,7 +114,9 @@ class TrainInterface:
 
     def get_dataloaders(self):
         """(train, valid, test) loaders (trainers/base.py:157-179, fixed-length time; batch_size, shuffle).
-        GPU device: data.DeviceLoader (rank-sharded under torch.distributed); CPU: torch DataLoader."""
+        GPU device: data.DeviceLoader; CPU: torch DataLoader.  Under torch.distributed `batch_size` is per
+        rank; the training split is sharded like DistributedSampler (padded so every rank takes the same
+        number of steps), the validation / test splits without padding (each sample counted once)."""
         if self.config.variable_time:
             raise NotImplementedError("variable-length time (sim1d_var_t) is not on the grid path")
         device = torch.device(self.config.device)
@@ -96,15 +125,15 @@ class TrainInterface:
         splits = (self.data.train, self.data.valid, self.data.test)
         if device.type == "cuda":
             from data.device_loader import DeviceLoader
-            return tuple(DeviceLoader(d, bs, shuffle=True, device=device, num_replicas=world, rank=rank)
-                         for d in splits)
+            return tuple(DeviceLoader(d, bs, shuffle=True, device=device, num_replicas=world, rank=rank,
+                                      pad=(i == 0)) for i, d in enumerate(splits))
         from torch.utils.data import DataLoader
         nw = getattr(self.config, "nw", 0)
         if world > 1:
             from torch.utils.data.distributed import DistributedSampler
-            return tuple(DataLoader(d, batch_size=bs, num_workers=nw,
-                                    sampler=DistributedSampler(d, num_replicas=world, rank=rank, shuffle=True))
-                         for d in splits)
+            samplers = [DistributedSampler(splits[0], num_replicas=world, rank=rank, shuffle=True)]
+            samplers += [_UnpaddedShardSampler(len(d), world, rank) for d in splits[1:]]
+            return tuple(DataLoader(d, batch_size=bs, num_workers=nw, sampler=sm) for d, sm in zip(splits, samplers))
         return tuple(DataLoader(d, batch_size=bs, shuffle=True, num_workers=nw, persistent_workers=nw > 0,
                                 pin_memory=True) for d in splits)
 
@@ -135,23 +164,33 @@ class TrainInterface:
             if obj is not None and hasattr(obj, "set_epoch"):
                 obj.set_epoch(epoch)
 
-    def _reduce_mean(self, value):
-        """Average a scalar (tensor or float) over the ranks; identity in a single process."""
+    def _reduce(self, value, mean: bool):
+        """Sum (or average) a scalar / tensor over the ranks in fp64; identity in a single process."""
         world, _ = _dist()
         if world == 1:
             return value
         import torch.distributed as dist
         dev = torch.device(self.config.device)
-        t = (value.detach().to(dev, torch.float64) if isinstance(value, torch.Tensor)
+        t = (value.detach().to(dev, torch.float64).clone() if isinstance(value, torch.Tensor)
              else torch.tensor(float(value), dtype=torch.float64, device=dev))
         dist.all_reduce(t)
-        t = t / world
+        if mean:
+            t = t / world
         return t.to(value.dtype) if isinstance(value, torch.Tensor) else t.item()
+
+    def _reduce_mean(self, value):
+        return self._reduce(value, True)
+
+    def _global_batch_size(self, batch) -> int:
+        """Samples of this step over all ranks (the padded training shards give every rank the same
+        batch sizes, step by step)."""
+        return util.get_batch_size(batch) * self.world
 
     def train_one_epoch(self, loader, epoch) -> torch.Tensor:
         """trainers/base.py:472-507: zero_grad -> train_step -> backward -> [RCCL all-reduce] -> step;
         returns the sum of per-sample batch losses divided by len(loader), as the reference does (also
-        when max_train_batches stops the epoch early)."""
+        when max_train_batches stops the epoch early).  Under a process group the loss is the global
+        batch's, divided by the global batch size — the value the 1-process run logs."""
         self.model.train()
         device = self.config.device
         self._set_epoch(loader, epoch)
@@ -164,7 +203,7 @@ class TrainInterface:
             if self.grad_sync is not None:
                 self.grad_sync.finish()
             self.optimizer.step()
-            total_loss += loss.detach() / util.get_batch_size(batch)
+            total_loss += loss.detach() / self._global_batch_size(batch)
             if batch_idx >= self.max_train_batches:
                 break
         total_loss = total_loss / len(loader)
@@ -177,7 +216,8 @@ class TrainInterface:
     def test(self, loader, use_train_loss_calc=False, include_data=False, test_kwargs=None):
         """trainers/base.py:378-470: batch-size-weighted mean of test_step's loss and metrics over the
         loader, without gradients.  Returns (loss, metrics) or, with include_data, also
-        (stack([gt, pred]), per-sample info)."""
+        (stack([gt, pred]), per-sample info) (this rank's samples).  Under a process group the weighted
+        sums and sample counts are summed over the ranks (unpadded shards: each sample once)."""
         test_kwargs = {} if test_kwargs is None else test_kwargs
         if getattr(loader, "batch_size", self.config.batch_size) != self.config.batch_size:
             print("Alert: batch_size in the supplied dataloader is not equal to that in the config.")
@@ -201,8 +241,19 @@ class TrainInterface:
                     other.extend(out[2][2])
                 if batch_idx >= self.max_test_batches - 1:
                     break
-        loss = self._reduce_mean(loss / n_total)
-        metrics = {k: self._reduce_mean(v / n_total) for k, v in metrics.items()}
+        if self.world > 1:
+            import torch.distributed as dist
+            keys = [sorted(metrics)]
+            allkeys = [None] * self.world
+            dist.all_gather_object(allkeys, keys[0])  # a rank with an empty shard has no metric keys
+            for k in sorted(set().union(*map(set, allkeys))):
+                if k not in metrics:
+                    metrics[k] = 0.0
+            n_total = self._reduce(n_total, False)
+            loss = self._reduce(loss, False)
+            metrics = {k: self._reduce(metrics[k], False) for k in sorted(metrics)}
+        loss = loss / n_total
+        metrics = {k: v / n_total for k, v in metrics.items()}
         if not include_data:
             return loss, metrics
         if self.data.data_interface == D.sim1d_var_t:

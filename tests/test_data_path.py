@@ -73,3 +73,41 @@ def test_create_data_host_matches_reference():
     dc = DataCreator(pde=None, neighbors=3, time_window=3, t_resolution=11, x_resolution=(8, 6))
     d, l = dc.create_data(g["train_u"], g["cd_steps"].tolist())
     assert torch.equal(d, g["cd_data"]) and torch.equal(l, g["cd_labels"])
+
+
+@pytest.mark.parametrize("batch_size", [3, 2, 7])
+def test_device_loader_order_matches_dataloader_over_epochs(root, batch_size):
+    """Sample order per epoch == torch DataLoader(shuffle=True, generator=g) over three epochs (the
+    RandomSampler's trailing randperm keeps the two generators in step), and with generator=None from the
+    same global RNG state."""
+    from data import PDE2DDataset, DeviceLoader
+    from torch.utils.data import DataLoader
+    ds = PDE2DDataset(base_path=root, **DATASET_KW)
+    key = lambda b: b[1].flatten(1).sum(1).tolist()  # noqa: E731  (one id per trajectory)
+    for explicit in (True, False):
+        g1 = torch.Generator().manual_seed(7) if explicit else None
+        g2 = torch.Generator().manual_seed(7) if explicit else None
+        ref = DataLoader(ds.train, batch_size=batch_size, shuffle=True, generator=g1)
+        ld = DeviceLoader(ds.train, batch_size=batch_size, shuffle=True, device="cpu", generator=g2)
+        for _ in range(3):
+            torch.manual_seed(11)
+            want = [key(b) for b in ref]
+            torch.manual_seed(11)
+            got = [key(b) for b in ld]
+            assert got == want
+
+
+def test_device_loader_unpadded_shards_cover_split_once(root):
+    """pad=False (evaluation loaders under a process group): rank shards are disjoint, differ in length by
+    at most one, and together hold every sample of the split exactly once (no wrap-around duplicates)."""
+    from data import PDE2DDataset, DeviceLoader
+    ds = PDE2DDataset(base_path=root, **DATASET_KW)
+    n = len(ds.train)
+    for R in (2, 3, 4):
+        ids = []
+        for r in range(R):
+            ld = DeviceLoader(ds.train, batch_size=2, shuffle=True, device="cpu", num_replicas=R, rank=r, pad=False)
+            pos = ld.shard_positions().tolist()
+            assert len(pos) == len(range(r, n, R)) and len(ld) == (len(pos) + 1) // 2
+            ids += pos
+        assert sorted(ids) == list(range(n))

@@ -1,7 +1,7 @@
 """CPU (gloo, world_size 2) tests of the data-parallel gradient all-reduce (trainers/distributed.py) and the
 batch sharding the rollout bench uses.  The same code runs over RCCL on the MI355X node."""
 import os
-import socket
+import tempfile
 
 import pytest
 import torch
@@ -9,12 +9,10 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+def _init_file():
+    """A fresh file:// rendezvous (no TCP port to race for with other processes or earlier cases)."""
+    d = tempfile.mkdtemp(prefix="nps_pg_")
+    return os.path.join(d, "init")
 
 
 class _Toy(torch.nn.Module):
@@ -36,9 +34,8 @@ class _Toy(torch.nn.Module):
         return (z.real ** 2 + z.imag).sum()
 
 
-def _worker(rank, world, port, bucket_bytes, overlap, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _worker(rank, world, init_file, bucket_bytes, overlap, q):
+    dist.init_process_group("gloo", init_method="file://" + init_file, rank=rank, world_size=world)
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [os.path.join(root, "neural-pde-surrogates_amd")]
@@ -61,15 +58,16 @@ def test_grad_allreduce_matches_full_batch(bucket_bytes, overlap):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, bucket_bytes, overlap, q)) for r in range(world)]
+    init_file = _init_file()
+    procs = [ctx.Process(target=_worker, args=(r, world, init_file, bucket_bytes, overlap, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    # reference: gradient of the mean of the two shard losses = average of per-shard gradients
+    # reference: gradient of the sum of the two shard losses = sum of per-shard gradients (GradAllReducer
+    # sums: each rank's loss is its share of the global loss, trainers/distributed.py)
     m = _Toy()
     x = torch.randn(8, 6, generator=torch.Generator().manual_seed(1))
     grads = []
@@ -78,7 +76,7 @@ def test_grad_allreduce_matches_full_batch(bucket_bytes, overlap):
         m(x[r * 4:(r + 1) * 4]).backward()
         grads.append({k: (p.grad.clone() if p.grad is not None else torch.zeros_like(p))
                       for k, p in m.named_parameters()})
-    want = {k: (grads[0][k] + grads[1][k]) / 2 for k in grads[0]}
+    want = {k: grads[0][k] + grads[1][k] for k in grads[0]}
     for rank, got, nb in res:
         if bucket_bytes == 64:
             assert nb > 1
@@ -113,9 +111,8 @@ class _ModelShaped(torch.nn.Module):
         return (y.abs() ** 2).sum() + (c ** 2).mean() + p.square().mean()
 
 
-def _model_worker(rank, world, port, q, done):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _model_worker(rank, world, init_file, q, done):
+    dist.init_process_group("gloo", init_method="file://" + init_file, rank=rank, world_size=world)
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root, os.path.join(root, "neural-pde-surrogates_amd"), os.path.join(root, "tests")]
@@ -123,7 +120,7 @@ def _model_worker(rank, world, port, q, done):
     import bench
     torch.set_num_threads(2)
     m = _ModelShaped()
-    sync = GradAllReducer(m.parameters(), bucket_bytes=16 * 1024 * 1024)
+    sync = GradAllReducer(m.parameters(), bucket_bytes=16 * 1024 * 1024, average=True)
     sync.broadcast_parameters(0)
     x = torch.randn(4, 196, 20, 20, generator=torch.Generator().manual_seed(1))
     lo, hi = bench.shard_bounds(4, world, rank)
@@ -151,7 +148,9 @@ def _model_worker(rank, world, port, q, done):
         dist.all_gather_object(allseen, seen)
         shards[epoch] = allseen
     elapsed = bench.max_over_ranks(1.0 + rank, torch.device("cpu"))
-    q.put((rank, grads, len(sync.buckets), (lo, hi), shards, elapsed))
+    times = bench.per_rank_times(1.0 + rank, torch.device("cpu"))
+    info = bench.dist_info(world)
+    q.put((rank, grads, len(sync.buckets), (lo, hi), shards, (elapsed, times, info)))
     done.wait(timeout=120)  # keep the tensors' shared memory alive until the parent has received them
     dist.destroy_process_group()
 
@@ -161,8 +160,8 @@ def test_model_shaped_allreduce_shards_and_bench_reduction():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     done = ctx.Event()
-    port = _free_port()
-    procs = [ctx.Process(target=_model_worker, args=(r, world, port, q, done)) for r in range(world)]
+    init_file = _init_file()
+    procs = [ctx.Process(target=_model_worker, args=(r, world, init_file, q, done)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=150) for _ in range(world)], key=lambda r: r[0])
@@ -175,10 +174,12 @@ def test_model_shaped_allreduce_shards_and_bench_reduction():
     m.zero_grad()
     (m(x[:2]) + m(x[2:])).div(2).backward()  # 1-process gradient of the mean of the two shard losses
     want = {k: p.grad for k, p in m.named_parameters()}
-    for rank, grads, nb, (lo, hi), shards, elapsed in res:
+    for rank, grads, nb, (lo, hi), shards, (elapsed, times, info) in res:
         assert nb >= 3  # 60 MB of complex weights + the rest in 16 MB buckets
         assert (lo, hi) == (2 * rank, 2 * rank + 2)
         assert elapsed == 2.0  # the slowest rank's time on every rank
+        assert times == [1.0, 2.0]  # every rank's own time, in rank order
+        assert info["backend"] == "gloo" and info["world_size"] == 2
         for k in want:
             torch.testing.assert_close(grads[k], want[k], rtol=1e-5, atol=1e-7)
     # every epoch: the ranks' shards are disjoint and cover the 10-sample split exactly once
@@ -191,3 +192,16 @@ def test_model_shaped_allreduce_shards_and_bench_reduction():
         ds_ids = allids if ds_ids is None else ds_ids
         assert allids == ds_ids
     assert shards[0][0] != shards[1][0]  # set_epoch reshuffles
+
+
+def test_bench_traffic_keyed_on_per_gpu_workload():
+    """bench.py attaches the committed PMC bytes per launch only to the per-GPU workload those passes
+    profiled; at N > 1 (per-GPU batch 16/N) or any other workload traffic is null, with the reason."""
+    import bench
+    roof = dict(kclass="x3f16_9tap", traffic=None)
+    got = bench.attach_traffic(dict(roof), dict(bench.PMC_WORKLOAD))
+    assert got["traffic"] is not None and got["traffic"] > 1e8
+    for n in (2, 4, 8):
+        w = dict(bench.PMC_WORKLOAD, per_gpu_batch=16 // n)
+        got = bench.attach_traffic(dict(roof), w)
+        assert got["traffic"] is None and "no PMC pass" in got["traffic_note"]

@@ -163,3 +163,44 @@ def test_fused_groupnorm_prologue_range(cout, xscale, gscale):
         ops.frame_pack = real_pack
     assert not packs, "GroupNorm prologue went through frame_pack"
     assert rel_l2(ops.nhwc_to_nchw(y).cpu(), ref) < TOL, (cout, xscale, gscale)
+
+
+def test_tag_arena_wrap_inside_a_conv_keeps_range():
+    """a conv reads its inputs' tag pointers and then allocates its output tag.  With one arena
+    slot left, the output allocation used to wrap the arena (zeroing every tag) after the input's tag
+    pointer was taken, so the split-fp16 conv ran unscaled and overflowed fp16 at 1e5.  conv2d now
+    reserves every tag it needs before reading any."""
+    from models.common import Conv2d
+    from nps_hip import ops
+    torch.manual_seed(0)
+    m = Conv2d(64, 64, 3)
+    x = torch.randn(2, 64, 20, 24) * 1.5e5
+    ref = _ref_conv(x, m.weight.detach(), m.bias.detach(), 1, 1, 0, "zeros")
+    md = m.to(DEV)
+    xd = ops.nchw_to_nhwc(x.to(DEV))
+    ar = ops._arena(xd.device)
+    xd._nps_tag = None                   # untagged input: the conv's input_tag allocates the last slot
+    ar.next = ops._ARENA_TAGS - 1
+    gen = ar.gen
+    y = md.run([ops.Src(xd)], (20, 24))
+    assert ar.gen == gen + 1             # the wrap happened, before the launch
+    out = ops.nhwc_to_nchw(y).cpu()
+    assert torch.isfinite(out).all()
+    assert rel_l2(out, ref) < TOL
+
+
+def test_tag_invalidated_by_torch_inplace_write():
+    """a range tag is recorded with the tensor's version; a torch in-place write drops it, so
+    the next split-fp16 conv re-measures the input (nps_absmax) instead of trusting a stale bound."""
+    from models.common import Conv2d
+    from nps_hip import ops
+    torch.manual_seed(0)
+    m = Conv2d(64, 64, 3).to(DEV)
+    xd = ops.nchw_to_nhwc(torch.randn(2, 64, 20, 24).to(DEV))
+    m.run([ops.Src(xd)], (20, 24))       # tags xd with max|x| ~ 4
+    assert ops.tag_of(xd) is not None
+    xd.mul_(1e5)                         # torch in-place: the bound is stale
+    assert ops.tag_of(xd) is None
+    y = m.run([ops.Src(xd)], (20, 24))
+    ref = _ref_conv(ops.nhwc_to_nchw(xd).cpu(), m.weight.detach().cpu(), m.bias.detach().cpu(), 1, 1, 0, "zeros")
+    assert rel_l2(ops.nhwc_to_nchw(y).cpu(), ref) < TOL
