@@ -69,7 +69,7 @@ def build_model(kind, res, num_c, device, fno_modes=None, seed=42):
 # dense MFMA peaks, MI355X_MICROARCH.md: f32 (v_mfma_f32_32x32x2_f32) 157.3 TF; f16 2.5 PF.  A split-fp16
 # conv spends 3 f16 MFMA products per algorithmic fp32 product, so its fp32-equivalent ceiling is 2.5 PF / 3.
 PEAK_TFLOPS = {"f32": FP32_MFMA_PEAK_TFLOPS, "x3f16": 2500.0 / 3.0, "f32w": FP32_MFMA_PEAK_TFLOPS,
-               "x3w": 2500.0 / 3.0}
+               "x3w": 2500.0 / 3.0, "bf16_3d": 2500.0, "f32_3d": FP32_MFMA_PEAK_TFLOPS}
 KERNEL_NAMES = {("x3f16", 9): "conv2d_x3_kernel<9,*> (3x3, split-fp16 MFMA)",
                 ("x3f16", 4): "conv2d_x3_kernel<4,*> (2x2 phase / space-to-depth, split-fp16 MFMA)",
                 ("x3f16", 1): "conv2d_x3_kernel<1,*> (1x1, split-fp16 MFMA)",
@@ -80,7 +80,11 @@ KERNEL_NAMES = {("x3f16", 9): "conv2d_x3_kernel<9,*> (3x3, split-fp16 MFMA)",
                 ("f32w", 1): "wgrad_kernel (1x1 weight gradient, f32 MFMA)",
                 ("x3w", 9): "wgrad_x3_kernel<3,3> (3x3 weight gradient, split-fp16 MFMA)",
                 ("x3w", 4): "wgrad_x3_kernel<2,2> (2x2 weight gradient, split-fp16 MFMA)",
-                ("x3w", 1): "wgrad_x3_kernel<1,1> (1x1 weight gradient, split-fp16 MFMA)"}
+                ("x3w", 1): "wgrad_x3_kernel<1,1> (1x1 weight gradient, split-fp16 MFMA)",
+                ("bf16_3d", 27): "conv3d_kernel<bf16,3,*> (3x3x3, bf16 MFMA)",
+                ("bf16_3d", 8): "conv3d_kernel<bf16,2,1,8> (ConvTranspose3d phases, bf16 MFMA)",
+                ("bf16_3d", 1): "conv3d_kernel<bf16,1,1,8> (1x1x1, bf16 MFMA)",
+                ("f32_3d", 27): "conv3d_kernel<f32,3,*> (3x3x3, f32 MFMA)"}
 
 
 def conv_roofline(model, x, cond, pos, sc):
@@ -258,8 +262,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--model", default="ufno", choices=list(CFGS) + ["fno3d"],
-                    help="fno3d = BASELINE config C5 (3-D FNO over a 16x128x128 time-bundled volume)")
+    ap.add_argument("--model", default="ufno", choices=list(CFGS) + ["fno3d", "ufno3d"],
+                    help="ufno3d = BASELINE config C5 (3-D U-FNO over a 16x128x128 time-bundled volume); fno3d = "
+                         "its FNO-3D processor alone")
     ap.add_argument("--res", type=int, default=256)
     ap.add_argument("--num-c", type=int, default=3)
     ap.add_argument("--global-batch", type=int, default=16)
@@ -273,7 +278,7 @@ def main():
     args = ap.parse_args()
     if args.mode == "train":
         return run_train(args)
-    if args.model == "fno3d":
+    if args.model in ("fno3d", "ufno3d"):
         return run_fno3d(args)
 
     world, rank, dev = init_ranks()
@@ -367,19 +372,27 @@ def main():
 C5_CFG = dict(num_spatial_dims=3, n_cond=4, hidden_features=64, fno_modes=(8, 12, 12), hidden_blocks=4,
               cond_mode="concat", fno_kernel_size=1)
 C5_VOL = (16, 128, 128)
+# the 3-D U-FNO of C5: the same FNO-3D layers plus, per block, a 3-D U-Net as the twophase U-FNO cfg builds it
+# (ch_mults [1, 1], n_blocks 1, GroupNorm, 1x1 final, circular; cfg_twophase_ufno.py) — its Upsample is this
+# build's 3-D definition (DESIGN.md "3-D U-FNO")
+C5_UFNO_CFG = dict(C5_CFG, ch_mults=[1, 1], is_attn=[False, False], mid_attn=False, norm=True, n_blocks=1,
+                   use1x1=True, padding_mode="circular")
 
 
 def run_fno3d(args):
-    """C5 throughput: one step = one FNO-3D processor forward over the batch (16 bundled timesteps per
-    sample), fp32 or bf16 storage; batch-sharded over the ranks like the rollout."""
+    """C5 throughput: one step = one 3-D processor forward over the batch (16 bundled timesteps per
+    sample) — the U-FNO 3D (--model ufno3d: FNO-3D layers + 3-D U-Nets) or the FNO-3D alone (fno3d) —
+    fp32 or bf16 storage; batch-sharded over the ranks like the rollout."""
     from models.enc_proc_dec_components.proc_fno import FNO
+    from models.enc_proc_dec_components.proc_ufno import UFNO
     from nps_hip import ops
     world, rank, dev = init_ranks()
     gb = args.global_batch if args.global_batch != 16 else 8  # C5: global batch 8 (one volume per GPU at 8)
     lo, hi = shard_bounds(gb, world, rank)
     B = hi - lo
     torch.manual_seed(42)
-    m = FNO(pde=None, **C5_CFG).to(dev).eval()
+    ufno = args.model == "ufno3d"
+    m = (UFNO(pde=None, **C5_UFNO_CFG) if ufno else FNO(pde=None, **C5_CFG)).to(dev).eval()
     D, H, W = C5_VOL
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     h = torch.rand(B, C5_CFG["hidden_features"], D * H, W, device=dev, generator=g) * 2 - 1
@@ -389,9 +402,14 @@ def run_fno3d(args):
     hn, vn = ops.nchw_to_nhwc(h), ops.nchw_to_nhwc(vb)
     if bf16:
         hn, vn = ops.to_bf16(hn), ops.to_bf16(vn)
+    if ufno:  # NDHWC volumes
+        hn = hn.view(B, D, H, W, hn.shape[3])
+        vn = vn.view(B, D, H, W, vn.shape[3])
 
     def step():
         with torch.no_grad():
+            if ufno:
+                return m.run3d(hn, vn)
             return m.run_bf16(hn, vn, D) if bf16 else m.run(hn, vn, D)
 
     for _ in range(max(1, args.warmup)):
@@ -410,6 +428,8 @@ def run_fno3d(args):
     mine = time.perf_counter() - t0
     elapsed = max_over_ranks(mine, dev)
     times = per_rank_times(mine, dev)
+    if rank == 0 and ufno:
+        return print_ufno3d_line(args, m, step, hn, vn, gb, B, world, elapsed, times, bf16)
     if rank == 0:
         # bytes one layer must move at least: input frame read by the pointwise conv and by the W-DFT, the
         # output written and re-read by the spectral accumulate, the per-mode weights once
@@ -434,6 +454,56 @@ def run_fno3d(args):
             "out_abs_mean": float(y.float().abs().mean())}), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
+
+
+def print_ufno3d_line(args, m, step, hn, vn, gb, B, world, elapsed, times, bf16):
+    """The C5 U-FNO 3D line: throughput, the conv3d roofline (HIP events on every conv launch of one step)
+    and the CPU oracle on a bounded sample (one of the 4 blocks, B=1, fp32 PyTorch-CPU restatement, scaled
+    to the 4-block call) with the GPU-vs-oracle rel-L2 of that block."""
+    import oracle  # noqa: F401  (CPU baseline only, outside the timed region)
+    from oracle import functional as Fo
+    from models.common import to_ncdhw
+    from nps_hip import ops
+    D = C5_VOL[0]
+    roof = probe_roofline(step)
+    cpu = None
+    if args.cpu_calls > 0 and world == 1:
+        threads = int(os.environ.get("OMP_NUM_THREADS", len(os.sched_getaffinity(0))))
+        torch.set_num_threads(threads)
+        sd = {k: v.detach().cpu() for k, v in m.state_dict().items() if k.split(".")[1] == "0"}
+        h1 = to_ncdhw(ops.to_f32(hn[:1]) if bf16 else hn[:1]).cpu()
+        v1 = to_ncdhw(ops.to_f32(vn[:1]) if bf16 else vn[:1]).cpu()
+        cfg1 = dict(C5_UFNO_CFG, hidden_blocks=1)
+        t0 = time.perf_counter()
+        with torch.no_grad():
+            ref = Fo.ufno3d(sd, "", cfg1, h1, v1)
+        dt = time.perf_counter() - t0
+        nblk = C5_UFNO_CFG["hidden_blocks"]
+        with torch.no_grad():  # the GPU's first block on the same volume
+            fl, ul = m.fno_layers, m.unet_layers
+            m.fno_layers, m.unet_layers = fl[:1], ul[:1]
+            try:
+                y1 = m.run3d(hn[:1], vn[:1])
+            finally:
+                m.fno_layers, m.unet_layers = fl, ul
+        y1 = to_ncdhw(ops.to_f32(y1) if bf16 else y1).cpu().double()
+        err = (torch.linalg.vector_norm(y1 - ref.double()) / torch.linalg.vector_norm(ref.double())).item()
+        cpu = dict(value=round(D / (nblk * dt), 4), unit="sample-timesteps/s", cores=threads, kind="port",
+                   sample=f"oracle (fp32 PyTorch-CPU restatement) U-FNO 3D block 1 of {nblk}, B=1, "
+                          f"{'x'.join(map(str, C5_VOL))}: {dt:.1f} s, scaled x{nblk} to the whole processor call",
+                   rel_l2_gpu_vs_cpu_block1=err)
+    ms = elapsed / args.steps * 1e3
+    print(json.dumps({
+        "metric": "C5 U-FNO 3D processor throughput (sample-timesteps/s, 16 time-bundled steps per volume)",
+        "value": round(gb * D * args.steps / elapsed, 3), "unit": "sample-timesteps/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, **timing_fields(elapsed, times, args.steps),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+        "dtype": "bf16 storage, bf16 MFMA / fp32 accumulate" if bf16 else "f32", "data": "synthetic",
+        "dist": dist_info(world),
+        "config": {"workload": "U-FNO 3D (C5) over a 16x128x128 volume, 64 hidden + 4 cond, modes (8,12,12), "
+                               "4 blocks, 3-D U-Nets ch_mults [1,1]", "model": "ufno3d", "global_batch": gb,
+                   "per_gpu_batch": B, "parallelism": f"dp{world} (batch-sharded, no collective)"},
+        "roofline": roof, "cpu_baseline": cpu}), flush=True)
 
 
 def cpu_baseline_train(model, args, B=1):

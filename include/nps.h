@@ -361,6 +361,59 @@ int nps_volume_rescale_bwd(const float* g, const double* new_tot, const double* 
                            const float* mask, int mask_S, int mask_ch, const double* D, float* gu, int B, int num_c,
                            int tw, int H, int W, void* stream);
 
+/* ---- 3-D U-Net of the 3-D U-FNO (BASELINE config C5: U-FNO 3D over a time-bundled D x H x W volume) ----
+ * The reference builds the 3-D U-Net's ResidualBlock / Down / Middle / Downsample from nn.Conv3d and
+ * nn.GroupNorm (proc_unet_modern.py:199-455 with num_spatial_dims=3) but has no 3-D Upsample
+ * (models/common.py:103-120 raises); this build defines it per axis as the 2-D rule: circular pad 1,
+ * then ConvTranspose3d(k=4, s=2, p=0) (DESIGN.md "3-D U-FNO").  Activations are NDHWC; storage and MFMA
+ * arithmetic are bf16 (v_mfma_f32_32x32x16_bf16, fp32 accumulate) or exact fp32 (v_mfma_f32_32x32x2_f32). */
+typedef struct {
+    const void* ptr;            /* [B][D][H][W][C] NDHWC, element type per nps_conv3d_t.bf16 */
+    int C, D, H, W;
+    int off_d, off_h, off_w;    /* placement in the core frame (crop_Nd: < 0 crops, > 0 zero-pads) */
+} nps_src3_t;
+
+typedef struct {
+    int nsrc;
+    nps_src3_t src[NPS_MAX_SRC];
+    int B, Dc, Hc, Wc, Cin;     /* core frame (the virtual concatenation); Cin = sum of src[i].C */
+    /* frame extension, per side of every spatial axis: circular by `circ` (circular_pad), then `zpad`
+     * zeros; the conv is valid over the extended frame */
+    int circ, zpad;
+    /* prologue on core-frame values (sources' zeros included): x' = act(GN(x)) */
+    const double* gn_stats;     /* [B][G][2] (sum, sum of squares) from nps_gn_stats3d, or NULL */
+    const float* gn_gamma;      /* [Cin] */
+    const float* gn_beta;
+    int gn_groups;
+    float gn_eps;
+    int pre_act;                /* 0 none, 1 GELU(erf) */
+    int K, stride;              /* K^3 taps; K in {1, 2, 3}, stride 1 or 2 (K = 3) */
+    int transposed;             /* 1: a k4/s2 ConvTranspose3d as 8 phase convs with K = 2, stride 1 */
+    int Dout, Hout, Wout;       /* conv output positions (per phase) */
+    const void* wpack;          /* nps_conv3d_pack_weights layout */
+    const float* bias;          /* [Cout] or NULL */
+    int Cout;
+    /* epilogue: destination index per axis = m*out_os + out_off (+ the phase bit when transposed);
+     * positions outside [0, out_D) x [0, out_H) x [0, out_W) are skipped (crop) */
+    void* out;
+    int out_C, out_D, out_H, out_W, out_os, out_off_d, out_off_h, out_off_w;
+    int accumulate;             /* out += result (crop_Nd(h) + shortcut, proc_unet_modern.py:250) */
+    const void* addend;         /* indexed like out, or NULL (proc_ufno.py:118 h_fno + h_unet) */
+    int act;                    /* 0 none, 1 GELU, after bias + addend */
+    int bf16;                   /* 1: bf16 storage / bf16 MFMA; 0: fp32 storage / exact fp32 MFMA */
+} nps_conv3d_t;
+
+/* Conv3d weight (Cout, Cin, K, K, K) or, transposed != 0, ConvTranspose3d weight (Cin, Cout, 4, 4, 4) ->
+ * the kernel's packing ([phase][64-channel Cout tile][kd][16-channel Cin chunk][kh][kw][64][16], zero
+ * padded), fp32 or bf16 elements.  nps_conv3d_packed_bytes gives the buffer size. */
+size_t nps_conv3d_packed_bytes(int Cout, int Cin, int K, int transposed, int bf16);
+int nps_conv3d_pack_weights(const float* w, void* wpack, int Cout, int Cin, int K, int transposed, int bf16,
+                            void* stream);
+int nps_conv3d_fwd(const nps_conv3d_t* a, void* stream);
+/* GroupNorm moments of a core frame (a's sources and B, Dc, Hc, Wc, Cin, bf16): ADDS per (b, group) the
+ * fp64 (sum, sum of squares) of the frame's values (uncovered positions count as 0) to stats[B][G][2] */
+int nps_gn_stats3d(const nps_conv3d_t* a, int G, double* stats, void* stream);
+
 const char* nps_last_error(void);
 const char* nps_version(void);
 

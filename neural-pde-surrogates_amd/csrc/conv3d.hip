@@ -1,0 +1,542 @@
+// 3-D U-Net convolutions of the 3-D U-FNO (BASELINE config C5): every Conv3d / ConvTranspose3d of
+// UNetModern(num_spatial_dims=3) (proc_unet_modern.py:199-455; the 3-D Upsample is this build's definition,
+// include/nps.h) as one implicit-GEMM kernel on NDHWC activations, bf16 storage on v_mfma_f32_32x32x16_bf16
+// or fp32 storage on the exact-fp32 v_mfma_f32_32x32x2_f32, with the GroupNorm+GELU prologue, torch.cat /
+// crop_Nd as a virtual frame of up to 3 sources, circular / zero frame extension, and the bias / addend /
+// GELU / accumulate-at-offset epilogue.
+//
+// GEMM: out[co][voxel] = sum over (kd, ci, kh, kw) of W[co][ci][kd][kh][kw] * frame[voxel*S + (kd, kh, kw)][ci].
+// Work-group = 256 threads (4 waves): 64 output channels x (TH rows x 32 columns) of one output depth slice;
+// wave w owns the 64 channels x rows [w*TH/4, +TH/4) (2 x TH/4 32x32 accumulators).  K loop in stages of
+// (kd, 16-channel chunk): the stage's input patch ((TH-1)S+K rows x 31S+K columns x 16 channels, the
+// prologue applied while staging) and its K*K x 64 x 16 weights go through a double-buffered LDS ring,
+// loaded into registers one stage ahead so the global loads overlap the MFMAs of the current stage.
+// LDS images are [pixel | channel row][16] with the two 8-channel halves XOR-swizzled by bit 3 of the row,
+// so the ds_read_b128 B / A fragment reads of 32 consecutive rows are bank-conflict free.
+#include "nps_common.hpp"
+
+namespace {
+
+typedef unsigned short bf16_t;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float bf2f(unsigned v) { return __uint_as_float(v << 16); }
+__device__ __forceinline__ unsigned f2bf(float v) { return (unsigned)__builtin_bit_cast(bf16_t, (__bf16)v); }
+
+// 8 consecutive channels of one voxel, raw storage bits
+template <typename T> struct Vec8;
+template <> struct Vec8<bf16_t> {
+    u32x4 a;
+    __device__ __forceinline__ void zero() { a = u32x4{0u, 0u, 0u, 0u}; }
+    __device__ __forceinline__ float get(int e) const {
+        const unsigned w = a[e >> 1];
+        return bf2f((e & 1) ? (w >> 16) : (w & 0xffffu));
+    }
+    __device__ __forceinline__ void set(int e, float x) {
+        const unsigned h = f2bf(x);
+        const unsigned w = a[e >> 1];
+        a[e >> 1] = (e & 1) ? ((w & 0xffffu) | (h << 16)) : ((w & 0xffff0000u) | h);
+    }
+    __device__ __forceinline__ void load(const bf16_t* p) { a = *reinterpret_cast<const u32x4*>(p); }
+    __device__ __forceinline__ void load_elem(int e, const bf16_t* p) {
+        const unsigned h = *p, w = a[e >> 1];
+        a[e >> 1] = (e & 1) ? ((w & 0xffffu) | (h << 16)) : ((w & 0xffff0000u) | h);
+    }
+    __device__ __forceinline__ void store(bf16_t* p) const { *reinterpret_cast<u32x4*>(p) = a; }
+};
+template <> struct Vec8<float> {
+    u32x4 a, b;
+    __device__ __forceinline__ void zero() { a = b = u32x4{0u, 0u, 0u, 0u}; }
+    __device__ __forceinline__ float get(int e) const { return __uint_as_float(e < 4 ? a[e] : b[e - 4]); }
+    __device__ __forceinline__ void set(int e, float x) {
+        if (e < 4) a[e] = __float_as_uint(x); else b[e - 4] = __float_as_uint(x);
+    }
+    __device__ __forceinline__ void load(const float* p) {
+        a = reinterpret_cast<const u32x4*>(p)[0];
+        b = reinterpret_cast<const u32x4*>(p)[1];
+    }
+    __device__ __forceinline__ void load_elem(int e, const float* p) { set(e, *p); }
+    __device__ __forceinline__ void store(float* p) const {
+        reinterpret_cast<u32x4*>(p)[0] = a;
+        reinterpret_cast<u32x4*>(p)[1] = b;
+    }
+};
+
+template <typename T> __device__ __forceinline__ float ld1(const T* p);
+template <> __device__ __forceinline__ float ld1<bf16_t>(const bf16_t* p) { return bf2f(*p); }
+template <> __device__ __forceinline__ float ld1<float>(const float* p) { return *p; }
+template <typename T> __device__ __forceinline__ void st1(T* p, float v);
+template <> __device__ __forceinline__ void st1<bf16_t>(bf16_t* p, float v) { *p = (bf16_t)f2bf(v); }
+template <> __device__ __forceinline__ void st1<float>(float* p, float v) { *p = v; }
+
+// extended-frame index -> core-frame index, -1 in the zero padding
+__device__ __forceinline__ int ext_to_core(int f, int n, int circ, int zpad) {
+    const int g = f - zpad;
+    if (g < 0 || g >= n + 2 * circ) return -1;
+    return circ ? nps::wrap_mod(g - circ, n) : g;
+}
+
+// channels [c0, c0+8) of core voxel (cd, ch, cw): each source fills the channels it holds where it covers
+// the voxel; everything else reads 0
+template <typename T>
+__device__ __forceinline__ void load_piece(Vec8<T>& r, const nps_conv3d_t& a, int b, int cd, int ch, int cw, int c0) {
+    r.zero();
+    int lo = 0;
+#pragma unroll
+    for (int si = 0; si < NPS_MAX_SRC; ++si) {
+        if (si < a.nsrc) {
+            const nps_src3_t& s = a.src[si];
+            if (c0 + 8 > lo && c0 < lo + s.C) {
+                const int dd = cd - s.off_d, hh = ch - s.off_h, ww = cw - s.off_w;
+                if (dd >= 0 && dd < s.D && hh >= 0 && hh < s.H && ww >= 0 && ww < s.W) {
+                    const T* p = reinterpret_cast<const T*>(s.ptr) +
+                                 ((((size_t)b * s.D + dd) * s.H + hh) * s.W + ww) * s.C;
+                    if (c0 >= lo && c0 + 8 <= lo + s.C && (s.C & 7) == 0 && ((c0 - lo) & 7) == 0) {
+                        r.load(p + (c0 - lo));
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) {
+                            const int c = c0 + e;
+                            if (c >= lo && c < lo + s.C) r.load_elem(e, p + (c - lo));
+                        }
+                    }
+                }
+            }
+            lo += s.C;
+        }
+    }
+}
+
+template <int K, int S, int TH>
+struct Geo {
+    static constexpr int TW = 32;
+    static constexpr int PR = (TH - 1) * S + K;
+    static constexpr int PC = (TW - 1) * S + K;
+    static constexpr int NPIX = PR * PC;
+    static constexpr int NPP = NPIX * 2;           // 8-channel pieces of a stage's patch
+    static constexpr int NWP = K * K * 64 * 2;     // 8-channel pieces of a stage's weights
+    static constexpr int PPT = (NPP + 255) / 256;  // per thread
+    static constexpr int WPT = (NWP + 255) / 256;
+    static constexpr int PATCH = NPIX * 16;        // elements
+    static constexpr int WTS = K * K * 64 * 16;
+    static constexpr int BUF = PATCH + WTS;
+    static constexpr int RW = TH / 4;              // rows (32-voxel blocks) per wave
+};
+
+__device__ __forceinline__ int swz(int row) { return (row >> 3) & 1; }
+
+template <typename T, int K, int S, int TH>
+__global__ __launch_bounds__(256) void conv3d_kernel(const nps_conv3d_t a, int nchunk, int ntile) {
+    using G = Geo<K, S, TH>;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    T* ring = reinterpret_cast<T*>(smem);
+    float* gscale = reinterpret_cast<float*>(smem + 2 * G::BUF * sizeof(T));  // [nchunk*16] GN affine per channel
+    float* gshift = gscale + nchunk * 16;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int ntw = (a.Wout + 31) / 32, nth = (a.Hout + TH - 1) / TH;
+    int t = blockIdx.x;
+    const int tw = t % ntw; t /= ntw;
+    const int th = t % nth; t /= nth;
+    const int md = t % a.Dout;
+    const int b = t / a.Dout;
+    const int tile = blockIdx.y, z = blockIdx.z;
+    const int h0 = th * TH, w0 = tw * 32;
+    const int Dext = a.Dc + 2 * (a.circ + a.zpad), Hext = a.Hc + 2 * (a.circ + a.zpad),
+              Wext = a.Wc + 2 * (a.circ + a.zpad);
+    (void)Dext;
+    const bool pro = a.gn_stats != nullptr || a.pre_act != 0;
+
+    if (pro) {  // x' = x * scale[c] + shift[c] (GroupNorm affine of this sample), then the activation
+        for (int c = tid; c < nchunk * 16; c += 256) {
+            float sc = 1.f, sh = 0.f;
+            if (a.gn_stats != nullptr && c < a.Cin) {
+                const int g = c / (a.Cin / a.gn_groups);
+                const double n = (double)a.Dc * a.Hc * a.Wc * (a.Cin / a.gn_groups);
+                const double mean = a.gn_stats[(b * a.gn_groups + g) * 2] / n;
+                const double var = fmax(a.gn_stats[(b * a.gn_groups + g) * 2 + 1] / n - mean * mean, 0.0);
+                const float rstd = (float)(1.0 / sqrt(var + (double)a.gn_eps));
+                sc = a.gn_gamma[c] * rstd;
+                sh = a.gn_beta[c] - (float)mean * sc;
+            }
+            gscale[c] = sc;
+            gshift[c] = sh;
+        }
+        __syncthreads();
+    }
+
+    const T* wbase = reinterpret_cast<const T*>(a.wpack) + (size_t)(z * ntile + tile) * K * nchunk * G::WTS;
+    const int nstage = K * nchunk;
+
+    Vec8<T> pr[G::PPT], wr[G::WPT];
+    auto fetch = [&](int st) {
+        const int kd = st / nchunk, chunk = st - kd * nchunk;
+        const int fd = md * S + kd;
+        const int cd = ext_to_core(fd, a.Dc, a.circ, a.zpad);
+#pragma unroll
+        for (int i = 0; i < G::PPT; ++i) {
+            const int idx = tid + 256 * i;
+            pr[i].zero();
+            if (idx < G::NPP) {
+                const int pix = idx >> 1, half = idx & 1;
+                const int prr = pix / G::PC, pcc = pix - prr * G::PC;
+                const int fh = h0 * S + prr, fw = w0 * S + pcc;
+                const int ch = fh < Hext ? ext_to_core(fh, a.Hc, a.circ, a.zpad) : -1;
+                const int cw = fw < Wext ? ext_to_core(fw, a.Wc, a.circ, a.zpad) : -1;
+                if (cd >= 0 && ch >= 0 && cw >= 0) load_piece<T>(pr[i], a, b, cd, ch, cw, chunk * 16 + half * 8);
+            }
+        }
+        const T* wsrc = wbase + (size_t)st * G::WTS;
+#pragma unroll
+        for (int i = 0; i < G::WPT; ++i) {
+            const int idx = tid + 256 * i;
+            if (idx < G::NWP) wr[i].load(wsrc + idx * 8);
+        }
+    };
+    auto commit = [&](int st, int buf) {
+        const int kd = st / nchunk, chunk = st - kd * nchunk;
+        const int cd = ext_to_core(md * S + kd, a.Dc, a.circ, a.zpad);
+        T* P = ring + buf * G::BUF;
+#pragma unroll
+        for (int i = 0; i < G::PPT; ++i) {
+            const int idx = tid + 256 * i;
+            if (idx < G::NPP) {
+                const int pix = idx >> 1, half = idx & 1;
+                if (pro) {
+                    const int prr = pix / G::PC, pcc = pix - prr * G::PC;
+                    const int fh = h0 * S + prr, fw = w0 * S + pcc;
+                    const bool core = cd >= 0 && fh < Hext && fw < Wext &&
+                                      ext_to_core(fh, a.Hc, a.circ, a.zpad) >= 0 &&
+                                      ext_to_core(fw, a.Wc, a.circ, a.zpad) >= 0;
+                    if (core) {  // frame values, crop zeros included, are normalised (conv padding is not)
+                        const int c0 = chunk * 16 + half * 8;
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) {
+                            float x = fmaf(pr[i].get(e), gscale[c0 + e], gshift[c0 + e]);
+                            if (a.pre_act == 1) x = nps::gelu_fast(x);
+                            pr[i].set(e, c0 + e < a.Cin ? x : 0.f);
+                        }
+                    }
+                }
+                pr[i].store(P + pix * 16 + ((half ^ swz(pix)) * 8));
+            }
+        }
+        T* Wl = P + G::PATCH;
+#pragma unroll
+        for (int i = 0; i < G::WPT; ++i) {
+            const int idx = tid + 256 * i;
+            if (idx < G::NWP) {
+                const int half = idx & 1, row = idx >> 1;  // row = tap * 64 + co
+                wr[i].store(Wl + row * 16 + ((half ^ swz(row & 63)) * 8));
+            }
+        }
+    };
+
+    f32x16 acc[2][G::RW];
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int r = 0; r < G::RW; ++r)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) acc[cb][r][q] = 0.f;
+
+    fetch(0);
+    commit(0, 0);
+    __syncthreads();
+    const int col = lane & 31, hl = lane >> 5;
+    for (int st = 0; st < nstage; ++st) {
+        const int buf = st & 1;
+        if (st + 1 < nstage) fetch(st + 1);
+        const T* P = ring + buf * G::BUF;
+        const T* Wl = P + G::PATCH;
+#pragma unroll
+        for (int kh = 0; kh < K; ++kh) {
+#pragma unroll
+            for (int kw = 0; kw < K; ++kw) {
+                const int tap = kh * K + kw;
+                if constexpr (sizeof(T) == 2) {
+                    bf16x8 A[2], Bv[G::RW];
+#pragma unroll
+                    for (int cb = 0; cb < 2; ++cb) {
+                        const int co = cb * 32 + col;
+                        A[cb] = *reinterpret_cast<const bf16x8*>(Wl + (tap * 64 + co) * 16 + ((hl ^ swz(co)) * 8));
+                    }
+#pragma unroll
+                    for (int r = 0; r < G::RW; ++r) {
+                        const int pix = ((wave * G::RW + r) * S + kh) * G::PC + col * S + kw;
+                        Bv[r] = *reinterpret_cast<const bf16x8*>(P + pix * 16 + ((hl ^ swz(pix)) * 8));
+                    }
+#pragma unroll
+                    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+                        for (int r = 0; r < G::RW; ++r)
+                            acc[cb][r] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[cb], Bv[r], acc[cb][r], 0, 0, 0);
+                } else {
+#pragma unroll
+                    for (int ks = 0; ks < 8; ++ks) {
+                        const int k = 2 * ks + hl;
+                        float A[2], Bv[G::RW];
+#pragma unroll
+                        for (int cb = 0; cb < 2; ++cb) {
+                            const int co = cb * 32 + col;
+                            A[cb] = Wl[(tap * 64 + co) * 16 + (((k >> 3) ^ swz(co)) * 8) + (k & 7)];
+                        }
+#pragma unroll
+                        for (int r = 0; r < G::RW; ++r) {
+                            const int pix = ((wave * G::RW + r) * S + kh) * G::PC + col * S + kw;
+                            Bv[r] = P[pix * 16 + (((k >> 3) ^ swz(pix)) * 8) + (k & 7)];
+                        }
+#pragma unroll
+                        for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+                            for (int r = 0; r < G::RW; ++r)
+                                acc[cb][r] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[cb], Bv[r], acc[cb][r], 0, 0, 0);
+                    }
+                }
+            }
+        }
+        if (st + 1 < nstage) commit(st + 1, buf ^ 1);
+        __syncthreads();
+    }
+
+    // epilogue: lane holds voxel column `col`, channels 8j + 4*hl + (0..3) of each 32-channel block
+    const int pd = a.transposed ? (z >> 2) : 0, ph = a.transposed ? ((z >> 1) & 1) : 0,
+              pw = a.transposed ? (z & 1) : 0;
+    const int od = md * a.out_os + a.out_off_d + pd;
+    if (od < 0 || od >= a.out_D) return;
+    T* out = reinterpret_cast<T*>(a.out);
+    const T* add = reinterpret_cast<const T*>(a.addend);
+    const int w = w0 + col;
+    const int ow = w * a.out_os + a.out_off_w + pw;
+    const bool vec4 = (a.out_C & 3) == 0 && (a.Cout & 3) == 0;
+#pragma unroll
+    for (int r = 0; r < G::RW; ++r) {
+        const int h = h0 + wave * G::RW + r;
+        const int oh = h * a.out_os + a.out_off_h + ph;
+        if (h >= a.Hout || w >= a.Wout || oh < 0 || oh >= a.out_H || ow < 0 || ow >= a.out_W) continue;
+        const size_t vox = (((size_t)b * a.out_D + od) * a.out_H + oh) * a.out_W + ow;
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int co0 = tile * 64 + cb * 32 + 8 * j + 4 * hl;
+                if (co0 >= a.Cout) continue;
+                float v[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int co = co0 + e;
+                    v[e] = acc[cb][r][4 * j + e] + ((a.bias != nullptr && co < a.Cout) ? a.bias[co] : 0.f);
+                }
+                T* op = out + vox * a.out_C + co0;
+                const T* ap = add != nullptr ? add + vox * a.out_C + co0 : nullptr;
+                if (vec4 && sizeof(T) == 4) {
+                    f32x4 o = {v[0], v[1], v[2], v[3]};
+                    if (ap) o += *reinterpret_cast<const f32x4*>(ap);
+                    if (a.act == 1)
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) o[e] = nps::gelu_erf(o[e]);
+                    if (a.accumulate) o += *reinterpret_cast<const f32x4*>(op);
+                    *reinterpret_cast<f32x4*>(op) = o;
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        if (co0 + e >= a.Cout) continue;
+                        float o = v[e];
+                        if (ap) o += ld1<T>(ap + e);
+                        if (a.act == 1) o = nps::gelu_erf(o);
+                        if (a.accumulate) o += ld1<T>(op + e);
+                        st1<T>(op + e, o);
+                    }
+                }
+            }
+        }
+    }
+}
+
+// wpack[(((((z*ntile + tile)*K + kd)*nchunk + chunk)*K*K + tap)*64 + col)*16 + k]
+template <typename T>
+__global__ void conv3d_pack_kernel(const float* __restrict__ w, T* __restrict__ wp, int Cout, int Cin, int K,
+                                   int transposed, int nchunk, int ntile, long n) {
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+        long r = i;
+        const int k = (int)(r % 16); r /= 16;
+        const int col = (int)(r % 64); r /= 64;
+        const int tap = (int)(r % (K * K)); r /= K * K;
+        const int chunk = (int)(r % nchunk); r /= nchunk;
+        const int kd = (int)(r % K); r /= K;
+        const int tile = (int)(r % ntile);
+        const int z = (int)(r / ntile);
+        const int co = tile * 64 + col, ci = chunk * 16 + k, kh = tap / K, kw = tap % K;
+        float v = 0.f;
+        if (co < Cout && ci < Cin) {
+            if (transposed) {  // phase (pd, ph, pw): tap t of an axis uses kernel index p + 2(1 - t)
+                const int qd = (z >> 2) + 2 * (1 - kd), qh = ((z >> 1) & 1) + 2 * (1 - kh), qw = (z & 1) + 2 * (1 - kw);
+                v = w[((((size_t)ci * Cout + co) * 4 + qd) * 4 + qh) * 4 + qw];
+            } else {
+                v = w[((((size_t)co * Cin + ci) * K + kd) * K + kh) * K + kw];
+            }
+        }
+        if constexpr (sizeof(T) == 2) wp[i] = (T)f2bf(v); else wp[i] = v;
+    }
+}
+
+// per (b, group) fp64 (sum, sum of squares) of a core frame; one thread per voxel, groups in registers
+template <typename T>
+__global__ __launch_bounds__(256) void gn_stats3d_kernel(const nps_conv3d_t a, int G, double* __restrict__ stats) {
+    __shared__ double scratch[4];
+    const int b = blockIdx.y;
+    const long nvox = (long)a.Dc * a.Hc * a.Wc;
+    const int cpg = a.Cin / G;
+    double s[8], q[8];
+#pragma unroll
+    for (int g = 0; g < 8; ++g) s[g] = q[g] = 0.0;
+    for (long v = (long)blockIdx.x * 256 + threadIdx.x; v < nvox; v += (long)gridDim.x * 256) {
+        const int cw = (int)(v % a.Wc);
+        const long r = v / a.Wc;
+        const int ch = (int)(r % a.Hc), cd = (int)(r / a.Hc);
+        int lo = 0;
+#pragma unroll
+        for (int si = 0; si < NPS_MAX_SRC; ++si) {
+            if (si < a.nsrc) {
+                const nps_src3_t& src = a.src[si];
+                const int dd = cd - src.off_d, hh = ch - src.off_h, ww = cw - src.off_w;
+                if (dd >= 0 && dd < src.D && hh >= 0 && hh < src.H && ww >= 0 && ww < src.W) {
+                    const T* p = reinterpret_cast<const T*>(src.ptr) +
+                                 ((((size_t)b * src.D + dd) * src.H + hh) * src.W + ww) * src.C;
+#pragma unroll
+                    for (int g = 0; g < 8; ++g) {
+                        if (g < G) {
+                            const int c1 = max(g * cpg, lo) - lo, c2 = min((g + 1) * cpg, lo + src.C) - lo;
+                            float fs = 0.f, fq = 0.f;
+                            for (int c = c1; c < c2; ++c) {
+                                const float x = ld1<T>(p + c);
+                                fs += x;
+                                fq = fmaf(x, x, fq);
+                            }
+                            s[g] += fs;
+                            q[g] += fq;
+                        }
+                    }
+                }
+                lo += src.C;
+            }
+        }
+    }
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+        if (g < G) {
+            const double ts = nps::block_sum(s[g], scratch);
+            const double tq = nps::block_sum(q[g], scratch);
+            if (threadIdx.x == 0) {
+                atomicAdd(stats + (b * G + g) * 2, ts);
+                atomicAdd(stats + (b * G + g) * 2 + 1, tq);
+            }
+        }
+    }
+}
+
+template <typename T, int K, int S, int TH>
+int launch(const nps_conv3d_t& a, int nchunk, int ntile, hipStream_t s) {
+    using G = Geo<K, S, TH>;
+    const size_t lds = 2 * (size_t)G::BUF * sizeof(T) + 2 * (size_t)nchunk * 16 * sizeof(float);
+    NPS_CHECK_ARG(lds <= 160 * 1024, "conv3d: %zu B of LDS (Cin too large for the GroupNorm table)", lds);
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)conv3d_kernel<T, K, S, TH>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        attr = true;
+    }
+    const long ntiles = (long)a.B * a.Dout * ((a.Hout + TH - 1) / TH) * ((a.Wout + 31) / 32);
+    NPS_CHECK_ARG(ntiles < (1L << 31), "conv3d: grid too large");
+    const dim3 grid((unsigned)ntiles, (unsigned)ntile, a.transposed ? 8u : 1u);
+    conv3d_kernel<T, K, S, TH><<<grid, 256, lds, s>>>(a, nchunk, ntile);
+    NPS_CHECK_LAUNCH("conv3d");
+    return 0;
+}
+
+template <typename T>
+int dispatch(const nps_conv3d_t& a, int nchunk, int ntile, hipStream_t s) {
+    if (a.K == 3 && a.stride == 1) return launch<T, 3, 1, 8>(a, nchunk, ntile, s);
+    if (a.K == 3 && a.stride == 2) return launch<T, 3, 2, 4>(a, nchunk, ntile, s);
+    if (a.K == 2 && a.stride == 1) return launch<T, 2, 1, 8>(a, nchunk, ntile, s);
+    if (a.K == 1 && a.stride == 1) return launch<T, 1, 1, 8>(a, nchunk, ntile, s);
+    NPS_CHECK_ARG(false, "conv3d: K=%d stride=%d not supported (K in {1,2,3}, stride 2 only for K=3)", a.K, a.stride);
+}
+
+int check_frame(const nps_conv3d_t& a, const char* who) {
+    NPS_CHECK_ARG(a.nsrc >= 1 && a.nsrc <= NPS_MAX_SRC && a.B > 0 && a.Dc > 0 && a.Hc > 0 && a.Wc > 0 && a.Cin > 0,
+                  "%s: bad frame", who);
+    int cs = 0;
+    for (int i = 0; i < a.nsrc; ++i) {
+        const nps_src3_t& s = a.src[i];
+        NPS_CHECK_ARG(s.ptr != nullptr && s.C > 0 && s.D > 0 && s.H > 0 && s.W > 0, "%s: bad source %d", who, i);
+        cs += s.C;
+    }
+    NPS_CHECK_ARG(cs == a.Cin, "%s: sources hold %d channels, frame Cin %d", who, cs, a.Cin);
+    return 0;
+}
+
+}  // namespace
+
+extern "C" size_t nps_conv3d_packed_bytes(int Cout, int Cin, int K, int transposed, int bf16) {
+    if (Cout <= 0 || Cin <= 0 || K <= 0) return 0;
+    const size_t nphase = transposed ? 8 : 1, nchunk = (Cin + 15) / 16, ntile = (Cout + 63) / 64;
+    return nphase * ntile * K * nchunk * K * K * 64 * 16 * (bf16 ? 2 : 4);
+}
+
+extern "C" int nps_conv3d_pack_weights(const float* w, void* wpack, int Cout, int Cin, int K, int transposed, int bf16,
+                                       void* stream) {
+    NPS_CHECK_ARG(w && wpack && Cout > 0 && Cin > 0 && (K >= 1 && K <= 3) && (!transposed || K == 2),
+                  "conv3d_pack_weights: bad args");
+    const int nchunk = (Cin + 15) / 16, ntile = (Cout + 63) / 64;
+    const long n = (long)(transposed ? 8 : 1) * ntile * K * nchunk * K * K * 64 * 16;
+    const long nb = (n + 255) / 256 < 8192 ? (n + 255) / 256 : 8192;
+    hipStream_t s = (hipStream_t)stream;
+    if (bf16)
+        conv3d_pack_kernel<bf16_t><<<(unsigned)nb, 256, 0, s>>>(w, reinterpret_cast<bf16_t*>(wpack), Cout, Cin, K,
+                                                                 transposed, nchunk, ntile, n);
+    else
+        conv3d_pack_kernel<float><<<(unsigned)nb, 256, 0, s>>>(w, reinterpret_cast<float*>(wpack), Cout, Cin, K,
+                                                                transposed, nchunk, ntile, n);
+    NPS_CHECK_LAUNCH("conv3d_pack_weights");
+    return 0;
+}
+
+extern "C" int nps_conv3d_fwd(const nps_conv3d_t* ap, void* stream) {
+    NPS_CHECK_ARG(ap != nullptr, "conv3d: null args");
+    const nps_conv3d_t& a = *ap;
+    if (check_frame(a, "conv3d") < 0) return -1;
+    NPS_CHECK_ARG(a.wpack && a.out && a.Cout > 0 && a.out_C >= a.Cout && a.out_os >= 1 && a.out_D > 0 &&
+                      a.out_H > 0 && a.out_W > 0 && a.circ >= 0 && a.zpad >= 0,
+                  "conv3d: bad output / weight args");
+    NPS_CHECK_ARG(!a.transposed || (a.K == 2 && a.stride == 1), "conv3d: transposed = 8 phases of K=2, stride 1");
+    NPS_CHECK_ARG(a.circ <= a.Dc && a.circ <= a.Hc && a.circ <= a.Wc, "conv3d: circular extension beyond the frame");
+    const int ext = 2 * (a.circ + a.zpad);
+    NPS_CHECK_ARG(a.Dout == (a.Dc + ext - a.K) / a.stride + 1 && a.Hout == (a.Hc + ext - a.K) / a.stride + 1 &&
+                      a.Wout == (a.Wc + ext - a.K) / a.stride + 1 && a.Dout > 0 && a.Hout > 0 && a.Wout > 0,
+                  "conv3d: output extent %dx%dx%d does not match the frame", a.Dout, a.Hout, a.Wout);
+    NPS_CHECK_ARG(a.gn_stats == nullptr || (a.gn_gamma && a.gn_beta && a.gn_groups >= 1 && a.gn_groups <= 8 &&
+                                            a.Cin % a.gn_groups == 0),
+                  "conv3d: bad GroupNorm prologue");
+    NPS_CHECK_ARG(a.pre_act == 0 || a.pre_act == 1, "conv3d: pre_act 0 or 1");
+    const int nchunk = (a.Cin + 15) / 16, ntile = (a.Cout + 63) / 64;
+    hipStream_t s = (hipStream_t)stream;
+    return a.bf16 ? dispatch<bf16_t>(a, nchunk, ntile, s) : dispatch<float>(a, nchunk, ntile, s);
+}
+
+extern "C" int nps_gn_stats3d(const nps_conv3d_t* ap, int G, double* stats, void* stream) {
+    NPS_CHECK_ARG(ap != nullptr && stats != nullptr, "gn_stats3d: null args");
+    const nps_conv3d_t& a = *ap;
+    if (check_frame(a, "gn_stats3d") < 0) return -1;
+    NPS_CHECK_ARG(G >= 1 && G <= 8 && a.Cin % G == 0, "gn_stats3d: groups %d must divide Cin %d (<= 8)", G, a.Cin);
+    const long nvox = (long)a.Dc * a.Hc * a.Wc;
+    const long nb = (nvox + 255) / 256 < 1024 ? (nvox + 255) / 256 : 1024;
+    hipStream_t s = (hipStream_t)stream;
+    if (a.bf16)
+        gn_stats3d_kernel<bf16_t><<<dim3((unsigned)nb, (unsigned)a.B), 256, 0, s>>>(a, G, stats);
+    else
+        gn_stats3d_kernel<float><<<dim3((unsigned)nb, (unsigned)a.B), 256, 0, s>>>(a, G, stats);
+    NPS_CHECK_LAUNCH("gn_stats3d");
+    return 0;
+}

@@ -172,10 +172,77 @@ class ConvTranspose2d_padded(ConvTranspose2d):
         self.pre_pad = pad
 
 
-class Conv3d(_PackedMixin, nn.Conv3d):
+def crop_offsets3(cur, des):
+    """(d, h, w) placement of a cur-sized volume inside a des-sized frame, crop_Nd semantics (common.py:20-34)."""
+    return tuple(ops.crop_offset(c, d) for c, d in zip(cur, des))
+
+
+def to_ndhwc(x):
+    """(B, C, D, H, W) -> contiguous (B, D, H, W, C) on the HIP transpose (fp32; bf16 via fp32)."""
+    B, C, D, H, W = x.shape
+    bf = x.dtype == torch.bfloat16
+    x4 = x.reshape(B, C, D * H, W)
+    y = ops.nchw_to_nhwc(ops.to_f32(x4.contiguous()) if bf else x4)
+    return (ops.to_bf16(y) if bf else y).view(B, D, H, W, C)
+
+
+def to_ncdhw(y):
+    """(B, D, H, W, C) -> (B, C, D, H, W) on the HIP transpose."""
+    B, D, H, W, C = y.shape
+    bf = y.dtype == torch.bfloat16
+    y4 = y.reshape(B, D * H, W, C)
+    x = ops.nhwc_to_nchw(ops.to_f32(y4) if bf else y4)
+    return (ops.to_bf16(x) if bf else x).view(B, C, D, H, W)
+
+
+class _Packed3Mixin:
+    """Caches the nps_conv3d packing of `weight` per storage dtype, re-packed when the parameter changes."""
+
+    def _packed3(self, bf16: bool, transposed: bool = False):
+        w = self.weight
+        key = (w.data_ptr(), w._version, str(w.device), bf16)
+        cache = self.__dict__.setdefault("_pk3", {})
+        if cache.get("key_" + str(bf16)) != key:
+            cache[bf16] = ops.pack_conv3d_weight(w, transposed=transposed, bf16=bf16)
+            cache["key_" + str(bf16)] = key
+        return cache[bf16]
+
+
+class Conv3d(_Packed3Mixin, _PackedMixin, nn.Conv3d):
     """nn.Conv3d parameters (common.py:37-47 with spatial_dim 3).  The FNO-3D pointwise `w` conv
-    (fno_kernel_size 1) runs as a 1x1 conv over the (D*H, W) view of NDHWC activations on the HIP
-    conv kernel; other 3-D convs are not on the MI355X path."""
+    (fno_kernel_size 1) runs as a 1x1 conv over the (D*H, W) view of NDHWC activations on the 2-D HIP
+    conv kernels (run / run_bf16); the 3-D U-Net's convs (k = 1 or 3, stride 1 or 2, valid / zero / circular
+    padding) run on the NDHWC implicit-GEMM kernel nps_conv3d (run3d)."""
+
+    def geometry3d(self):
+        """(K, stride, circ, zpad) of a cubic, isotropic, undilated conv."""
+        ks, st, dl = set(self.kernel_size), set(self.stride), set(self.dilation)
+        if len(ks) != 1 or len(st) != 1 or dl != {1} or self.groups != 1:
+            raise NotImplementedError("3-D convs: cubic kernel, isotropic stride, no dilation or groups")
+        K, s = ks.pop(), st.pop()
+        if self.padding == "same":
+            if K % 2 == 0:
+                raise NotImplementedError("3-D 'same' padding with an even kernel")
+            p = (K - 1) // 2
+        elif self.padding == "valid":
+            p = 0
+        else:
+            pads = set(self.padding)
+            if len(pads) != 1:
+                raise NotImplementedError("anisotropic 3-D padding")
+            p = pads.pop()
+        if self.padding_mode == "circular":
+            return K, s, p, 0
+        if self.padding_mode != "zeros":
+            raise NotImplementedError(f"padding_mode {self.padding_mode}")
+        return K, s, 0, p
+
+    def run3d(self, srcs, frame_dhw, **kw):
+        """srcs: ops.Src3 NDHWC sources (fp32 or bf16) of a virtual frame -> (B, Do, Ho, Wo, Cout)."""
+        K, s, circ, zpad = self.geometry3d()
+        bf16 = srcs[0].t.dtype == torch.bfloat16
+        return ops.conv3d(srcs, frame_dhw, self._packed3(bf16), self.bias, self.out_channels, K, stride=s, circ=circ,
+                          zpad=zpad, **kw)
 
     def _check(self):
         if tuple(self.kernel_size) != (1, 1, 1) or tuple(self.stride) != (1, 1, 1) or self.groups != 1 \
@@ -207,6 +274,10 @@ class Conv3d(_PackedMixin, nn.Conv3d):
                                  self.bias)
 
     def forward(self, x):
+        if tuple(self.kernel_size) != (1, 1, 1) or tuple(self.stride) != (1, 1, 1):
+            if use_autograd(self):
+                raise NotImplementedError("the 3-D U-Net is inference-only on the MI355X path (C5 rollout)")
+            return to_ncdhw(self.run3d([ops.Src3(to_ndhwc(x))], x.shape[2:]))
         B, C, D, H, W = x.shape
         x4 = x.reshape(B, C, D * H, W)
         if use_autograd(self):
@@ -228,8 +299,32 @@ def get_conv_with_right_spatial_dim(spatial_dim, **kwargs):
     raise NotImplementedError(f"only 0<x<=3d convs implemented so far, but found spatial dim {spatial_dim}!")
 
 
+class ConvTranspose3d_padded(_Packed3Mixin, nn.ConvTranspose3d):
+    """The 3-D U-Net Upsample, DEFINED by this build (the reference raises NotImplementedError for 3-D,
+    common.py:103-120): the 2-D rule of ConvTranspose2d_padded (common.py:93-100) applied per axis —
+    circular pad `pad` on every spatial axis, then ConvTranspose3d(k=4, s=2, p=0).  Runs as the 8 phase
+    convs of nps_conv3d (transposed)."""
+
+    def __init__(self, pad, *args, **kwargs):
+        super().__init__(*args, **kwargs)
+        self.pad = pad
+
+    def run3d(self, x, **kw):
+        if (set(self.kernel_size) != {4} or set(self.stride) != {2} or set(self.padding) != {0}
+                or set(self.output_padding) != {0} or set(self.dilation) != {1} or self.groups != 1):
+            raise NotImplementedError("3-D Upsample: ConvTranspose3d(k=4, s=2, p=0) only")
+        bf16 = x.dtype == torch.bfloat16
+        return ops.conv3d([ops.Src3(x)], x.shape[1:4], self._packed3(bf16, transposed=True), self.bias,
+                          self.out_channels, 2, transposed=True, circ=self.pad, zpad=1, **kw)
+
+    def forward(self, x):
+        if use_autograd(self):
+            raise NotImplementedError("the 3-D U-Net is inference-only on the MI355X path (C5 rollout)")
+        return to_ncdhw(self.run3d(to_ndhwc(x)))
+
+
 def get_upconv_with_right_spatial_dim(spatial_dim, in_channels, out_channels, **kwargs):
-    """common.py:103-120."""
+    """common.py:103-120, plus a 3-D circular form the reference lacks (ConvTranspose3d_padded)."""
     if spatial_dim == 1:
         return nn.ConvTranspose1d(in_channels, out_channels, **kwargs)
     if spatial_dim == 2:
@@ -240,4 +335,9 @@ def get_upconv_with_right_spatial_dim(spatial_dim, in_channels, out_channels, **
             del kw["padding_mode"]
             return ConvTranspose2d_padded(slice_size, in_channels, out_channels, **kw)
         return ConvTranspose2d(in_channels, out_channels, **kwargs)
+    if spatial_dim == 3 and kwargs.get("padding_mode") == "circular":
+        # DESIGN.md "3-D U-FNO": BASELINE config C5 needs a 3-D Upsample; defined as the 2-D rule per axis
+        kw = copy.deepcopy(kwargs)
+        del kw["padding_mode"]
+        return ConvTranspose3d_padded((kw["kernel_size"] - 1) // 2, in_channels, out_channels, **kw)
     raise NotImplementedError(f"only 0<x<=2d convs implemented so far, but found spatial dim {spatial_dim}!")

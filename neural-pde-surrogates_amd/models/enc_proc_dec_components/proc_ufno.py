@@ -11,7 +11,7 @@ import torch
 from torch import nn
 
 from common.interfaces import D, M
-from models.common import activation_code, use_autograd
+from models.common import activation_code, use_autograd, to_ndhwc, to_ncdhw
 from models.enc_proc_dec_components.proc_fno import FNO_Layer
 from models.enc_proc_dec_components.proc_unet_modern import UNetModern
 from nps_hip import ops
@@ -68,6 +68,24 @@ class UFNO(nn.Module):
             h = unet.run(h, vb, addend=h_fno, act_after=act)
         return h
 
+    def run3d(self, h, vb):
+        """3-D U-FNO (BASELINE config C5) on NDHWC (B, D, H, W, C) activations, fp32 or bf16 storage: per
+        block the FNO-3D layer on cat(h, vb) (the (B, D*H, W, C) view), then the 3-D U-Net whose final conv
+        epilogue adds it and applies the activation (proc_ufno.py:105-118)."""
+        if self.cond_mode != "concat":
+            raise NotImplementedError("U-FNO: only cond_mode='concat' runs on the MI355X path")
+        if self.num_spatial_dims != 3:
+            raise NotImplementedError("UFNO.run3d: 3-D only")
+        act = activation_code(self.activation)
+        bf16 = h.dtype == torch.bfloat16
+        B, D, H, W = h.shape[:4]
+        flat = lambda t: t.view(t.shape[0], D * H, W, t.shape[4])  # noqa: E731
+        for fno, unet in zip(self.fno_layers, self.unet_layers):
+            srcs = [ops.Src(flat(h))] + ([ops.Src(flat(vb))] if vb is not None else [])
+            h_fno = fno.run_bf16(srcs, D) if bf16 else fno.run(srcs, D=D)
+            h = unet.run3d(h, vb, addend=h_fno.view(B, D, H, W, h_fno.shape[3]), act_after=act)
+        return h
+
     def run_ad(self, h, vb):
         """Differentiable form of run() (training)."""
         if self.cond_mode != "concat":
@@ -81,6 +99,13 @@ class UFNO(nn.Module):
 
     def forward(self, h: torch.Tensor, variables: torch.Tensor = None, variables_broadcast: torch.Tensor = None,
                 pos=None):
+        if self.num_spatial_dims == 3:  # (B, C, D, H, W), fp32 or bf16 storage (C5)
+            if use_autograd(self):
+                raise NotImplementedError("the 3-D U-FNO is inference-only on the MI355X path (C5 rollout)")
+            vb = to_ndhwc(variables_broadcast) if variables_broadcast is not None else None
+            if vb is not None and vb.dtype != h.dtype:  # conditioning in the activations' storage dtype
+                vb = ops.to_bf16(vb) if h.dtype == torch.bfloat16 else ops.to_f32(vb)
+            return to_ncdhw(self.run3d(to_ndhwc(h), vb))
         if use_autograd(self):
             vb = ad.to_nhwc(variables_broadcast) if variables_broadcast is not None else None
             return ad.to_nchw(self.run_ad(ad.to_nhwc(h), vb))

@@ -17,7 +17,7 @@ from torch import nn
 
 from common.interfaces import D, M
 from models.common import (get_conv_with_right_spatial_dim, get_upconv_with_right_spatial_dim, crop_offsets,
-                           activation_code, use_autograd)
+                           crop_offsets3, activation_code, use_autograd, to_ndhwc, to_ncdhw)
 from nps_hip import ops
 from nps_hip import autograd as ad
 from pdes import PDE
@@ -167,6 +167,52 @@ class UNetModern(nn.Module):
         y = ad.conv2d(self.final, ad.frame([ops.Src(h)], (H, W), norm, activation_code(self.activation)))
         return ad.crop(y, h_shape[1:3], crop_offsets(y.shape[1:3], h_shape[1:3]))
 
+    def run3d(self, h, vb, addend=None, act_after=0):
+        """NDHWC forward of the 3-D U-Net (proc_unet_modern.py:169-196 with num_spatial_dims=3; the 3-D
+        Upsample is this build's ConvTranspose3d_padded), fp32 or bf16 storage.  Optional fused epilogue on
+        the final conv: out = act_after(final(...) + addend) — the U-FNO block combination."""
+        if self.num_spatial_dims != 3:
+            raise NotImplementedError("UNetModern.run3d: 3-D U-Nets only")
+        if self.n_cond > 0 and vb is None:
+            raise ValueError("UNetModern with n_cond > 0 needs variables_broadcast")
+        if self.n_cond == 0:
+            vb = None
+        h_shape = h.shape
+        feats, vbs = [h], [vb]
+        for m in self.down:
+            if isinstance(m, Downsample):
+                h, vb = m.run3d(h, vb)
+            else:
+                h = m.run3d(h, vb)
+            feats.append(h)
+            vbs.append(vb)
+        h = self.middle.run3d(h, vb)
+        for m in self.up:
+            if isinstance(m, Upsample):
+                h = m.conv.run3d(h)
+            else:
+                _check_no_attn(m)
+                s = feats.pop()
+                v = vbs.pop()
+                dhw = tuple(h.shape[1:4])
+                srcs = [ops.Src3(h), ops.Src3(s, *crop_offsets3(s.shape[1:4], dhw))]
+                if v is not None:
+                    srcs.append(ops.Src3(v, *crop_offsets3(v.shape[1:4], dhw)))
+                h = m.res.run3d(srcs, dhw)
+        dhw = tuple(h.shape[1:4])
+        gn = None
+        if isinstance(self.norm, nn.GroupNorm):
+            gn = _gn_args(self.norm, ops.gn_stats3d([ops.Src3(h)], dhw, self.norm.num_groups))
+        K, s, circ, zpad = self.final.geometry3d()
+        fo = tuple((n + 2 * (circ + zpad) - K) // s + 1 for n in dhw)
+        off = crop_offsets3(fo, h_shape[1:4])
+        out = torch.empty(tuple(h_shape[:4]) + (self.final.out_channels,), dtype=h.dtype, device=h.device)
+        if any(o > 0 for o in off):
+            out.zero_()  # crop_Nd zero-pads when the output is smaller than the input
+        self.final.run3d([ops.Src3(h)], dhw, gn=gn, pre_act=activation_code(self.activation), out=out, out_off=off,
+                         addend=addend, act=act_after)
+        return out
+
     def final_out_hw(self, H, W):
         KH, KW, s, d, lo, hi, circ = self.final.geometry()
         return ((H + 2 * circ + lo[0] + hi[0] - d * (KH - 1) - 1) // s + 1,
@@ -174,6 +220,11 @@ class UNetModern(nn.Module):
 
     def forward(self, h: torch.Tensor, variables_broadcast: torch.Tensor = None, pos=None):
         assert h.dim() == 2 + self.num_spatial_dims
+        if self.num_spatial_dims == 3:
+            if use_autograd(self):
+                raise NotImplementedError("the 3-D U-Net is inference-only on the MI355X path (C5 rollout)")
+            vb = to_ndhwc(variables_broadcast) if variables_broadcast is not None else None
+            return to_ncdhw(self.run3d(to_ndhwc(h), vb))
         if use_autograd(self):
             vb = ad.to_nhwc(variables_broadcast) if variables_broadcast is not None else None
             return ad.to_nchw(self.run_ad(ad.to_nhwc(h), vb))
@@ -244,6 +295,30 @@ class ResidualBlock(nn.Module):
             ops.attach_stats(out, st2)
         return out
 
+    def run3d(self, srcs, frame_dhw):
+        """3-D form of run() on NDHWC Src3 sources: GN-stats -> conv1 [GN+GELU prologue] -> GN-stats ->
+        conv2 [GN+GELU prologue] accumulated at the crop_Nd offset into the shortcut (1x1 conv or x)."""
+        act = activation_code(self.activation)
+        gn1 = gn2 = None
+        if isinstance(self.norm1, nn.GroupNorm):
+            gn1 = _gn_args(self.norm1, ops.gn_stats3d(srcs, frame_dhw, self.norm1.num_groups))
+        h1 = self.conv1.run3d(srcs, frame_dhw, gn=gn1, pre_act=act)
+        if isinstance(self.shortcut, nn.Identity):
+            s0 = srcs[0]
+            if len(srcs) != 1 or s0.off_d or s0.off_h or s0.off_w or tuple(s0.t.shape[1:4]) != tuple(frame_dhw):
+                raise RuntimeError("identity shortcut on a concatenated input")
+            out = s0.t.clone()
+        else:
+            out = self.shortcut.run3d(srcs, frame_dhw)
+        d1 = tuple(h1.shape[1:4])
+        if isinstance(self.norm2, nn.GroupNorm):
+            gn2 = _gn_args(self.norm2, ops.gn_stats3d([ops.Src3(h1)], d1, self.norm2.num_groups))
+        K, s, circ, zpad = self.conv2.geometry3d()
+        d2 = tuple((n + 2 * (circ + zpad) - K) // s + 1 for n in d1)
+        self.conv2.run3d([ops.Src3(h1)], d1, gn=gn2, pre_act=act, out=out,
+                         out_off=crop_offsets3(d2, out.shape[1:4]), accumulate=True)
+        return out
+
     def run_ad(self, srcs, frame_hw):
         """Differentiable form of run(): frame -> GN+GELU -> conv1 -> GN+GELU -> conv2, + shortcut."""
         act = activation_code(self.activation)
@@ -261,6 +336,11 @@ class ResidualBlock(nn.Module):
         return ad.add_at(sc, h2, crop_offsets(h2.shape[1:3], sc.shape[1:3]))
 
     def forward(self, x: torch.Tensor):
+        if self.num_spatial_dims == 3:
+            if use_autograd(self):
+                raise NotImplementedError("the 3-D U-Net is inference-only on the MI355X path (C5 rollout)")
+            x = to_ndhwc(x)
+            return to_ncdhw(self.run3d([ops.Src3(x)], x.shape[1:4]))
         if use_autograd(self):
             x = ad.to_nhwc(x)
             return ad.to_nchw(self.run_ad([ops.Src(x)], x.shape[1:3]))
@@ -317,7 +397,15 @@ class DownBlock(nn.Module):
         srcs = [ops.Src(x)] + ([ops.Src(vb)] if vb is not None else [])
         return self.res.run_ad(srcs, x.shape[1:3])
 
+    def run3d(self, x, vb):
+        _check_no_attn(self)
+        srcs = [ops.Src3(x)] + ([ops.Src3(vb)] if vb is not None else [])
+        return self.res.run3d(srcs, x.shape[1:4])
+
     def forward(self, x: torch.Tensor, variables_broadcast: torch.Tensor = None):
+        if self.res.num_spatial_dims == 3:
+            vb = to_ndhwc(variables_broadcast) if variables_broadcast is not None else None
+            return to_ncdhw(self.run3d(to_ndhwc(x), vb)), variables_broadcast
         if use_autograd(self):
             vb = ad.to_nhwc(variables_broadcast) if variables_broadcast is not None else None
             return ad.to_nchw(self.run_ad(ad.to_nhwc(x), vb)), variables_broadcast
@@ -337,6 +425,8 @@ class UpBlock(nn.Module):
 
     def forward(self, x: torch.Tensor):
         _check_no_attn(self)
+        if self.res.num_spatial_dims == 3:
+            return self.res(x)
         if use_autograd(self):
             x = ad.to_nhwc(x)
             return ad.to_nchw(self.res.run_ad([ops.Src(x)], x.shape[1:3]))
@@ -368,7 +458,16 @@ class MiddleBlock(nn.Module):
         h = self.res1.run_ad(srcs, x.shape[1:3])
         return self.res2.run_ad([ops.Src(h)], h.shape[1:3])
 
+    def run3d(self, x, vb):
+        _check_no_attn(self)
+        srcs = [ops.Src3(x)] + ([ops.Src3(vb)] if vb is not None else [])
+        h = self.res1.run3d(srcs, x.shape[1:4])
+        return self.res2.run3d([ops.Src3(h)], h.shape[1:4])
+
     def forward(self, x: torch.Tensor, variables_broadcast: torch.Tensor = None):
+        if self.res1.num_spatial_dims == 3:
+            vb = to_ndhwc(variables_broadcast) if variables_broadcast is not None else None
+            return to_ncdhw(self.run3d(to_ndhwc(x), vb)), variables_broadcast
         if use_autograd(self):
             vb = ad.to_nhwc(variables_broadcast) if variables_broadcast is not None else None
             return ad.to_nchw(self.run_ad(ad.to_nhwc(x), vb)), variables_broadcast
@@ -413,12 +512,21 @@ class Downsample(nn.Module):
             vb = ad.conv2d(self.conv_variables_broadcast, vb)
         return h, vb
 
+    def run3d(self, x, vb):
+        h = self.conv.run3d([ops.Src3(x)], x.shape[1:4])
+        if vb is not None:
+            vb = self.conv_variables_broadcast.run3d([ops.Src3(vb)], vb.shape[1:4])
+        return h, vb
+
     def forward(self, x: torch.Tensor, variables_broadcast: torch.Tensor = None):
         if use_autograd(self):
             if variables_broadcast is not None:
                 h, v = self.run_ad(ad.to_nhwc(x), ad.to_nhwc(variables_broadcast))
                 return ad.to_nchw(h), ad.to_nchw(v)
             return self.conv(x)
+        if variables_broadcast is not None and x.dim() == 5:
+            h, v = self.run3d(to_ndhwc(x), to_ndhwc(variables_broadcast))
+            return to_ncdhw(h), to_ncdhw(v)
         if variables_broadcast is not None:
             h, v = self.run(ops.nchw_to_nhwc(x), ops.nchw_to_nhwc(variables_broadcast))
             return ops.nhwc_to_nchw(h), ops.nhwc_to_nchw(v)

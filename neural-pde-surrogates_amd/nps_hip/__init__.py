@@ -13,7 +13,7 @@ import os
 
 import torch
 
-__all__ = ["lib", "Src", "Conv2dArgs", "WgradArgs", "check", "stream_ptr", "ptr", "LIB_PATH"]
+__all__ = ["lib", "Src", "Conv2dArgs", "WgradArgs", "Src3", "Conv3dArgs", "check", "stream_ptr", "ptr", "LIB_PATH"]
 
 LIB_PATH = os.environ.get("NPS_HIP_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "libnps_hip.so"))
 if not os.path.exists(LIB_PATH):
@@ -57,6 +57,28 @@ class WgradArgs(ctypes.Structure):
         ("x", ctypes.c_void_p), ("Hx", ctypes.c_int), ("Wx", ctypes.c_int), ("N", ctypes.c_int),
         ("KH", ctypes.c_int), ("KW", ctypes.c_int), ("dil", ctypes.c_int), ("pad_y", ctypes.c_int),
         ("pad_x", ctypes.c_int), ("circ", ctypes.c_int), ("g", ctypes.c_void_p),
+    ]
+
+
+class Src3(ctypes.Structure):
+    _fields_ = [("ptr", ctypes.c_void_p), ("C", ctypes.c_int), ("D", ctypes.c_int), ("H", ctypes.c_int),
+                ("W", ctypes.c_int), ("off_d", ctypes.c_int), ("off_h", ctypes.c_int), ("off_w", ctypes.c_int)]
+
+
+class Conv3dArgs(ctypes.Structure):
+    _fields_ = [
+        ("nsrc", ctypes.c_int), ("src", Src3 * MAX_SRC),
+        ("B", ctypes.c_int), ("Dc", ctypes.c_int), ("Hc", ctypes.c_int), ("Wc", ctypes.c_int), ("Cin", ctypes.c_int),
+        ("circ", ctypes.c_int), ("zpad", ctypes.c_int),
+        ("gn_stats", ctypes.c_void_p), ("gn_gamma", ctypes.c_void_p), ("gn_beta", ctypes.c_void_p),
+        ("gn_groups", ctypes.c_int), ("gn_eps", ctypes.c_float), ("pre_act", ctypes.c_int),
+        ("K", ctypes.c_int), ("stride", ctypes.c_int), ("transposed", ctypes.c_int),
+        ("Dout", ctypes.c_int), ("Hout", ctypes.c_int), ("Wout", ctypes.c_int),
+        ("wpack", ctypes.c_void_p), ("bias", ctypes.c_void_p), ("Cout", ctypes.c_int),
+        ("out", ctypes.c_void_p), ("out_C", ctypes.c_int), ("out_D", ctypes.c_int), ("out_H", ctypes.c_int),
+        ("out_W", ctypes.c_int), ("out_os", ctypes.c_int), ("out_off_d", ctypes.c_int), ("out_off_h", ctypes.c_int),
+        ("out_off_w", ctypes.c_int), ("accumulate", ctypes.c_int), ("addend", ctypes.c_void_p), ("act", ctypes.c_int),
+        ("bf16", ctypes.c_int),
     ]
 
 
@@ -123,6 +145,11 @@ _SIGS = {
     "nps_conv1x1_bf16_kr": (_i, [_i]),
     "nps_pack_1x1_bf16": (_i, [_vp, _vp, _i, _i, _vp]),
     "nps_conv1x1_bf16": (_i, [ctypes.POINTER(Conv2dArgs), _vp]),
+    # 3-D U-Net (C5 U-FNO 3D)
+    "nps_conv3d_packed_bytes": (_sz, [_i, _i, _i, _i, _i]),
+    "nps_conv3d_pack_weights": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp]),
+    "nps_conv3d_fwd": (_i, [ctypes.POINTER(Conv3dArgs), _vp]),
+    "nps_gn_stats3d": (_i, [ctypes.POINTER(Conv3dArgs), _i, _vp, _vp]),
     "nps_last_error": (ctypes.c_char_p, []),
     "nps_version": (ctypes.c_char_p, []),
 }

@@ -11,7 +11,7 @@ from typing import List, NamedTuple, Optional, Sequence
 
 import torch
 
-from . import Conv2dArgs, Src as _CSrc, check, lib, ptr, stream_ptr
+from . import Conv2dArgs, Conv3dArgs, Src as _CSrc, Src3 as _CSrc3, check, lib, ptr, stream_ptr
 
 GELU = 1
 
@@ -673,6 +673,109 @@ def spectral_conv3d_bf16(srcs: Sequence[Src], D: int, wpack_bf16: torch.Tensor, 
     check(lib.nps_spectral_idft_h(ptr(Z1), ptr(Z2), B * D, H, m2, m3, Cout, s), "spectral3d idft_h (H)")
     check(lib.nps_spectral_idft_w_bf16(ptr(Z2), ptr(out), B, D * H, W, m3, Cout, 1 if accumulate else 0, ptr(addend),
                                        act, s), "idft_w bf16")
+    return out
+
+
+# ------------------------------------------------------------ 3-D U-Net (C5) -----
+class Src3(NamedTuple):
+    t: torch.Tensor          # (B, D, H, W, C) NDHWC contiguous, fp32 or bf16
+    off_d: int = 0
+    off_h: int = 0
+    off_w: int = 0
+
+
+def _fill_frame3(a, srcs: Sequence[Src3], frame_dhw):
+    t0 = srcs[0].t
+    dt = t0.dtype
+    if dt not in (torch.float32, torch.bfloat16):
+        raise RuntimeError(f"nps_hip conv3d: fp32 or bf16 sources, got {dt}")
+    a.nsrc = len(srcs)
+    for i, s in enumerate(srcs):
+        t = s.t
+        if t.dtype != dt or not t.is_contiguous() or t.dim() != 5 or t.shape[0] != t0.shape[0]:
+            raise RuntimeError(f"nps_hip conv3d: sources must be contiguous NDHWC of one dtype / batch, got "
+                               f"{t.dtype} {tuple(t.shape)}")
+        a.src[i].ptr = ptr(t)
+        a.src[i].D, a.src[i].H, a.src[i].W, a.src[i].C = t.shape[1], t.shape[2], t.shape[3], t.shape[4]
+        a.src[i].off_d, a.src[i].off_h, a.src[i].off_w = int(s.off_d), int(s.off_h), int(s.off_w)
+    a.B = t0.shape[0]
+    a.Dc, a.Hc, a.Wc = (int(v) for v in frame_dhw)
+    a.Cin = sum(s.t.shape[4] for s in srcs)
+    a.bf16 = 1 if dt == torch.bfloat16 else 0
+    return a
+
+
+def pack_conv3d_weight(w: torch.Tensor, transposed=False, bf16=False) -> torch.Tensor:
+    """nn.Conv3d weight (Cout, Cin, K, K, K) / nn.ConvTranspose3d weight (Cin, Cout, 4, 4, 4) -> the
+    nps_conv3d packing in fp32 or bf16."""
+    w = w.detach().float().contiguous()
+    if transposed:
+        Cin, Cout, K = w.shape[0], w.shape[1], 2
+    else:
+        Cout, Cin, K = w.shape[0], w.shape[1], w.shape[2]
+    nbytes = lib.nps_conv3d_packed_bytes(Cout, Cin, K, 1 if transposed else 0, 1 if bf16 else 0)
+    out = torch.empty(nbytes // (2 if bf16 else 4), dtype=torch.bfloat16 if bf16 else torch.float32, device=w.device)
+    check(lib.nps_conv3d_pack_weights(ptr(w), ptr(out), Cout, Cin, K, 1 if transposed else 0, 1 if bf16 else 0,
+                                      stream_ptr()), "conv3d_pack_weights")
+    return out
+
+
+def gn_stats3d(srcs: Sequence[Src3], frame_dhw, groups: int) -> torch.Tensor:
+    """(B, groups, 2) fp64 (sum, sum of squares) of the virtual NDHWC frame's GroupNorm groups."""
+    a = _fill_frame3(Conv3dArgs(), srcs, frame_dhw)
+    st = torch.zeros((a.B, groups, 2), dtype=torch.float64, device=srcs[0].t.device)
+    check(lib.nps_gn_stats3d(ctypes_byref(a), groups, ptr(st), stream_ptr()), "gn_stats3d")
+    return st
+
+
+def conv3d(srcs: Sequence[Src3], frame_dhw, wpack: torch.Tensor, bias: Optional[torch.Tensor], Cout: int, K: int,
+           stride=1, transposed=False, circ=0, zpad=0, gn: Optional[GN] = None, pre_act=0,
+           out: Optional[torch.Tensor] = None, out_os=1, out_off=(0, 0, 0), accumulate=False,
+           addend: Optional[torch.Tensor] = None, act=0) -> torch.Tensor:
+    """One nps_conv3d launch over a virtual NDHWC frame (sources at crop offsets), extended per side by
+    `circ` circular then `zpad` zero voxels; valid K^3 conv (stride), or with `transposed` the 8 phase convs
+    (K = 2) of a k4/s2 transposed conv written with out_os = 2.  Without `out` a tensor of the conv's
+    output extent (x2 per axis when transposed) is allocated.  Returns `out`."""
+    a = _fill_frame3(Conv3dArgs(), srcs, frame_dhw)
+    ext = 2 * (circ + zpad)
+    Dout, Hout, Wout = ((n + ext - K) // stride + 1 for n in (a.Dc, a.Hc, a.Wc))
+    if min(Dout, Hout, Wout) <= 0:
+        raise RuntimeError(f"nps_hip conv3d: empty output for frame {tuple(frame_dhw)} K={K}")
+    dt = srcs[0].t.dtype
+    if (wpack.dtype == torch.bfloat16) != (dt == torch.bfloat16):
+        raise RuntimeError("nps_hip conv3d: weight packing dtype must match the activations")
+    if out is None:
+        f = 2 if transposed else 1
+        out = torch.empty((a.B, f * Dout, f * Hout, f * Wout, Cout), dtype=dt, device=srcs[0].t.device)
+        if transposed:
+            out_os = 2
+    if out.dtype != dt or not out.is_contiguous() or out.dim() != 5:
+        raise RuntimeError("nps_hip conv3d: out must be contiguous NDHWC of the sources' dtype")
+    if addend is not None and (addend.shape != out.shape or addend.dtype != dt or not addend.is_contiguous()):
+        raise RuntimeError("nps_hip conv3d: addend must be laid out like out")
+    a.circ, a.zpad = circ, zpad
+    if gn is not None:
+        a.gn_stats, a.gn_gamma, a.gn_beta = ptr(gn.stats), ptr(gn.gamma), ptr(gn.beta)
+        a.gn_groups, a.gn_eps = gn.groups, gn.eps
+    a.pre_act = pre_act
+    a.K, a.stride, a.transposed = K, stride, 1 if transposed else 0
+    a.Dout, a.Hout, a.Wout = Dout, Hout, Wout
+    a.wpack, a.bias, a.Cout = ptr(wpack), ptr(bias), Cout
+    a.out, a.out_C, a.out_D, a.out_H, a.out_W = ptr(out), out.shape[4], out.shape[1], out.shape[2], out.shape[3]
+    a.out_os, (a.out_off_d, a.out_off_h, a.out_off_w) = out_os, out_off
+    a.accumulate, a.addend, a.act = 1 if accumulate else 0, ptr(addend), act
+    if conv_probe is not None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        check(lib.nps_conv3d_fwd(ctypes_byref(a), stream_ptr()), "conv3d")
+        e1.record()
+        nph = 8 if transposed else 1
+        es = 2 if a.bf16 else 4
+        nbytes = es * (sum(s.t.numel() for s in srcs) + nph * Cout * a.Cin * K ** 3 + nph * a.B * Dout * Hout * Wout * Cout)
+        conv_probe.append((e0, e1, 2.0 * nph * a.B * Dout * Hout * Wout * Cout * a.Cin * K ** 3,
+                           ("bf16_3d" if a.bf16 else "f32_3d", K ** 3, 4), nbytes))
+    else:
+        check(lib.nps_conv3d_fwd(ctypes_byref(a), stream_ptr()), "conv3d")
     return out
 
 

@@ -14,7 +14,8 @@ __all__ = [
     "crop_nd", "conv2d_ref", "conv_transpose_ref", "spectral_conv2d", "spectral_conv3d", "fno_layer", "fno",
     "fno_layer3d", "fno3d",
     "residual_block", "unet_modern", "dilated_resnet", "ufno", "enc_elementwise", "add_delta",
-    "dec_timeconvdense", "unet_structure",
+    "dec_timeconvdense", "unet_structure", "conv3d_ref", "upsample3d_ref", "residual_block3d", "unet_modern3d",
+    "ufno3d",
 ]
 
 
@@ -252,6 +253,106 @@ def ufno(sd, p, cfg, h, vb):
         h_fno = fno_layer(sd, _j(p, f"fno_layers.{i}"), h_in, activation=False,
                           padding_mode=pm if pm != "ones" else "zeros", conv_mode=cfg.get("fno_conv_mode", "single"))
         h_unet = unet_modern(sd, _j(p, f"unet_layers.{i}"), ucfg, h, vb)
+        h = gelu(h_fno + h_unet)
+    return h
+
+
+# ------------------------------------------------------ 3-D U-Net / U-FNO ----
+# UNetModern / UFNO with num_spatial_dims=3 (BASELINE config C5).  Everything but the Upsample follows the
+# reference's own 3-D modules (get_conv_with_right_spatial_dim(3) = nn.Conv3d, common.py:37-47; GroupNorm,
+# crop_Nd are dimension-generic) and is pinned by tests/golden/make_golden_3d.py's single-resolution 3-D
+# U-Net / U-FNO fixtures.  The reference has NO 3-D Upsample (common.py:103-120 raises): upsample3d_ref is
+# this build's definition — the 2-D rule (circular_pad_2d then ConvTranspose2d(k=4, s=2, p=0),
+# common.py:61-100) applied per axis — so multi-resolution 3-D U-Nets are PARITY UNPINNED beyond it.
+def conv3d_ref(x, sd, p, stride=1, padding=0, padding_mode="zeros"):
+    """nn.Conv3d as get_conv_with_right_spatial_dim(3, ...) builds it (cubic kernel, no dilation)."""
+    w = sd[_j(p, "weight")]
+    b = sd.get(_j(p, "bias"))
+    if padding_mode != "zeros":
+        if padding == "same":
+            k = w.shape[-1]
+            lo = (k - 1) // 2
+            pads = (lo, k - 1 - lo) * 3
+        else:
+            pads = (padding,) * 6
+        if any(pads):
+            x = F.pad(x, pads, mode="circular")
+        return F.conv3d(x, w, b, stride=stride)
+    return F.conv3d(x, w, b, stride=stride, padding=padding)
+
+
+def upsample3d_ref(x, sd, p):
+    """This build's 3-D Upsample: circular pad 1 on D, H and W, then ConvTranspose3d(k=4, s=2, p=0)."""
+    x = F.pad(x, (1, 1, 1, 1, 1, 1), mode="circular")
+    return F.conv_transpose3d(x, sd[_j(p, "weight")], sd.get(_j(p, "bias")), stride=2)
+
+
+def residual_block3d(sd, p, x, norm, pad_kw):
+    """ResidualBlock.forward with Conv3d, proc_unet_modern.py:243-250."""
+    h = x
+    if norm:
+        h = F.group_norm(h, 1, sd[_j(p, "norm1.weight")], sd[_j(p, "norm1.bias")], 1e-5)
+    h = conv3d_ref(gelu(h), sd, _j(p, "conv1"), **pad_kw)
+    if norm:
+        h = F.group_norm(h, 1, sd[_j(p, "norm2.weight")], sd[_j(p, "norm2.bias")], 1e-5)
+    h = conv3d_ref(gelu(h), sd, _j(p, "conv2"), **pad_kw)
+    sc = conv3d_ref(x, sd, _j(p, "shortcut")) if _j(p, "shortcut.weight") in sd else x
+    return crop_nd(h, sc.shape, 3) + sc
+
+
+def unet_modern3d(sd, p, cfg, h, vb):
+    """UNetModern.forward with num_spatial_dims=3, proc_unet_modern.py:169-196 (cond_mode='concat')."""
+    pmode = cfg.get("padding_mode", "ones")
+    pad_kw = dict(padding=1) if pmode == "ones" else dict(padding_mode="circular")
+    if pmode != "circular":
+        raise NotImplementedError("3-D Upsample is defined for padding_mode='circular' only")
+    norm = cfg.get("norm", False)
+    n_cond = cfg.get("n_cond", 0) if cfg.get("cond_mode", "concat") is not None else 0
+    down, _, up = unet_structure(cfg.get("hidden_features", 128), cfg.get("ch_mults", (1, 2, 2, 4)),
+                                 cfg.get("n_blocks", 2), n_cond)
+    h_shape = h.shape
+    feats, vbs = [h], [vb]
+    for i, m in enumerate(down):
+        q = _j(p, f"down.{i}")
+        if m[0] == "down":
+            x = torch.cat([h, vb], dim=1) if vb is not None else h
+            h = residual_block3d(sd, _j(q, "res"), x, norm, pad_kw)
+        else:
+            h = conv3d_ref(h, sd, _j(q, "conv"), stride=2, **pad_kw)
+            if vb is not None:
+                vb = conv3d_ref(vb, sd, _j(q, "conv_variables_broadcast"), stride=2, **pad_kw)
+        feats.append(h)
+        vbs.append(vb)
+    x = torch.cat([h, vb], dim=1) if vb is not None else h
+    h = residual_block3d(sd, _j(p, "middle.res1"), x, norm, pad_kw)
+    h = residual_block3d(sd, _j(p, "middle.res2"), h, norm, pad_kw)
+    for i, m in enumerate(up):
+        q = _j(p, f"up.{i}")
+        if m[0] == "upsample":
+            h = upsample3d_ref(h, sd, _j(q, "conv"))
+        else:
+            s = crop_nd(feats.pop(), h.shape, 3)
+            v = crop_nd(vbs.pop(), h.shape, 3) if vbs[-1] is not None else vbs.pop()
+            x = torch.cat((h, s, v), dim=1) if v is not None else torch.cat((h, s), dim=1)
+            h = residual_block3d(sd, _j(q, "res"), x, norm, pad_kw)
+    if norm:
+        h = F.group_norm(h, 8, sd[_j(p, "norm.weight")], sd[_j(p, "norm.bias")], 1e-5)
+    h = gelu(h)
+    h = conv3d_ref(h, sd, _j(p, "final")) if cfg.get("use1x1", False) else conv3d_ref(h, sd, _j(p, "final"), **pad_kw)
+    return crop_nd(h, h_shape, 3)
+
+
+def ufno3d(sd, p, cfg, h, vb):
+    """UFNO.forward with num_spatial_dims=3, proc_ufno.py:105-118 (cond_mode='concat', FNO `w` 1x1x1)."""
+    ucfg = dict(cfg)
+    ucfg.setdefault("ch_mults", (1, 1, 1))
+    ucfg.setdefault("n_blocks", 1)
+    ucfg.setdefault("use1x1", True)
+    ucfg["padding_mode"] = cfg.get("padding_mode", "circular")
+    for i in range(cfg.get("hidden_blocks", 4)):
+        h_in = torch.cat([h, vb], dim=1) if vb is not None else h
+        h_fno = fno_layer3d(sd, _j(p, f"fno_layers.{i}"), h_in, activation=False)
+        h_unet = unet_modern3d(sd, _j(p, f"unet_layers.{i}"), ucfg, h, vb)
         h = gelu(h_fno + h_unet)
     return h
 

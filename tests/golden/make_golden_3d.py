@@ -1,4 +1,6 @@
-"""Generate the 3-D golden fixtures (SpectralConv3d with corner overlaps + grads, FNO-3D processor).
+"""Generate the 3-D golden fixtures (SpectralConv3d with corner overlaps + grads, FNO-3D processor, and the
+3-D U-Net / U-FNO pieces the reference can build: a single-resolution 3-D UNetModern and U-FNO — the
+reference has no 3-D Upsample, common.py:103-120 — and the 3-D Downsample on its own).
 
 CONTAINER-ONLY TOOL, same contract as make_golden.py (imports the reference from /root/reference with
 the two unused import-time dependencies stubbed; only the written tensors travel):
@@ -21,6 +23,8 @@ def main():
     import torch
     torch.set_num_threads(8)
     from models.enc_proc_dec_components.proc_fno import SpectralConv3d, FNO
+    from models.enc_proc_dec_components.proc_unet_modern import UNetModern, Downsample
+    from models.enc_proc_dec_components.proc_ufno import UFNO
 
     def save(name, **payload):
         path = os.path.join(OUT_DIR, f"{name}.pt")
@@ -60,6 +64,30 @@ def main():
     y.backward(g)
     save("fno3d", kwargs=dict(kw, fno_modes=list(kw["fno_modes"])), state_dict=m.state_dict(), h=h.detach(), vb=vb,
          y=y.detach(), g=g, dh=h.grad)
+
+    # 3-D U-Net, single resolution (no Up/Downsample): ResidualBlocks of Conv3d, GroupNorm, crop_Nd, the
+    # concat of h / skip / conditioning, the final GroupNorm(8) + 1x1x1 conv — proc_unet_modern.py:24-250
+    with torch.no_grad():
+        torch.manual_seed(42)
+        kw = dict(num_spatial_dims=3, n_cond=2, hidden_features=8, cond_mode="concat", norm=True, ch_mults=[1],
+                  is_attn=[False], mid_attn=False, n_blocks=1, use1x1=True, padding_mode="circular")
+        m = UNetModern(pde=None, **kw)
+        h, vb = rnd(2, 8, 9, 10, 12), rnd(2, 2, 9, 10, 12, lo=0.0)
+        save("unet3d_single", kwargs=kw, state_dict=m.state_dict(), h=h, vb=vb, y=m(h, variables_broadcast=vb))
+        # 3-D Downsample (valid 3x3x3 stride-2 conv on h and on the conditioning), proc_unet_modern.py:439-455
+        torch.manual_seed(42)
+        m = Downsample(8, num_spatial_dims=3, n_cond=2, padding_kwargs=dict(padding_mode="circular"))
+        yh, yv = m(h, variables_broadcast=vb)
+        save("downsample3d", state_dict=m.state_dict(), h=h, vb=vb, yh=yh, yv=yv)
+        # 3-D U-FNO, single-resolution U-Nets (proc_ufno.py:25-118 with num_spatial_dims=3)
+        torch.manual_seed(42)
+        kw = dict(num_spatial_dims=3, n_cond=2, hidden_features=8, hidden_blocks=2, cond_mode="concat",
+                  padding_mode="circular", fno_modes=(3, 4, 3), fno_kernel_size=1, fno_conv_mode="single", norm=True,
+                  ch_mults=[1], is_attn=[False], mid_attn=False, n_blocks=1, use1x1=True)
+        m = UFNO(pde=None, **kw)
+        h, vb = rnd(2, 8, 8, 10, 12), rnd(2, 2, 8, 10, 12, lo=0.0)
+        save("ufno3d_single", kwargs=dict(kw, fno_modes=list(kw["fno_modes"])), state_dict=m.state_dict(), h=h,
+             vb=vb, y=m(h, variables_broadcast=vb))
 
 
 if __name__ == "__main__":

@@ -23,16 +23,22 @@ def test_library_exports_every_declared_symbol():
     assert nps_hip.lib.nps_version().startswith(b"nps_hip")
 
 
-def test_struct_layout_matches_header():
+import pytest
+
+
+@pytest.mark.parametrize("cstruct,pyname,srcname,pysrc", [("nps_conv2d_t", "Conv2dArgs", "nps_src_t", "Src"),
+                                                         ("nps_conv3d_t", "Conv3dArgs", "nps_src3_t", "Src3")])
+def test_struct_layout_matches_header(cstruct, pyname, srcname, pysrc):
     """ctypes mirror vs a C compile of the header (offsetof / sizeof)."""
     import subprocess
     import tempfile
     import nps_hip
-    fields = [f for f, _ in nps_hip.Conv2dArgs._fields_]
+    Args, SrcT = getattr(nps_hip, pyname), getattr(nps_hip, pysrc)
+    fields = [f for f, _ in Args._fields_]
     prog = "#include <stdio.h>\n#include <stddef.h>\n#include \"nps.h\"\nint main(){\n"
-    prog += 'printf("%zu %zu\\n", sizeof(nps_conv2d_t), sizeof(nps_src_t));\n'
+    prog += f'printf("%zu %zu\\n", sizeof({cstruct}), sizeof({srcname}));\n'
     for f in fields:
-        prog += f'printf("%zu\\n", offsetof(nps_conv2d_t, {f}));\n'
+        prog += f'printf("%zu\\n", offsetof({cstruct}, {f}));\n'
     prog += "return 0;}\n"
     with tempfile.TemporaryDirectory() as d:
         c = os.path.join(d, "t.c")
@@ -40,10 +46,10 @@ def test_struct_layout_matches_header():
         exe = os.path.join(d, "t")
         subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o", exe], check=True)
         out = subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()
-    assert int(out[0]) == ctypes.sizeof(nps_hip.Conv2dArgs)
-    assert int(out[1]) == ctypes.sizeof(nps_hip.Src)
+    assert int(out[0]) == ctypes.sizeof(Args)
+    assert int(out[1]) == ctypes.sizeof(SrcT)
     for f, off in zip(fields, out[2:]):
-        assert getattr(nps_hip.Conv2dArgs, f).offset == int(off), f
+        assert getattr(Args, f).offset == int(off), f
 
 
 def test_ops_refuse_cpu_tensors():

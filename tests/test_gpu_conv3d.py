@@ -1,0 +1,145 @@
+"""nps_conv3d (csrc/conv3d.hip): the 3-D U-Net convolutions of the 3-D U-FNO (BASELINE config C5) against
+torch fp64 references of the same ops — nn.Conv3d valid / stride 2 (proc_unet_modern.py:222-227, :445-449),
+the GroupNorm + GELU prologue on a torch.cat / crop_Nd frame (:245-247, :188-191), the 1x1 shortcut / final
+conv, the residual accumulate at the crop offset (:250), and this build's 3-D Upsample (circular pad 1 +
+ConvTranspose3d(k=4, s=2), DESIGN.md "3-D U-FNO").  fp32 storage runs on exact-fp32 MFMA (tolerance: rel-L2
+< 1e-5); bf16 storage is compared with the fp64 op on the same bf16-rounded operands (rel-L2 < 1e-2)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import rel_l2
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+TOL = {torch.float32: 1e-5, torch.bfloat16: 1e-2}
+DTYPES = [torch.float32, torch.bfloat16]
+
+
+def _ndhwc(x, dt):
+    return x.permute(0, 2, 3, 4, 1).contiguous().to(DEV, dt)
+
+
+def _ncdhw(y):
+    return y.float().cpu().permute(0, 4, 1, 2, 3).double()
+
+
+def _frame(srcs, B, dhw):
+    """torch.cat of crop_Nd-placed sources (NCDHW fp64)."""
+    C = sum(s.shape[1] for s, _ in srcs)
+    fr = torch.zeros(B, C, *dhw, dtype=torch.float64)
+    c = 0
+    for s, off in srcs:
+        D, H, W = s.shape[2:]
+        lo = [max(0, o) for o in off]
+        hi = [min(n, o + m) for n, o, m in zip(dhw, off, (D, H, W))]
+        if all(h > l for l, h in zip(lo, hi)):
+            fr[:, c:c + s.shape[1], lo[0]:hi[0], lo[1]:hi[1], lo[2]:hi[2]] = \
+                s[:, :, lo[0] - off[0]:hi[0] - off[0], lo[1] - off[1]:hi[1] - off[1], lo[2] - off[2]:hi[2] - off[2]]
+        c += s.shape[1]
+    return fr
+
+
+def _rt(x, dt):
+    """the operand as the kernel sees it (bf16-rounded for bf16 storage)."""
+    return x.to(dt).double() if dt == torch.bfloat16 else x.double()
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("K,stride,shape", [(3, 1, (2, 9, 20, 40)), (3, 2, (2, 9, 19, 37)), (1, 1, (1, 5, 7, 33))])
+def test_conv3d_valid(dt, K, stride, shape):
+    from nps_hip import ops
+    torch.manual_seed(0)
+    B, D, H, W = shape
+    x1, x2 = torch.randn(B, 64, D, H, W), torch.randn(B, 4, D, H, W)
+    w = torch.randn(48, 68, K, K, K) * 0.05
+    b = torch.randn(48) * 0.1
+    ref = F.conv3d(torch.cat([_rt(x1, dt), _rt(x2, dt)], 1), _rt(w, dt), b.double(), stride=stride)
+    wp = ops.pack_conv3d_weight(w.to(DEV), bf16=dt == torch.bfloat16)
+    y = ops.conv3d([ops.Src3(_ndhwc(x1, dt)), ops.Src3(_ndhwc(x2, dt))], (D, H, W), wp, b.to(DEV), 48, K,
+                   stride=stride)
+    assert rel_l2(_ncdhw(y), ref) < TOL[dt]
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+def test_conv3d_gn_prologue_on_crop_frame(dt):
+    """UpBlock shape: cat(h, crop_Nd(skip), crop_Nd(vb)) -> GroupNorm(1) -> GELU -> 3x3x3 valid conv; the
+    skip is cropped on one axis and zero-padded on another, so the frame has uncovered (zero) voxels that
+    the GroupNorm counts and normalises."""
+    from nps_hip import ops
+    torch.manual_seed(1)
+    B, dhw = 2, (8, 12, 36)
+    h = torch.randn(B, 32, *dhw)
+    s = torch.randn(B, 32, 10, 10, 36) * 2 + 0.5
+    v = torch.rand(B, 4, 6, 12, 36)
+    offs = [(0, 0, 0), (-1, 1, 0), (1, 0, 0)]
+    gamma, beta = 1 + 0.2 * torch.randn(68), 0.1 * torch.randn(68)
+    fr = _frame([(_rt(h, dt), offs[0]), (_rt(s, dt), offs[1]), (_rt(v, dt), offs[2])], B, dhw)
+    n = F.gelu(F.group_norm(fr, 1, gamma.double(), beta.double(), eps=1e-5))
+    w = torch.randn(40, 68, 3, 3, 3) * 0.05
+    ref = F.conv3d(_rt(n, dt), _rt(w, dt))
+    srcs = [ops.Src3(_ndhwc(t, dt), *o) for t, o in zip((h, s, v), offs)]
+    st = ops.gn_stats3d(srcs, dhw, 1)
+    # (per-voxel channel runs are summed in fp32, the runs in fp64)
+    torch.testing.assert_close(st[:, 0, 0].cpu(), fr.sum((1, 2, 3, 4)), rtol=1e-6, atol=1e-3)
+    torch.testing.assert_close(st[:, 0, 1].cpu(), (fr ** 2).sum((1, 2, 3, 4)), rtol=1e-6, atol=1e-3)
+    gn = ops.GN(st, gamma.to(DEV), beta.to(DEV), 1, 1e-5)
+    wp = ops.pack_conv3d_weight(w.to(DEV), bf16=dt == torch.bfloat16)
+    y = ops.conv3d(srcs, dhw, wp, None, 40, 3, gn=gn, pre_act=1)
+    # bf16: the kernel rounds the normalised frame to bf16 once more (as the LDS image) — the reference does too
+    assert rel_l2(_ncdhw(y), ref) < TOL[dt]
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+def test_conv3d_residual_accumulate_and_final_crop(dt):
+    """ResidualBlock tail: conv2 accumulated at crop offset (2, 2, 2) into the 1x1 shortcut output; and the
+    U-Net final GroupNorm(8) + GELU + 1x1 conv written at a negative crop offset with addend + GELU
+    (GELU(h_fno + h_unet), proc_ufno.py:118)."""
+    from nps_hip import ops
+    torch.manual_seed(2)
+    B, dhw = 1, (9, 14, 40)
+    x = torch.randn(B, 24, *dhw)
+    ws, bs = torch.randn(32, 24, 1, 1, 1) * 0.2, torch.randn(32) * 0.1
+    w2, b2 = torch.randn(32, 24, 3, 3, 3) * 0.05, torch.randn(32) * 0.1
+    sc = F.conv3d(_rt(x, dt), _rt(ws, dt), bs.double())
+    h = F.conv3d(_rt(x, dt), _rt(w2, dt), b2.double())
+    ref = sc.clone()
+    ref[:, :, 1:-1, 1:-1, 1:-1] += h  # crop_Nd(h, shortcut) + shortcut (valid 3^3 conv: offset 1 here)
+    xd = _ndhwc(x, dt)
+    out = ops.conv3d([ops.Src3(xd)], dhw, ops.pack_conv3d_weight(ws.to(DEV), bf16=dt == torch.bfloat16), bs.to(DEV),
+                     32, 1)
+    ops.conv3d([ops.Src3(xd)], dhw, ops.pack_conv3d_weight(w2.to(DEV), bf16=dt == torch.bfloat16), b2.to(DEV), 32, 3,
+               out=out, out_off=(1, 1, 1), accumulate=True)
+    assert rel_l2(_ncdhw(out), ref) < TOL[dt]
+    # final: GN(8) -> GELU -> 1x1 -> crop to (7, 12, 36) at offset -1, -1, -2, + addend, GELU
+    gamma, beta = 1 + 0.1 * torch.randn(32), 0.1 * torch.randn(32)
+    wf, bf = torch.randn(32, 32, 1, 1, 1) * 0.2, torch.randn(32) * 0.1
+    r = _rt(ref, dt) if dt == torch.bfloat16 else ref
+    fin = F.conv3d(_rt(F.gelu(F.group_norm(r, 8, gamma.double(), beta.double(), eps=1e-5)), dt), _rt(wf, dt),
+                   bf.double())[:, :, 1:8, 1:13, 2:38]
+    addend = torch.randn(B, 32, 7, 12, 36)
+    want = F.gelu(fin + _rt(addend, dt))
+    st = ops.gn_stats3d([ops.Src3(out)], dhw, 8)
+    o2 = torch.empty(B, 7, 12, 36, 32, dtype=dt, device=DEV)
+    ops.conv3d([ops.Src3(out)], dhw, ops.pack_conv3d_weight(wf.to(DEV), bf16=dt == torch.bfloat16), bf.to(DEV), 32,
+               1, gn=ops.GN(st, gamma.to(DEV), beta.to(DEV), 8, 1e-5), pre_act=1, out=o2, out_off=(-1, -1, -2),
+               addend=_ndhwc(addend, dt), act=1)
+    assert rel_l2(_ncdhw(o2), want) < TOL[dt]
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("shape", [(2, 5, 7, 20), (1, 4, 16, 33)])
+def test_conv3d_upsample_transposed(dt, shape):
+    """3-D Upsample: circular pad 1 on every axis, then ConvTranspose3d(k=4, s=2, p=0) — 8 phase convs."""
+    from nps_hip import ops
+    torch.manual_seed(3)
+    B, D, H, W = shape
+    x = torch.randn(B, 48, D, H, W)
+    w, b = torch.randn(48, 40, 4, 4, 4) * 0.05, torch.randn(40) * 0.1
+    xp = F.pad(_rt(x, dt), (1, 1, 1, 1, 1, 1), mode="circular")
+    ref = F.conv_transpose3d(xp, _rt(w, dt), b.double(), stride=2)
+    assert ref.shape[2:] == (2 * D + 6, 2 * H + 6, 2 * W + 6)
+    wp = ops.pack_conv3d_weight(w.to(DEV), transposed=True, bf16=dt == torch.bfloat16)
+    y = ops.conv3d([ops.Src3(_ndhwc(x, dt))], (D, H, W), wp, b.to(DEV), 40, 2, transposed=True, circ=1, zpad=1)
+    assert y.shape[1:4] == ref.shape[2:]
+    assert rel_l2(_ncdhw(y), ref) < TOL[dt]

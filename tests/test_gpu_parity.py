@@ -311,3 +311,44 @@ def test_ufno_c3_full_size_one_call():
     ref = oracle.build_oracle_model(ocfg, opde, {k: v.cpu() for k, v in m.state_dict().items()})(
         u, cond=cond, pos=pos, spatial_cond=sc)
     assert rel_l2(y, ref) < TOL
+
+
+def test_c1_unet_cfg_simulate_golden():
+    """BASELINE C1: the exact cfg_twophase_unet model (hidden 32, ch_mults [2,2,1,2]), 64x64, no obstacle,
+    B=2, t_res=150 — the 5-call rollout through the mirror's simulate on the GPU against the reference's
+    own simulate (tests/golden/make_golden_c1.py), every window and every loss."""
+    import argparse
+    import types
+    from common.interfaces import D
+    from trainers.autoregressivepushforwardtrainer import AutoregressivePushforwardTrainer
+    from c1_fixture import c1_golden, c1_inputs, c1_model
+    g = c1_golden()
+    u, cond, pos, sc = (t.to(DEV) for t in c1_inputs(g))
+    m, pde = c1_model(g)
+    m = m.to(DEV)
+    tw, T = g["cfg"]["time_window"], u.shape[2]
+    cfg = argparse.Namespace(time_window=tw, base_resolution=(T, u.shape[3], u.shape[4]), device=DEV, nr_gt_steps=1)
+    tr = AutoregressivePushforwardTrainer(model=m, data=types.SimpleNamespace(pde=pde, data_interface=D.sim2d),
+                                          criterion=nn.MSELoss(reduction="sum"), config=cfg)
+    with torch.no_grad():
+        losses, (gt, preds) = tr.simulate(u, cond, pos, compute_loss=True, include_data=True, nr_gt_steps=1, t_res=T,
+                                          spatial_conditioning=sc)
+    assert len(preds) == 6
+    for k in range(5):  # every window of the rollout (errors would compound through the feedback)
+        assert rel_l2(preds[k + 1].cpu(), g["sim_pred"][:, :, k * tw:(k + 1) * tw]) < TOL, k
+    assert rel_l2(torch.stack([l.cpu() for l in losses]), g["sim_losses"]) < TOL
+
+
+def test_ufno_c2_full_size_one_call():
+    """BASELINE C2: U-FNO twophase cfg with 12 Fourier modes (hidden 192, 3 blocks) at 128x128, 1 field,
+    B=2 — one rollout model call vs the CPU oracle (cf. test_ufno_c3_full_size_one_call)."""
+    import __graft_entry__  # noqa: F401
+    from bench import build_model
+    from trainers.synthetic import twophase_batch
+    m, ocfg, opde = build_model("ufno", res=128, num_c=1, device=DEV, fno_modes=12)
+    u, cond, pos, sc = twophase_batch(2, 1, 25, 128, 128, seed=11, obstacle="random")
+    with torch.no_grad():
+        y = m(u.to(DEV), cond=cond.to(DEV), bc=None, pos=pos.to(DEV), t_cond=None, spatial_cond=sc.to(DEV)).cpu()
+    ref = oracle.build_oracle_model(ocfg, opde, {k: v.cpu() for k, v in m.state_dict().items()})(
+        u, cond=cond, pos=pos, spatial_cond=sc)
+    assert rel_l2(y, ref) < TOL

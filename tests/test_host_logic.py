@@ -107,11 +107,37 @@ def test_fno3d_construction_matches_reference_seeded_init():
         assert torch.equal(sd[k], v), k
 
 
-def test_3d_ufno_unconstructible_as_reference():
-    """The reference's U-FNO / UNetModern with num_spatial_dims=3 and two or more U-Net resolutions fail at
-    construction (its Upsample has no 3-D form: src/models/common.py:103-120); the mirror fails the same way,
-    so a cfg behaves identically (C5 runs the FNO-3D processor)."""
+@pytest.mark.parametrize("name,cls", [("unet3d_single", "UNetModern"), ("ufno3d_single", "UFNO")])
+def test_3d_unet_ufno_construction_matches_reference_seeded_init(name, cls):
+    """The 3-D U-Net / U-FNO the reference can build (single U-Net resolution) get its parameters bit for bit."""
+    import torch
+    from conftest import load_golden
+    import models.enc_proc_dec_components as comps
+    g = load_golden(name)
+    kw = dict(g["kwargs"])
+    if "fno_modes" in kw:
+        kw["fno_modes"] = tuple(kw["fno_modes"])
+    torch.manual_seed(42)
+    m = getattr(comps, cls)(pde=None, **kw)
+    sd = m.state_dict()
+    assert list(sd) == list(g["state_dict"])
+    for k, v in g["state_dict"].items():
+        assert torch.equal(sd[k], v), k
+
+
+def test_3d_ufno_multires_defines_the_upsample():
+    """With two or more U-Net resolutions the reference's 3-D U-FNO fails at construction (no 3-D Upsample,
+    src/models/common.py:103-120).  BASELINE config C5 needs one, so the mirror DEFINES it (DESIGN.md
+    "3-D U-FNO"): circular pad 1 + ConvTranspose3d(k=4, s=2, p=0), the 2-D rule per axis, parameters named
+    like the 2-D Upsample's (up.{i}.conv.weight / .bias of shape (C, C, 4, 4, 4)).  Other padding modes
+    still raise as in the reference."""
+    from models.common import ConvTranspose3d_padded
     from models.enc_proc_dec_components.proc_ufno import UFNO
+    m = UFNO(pde=None, num_spatial_dims=3, n_cond=4, hidden_features=16, hidden_blocks=1, fno_modes=(4, 4, 4),
+             ch_mults=(1, 1), is_attn=(False, False), norm=True)
+    up = [u for u in m.unet_layers[0].up if type(u).__name__ == "Upsample"]
+    assert len(up) == 1 and isinstance(up[0].conv, ConvTranspose3d_padded) and up[0].conv.pad == 1
+    assert tuple(up[0].conv.weight.shape) == (16, 16, 4, 4, 4) and tuple(up[0].conv.stride) == (2, 2, 2)
     with pytest.raises(NotImplementedError, match="spatial dim 3"):
         UFNO(pde=None, num_spatial_dims=3, n_cond=4, hidden_features=16, hidden_blocks=1, fno_modes=(4, 4, 4),
-             ch_mults=(1, 1), is_attn=(False, False), norm=True)
+             ch_mults=(1, 1), is_attn=(False, False), norm=True, padding_mode="ones")
