@@ -48,7 +48,9 @@ def _worker(rank, world, init_file, bucket_bytes, overlap, q):
         m.zero_grad()
         m(x[rank * 4:(rank + 1) * 4]).backward()
         sync.finish()
-    q.put((rank, {k: p.grad.clone() for k, p in m.named_parameters()}, len(sync.buckets)))
+    # numpy copies travel by value: torch tensors would go through a file-descriptor server that dies with
+    # this process, racing the parent's unpickling (the round-2 flake)
+    q.put((rank, {k: p.grad.clone().numpy() for k, p in m.named_parameters()}, len(sync.buckets)))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -81,7 +83,7 @@ def test_grad_allreduce_matches_full_batch(bucket_bytes, overlap):
         if bucket_bytes == 64:
             assert nb > 1
         for k in want:
-            torch.testing.assert_close(got[k], want[k], rtol=1e-6, atol=1e-6)
+            torch.testing.assert_close(torch.from_numpy(got[k]), want[k], rtol=1e-6, atol=1e-6)
 
 
 # ----------------------------------------------------------------- model-shaped all-reduce, shards, bench
