@@ -338,6 +338,24 @@ __global__ __launch_bounds__(256) void conv3d_kernel(const nps_conv3d_t a, int n
                         for (int e = 0; e < 4; ++e) o[e] = nps::gelu_erf(o[e]);
                     if (a.accumulate) o += *reinterpret_cast<const f32x4*>(op);
                     *reinterpret_cast<f32x4*>(op) = o;
+                } else if (vec4) {  // bf16: 4 channels = one 8-B access
+                    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+                    float o[4] = {v[0], v[1], v[2], v[3]};
+                    if (ap) {
+                        const u32x2 w = *reinterpret_cast<const u32x2*>(ap);
+                        o[0] += bf2f(w[0] & 0xffffu); o[1] += bf2f(w[0] >> 16);
+                        o[2] += bf2f(w[1] & 0xffffu); o[3] += bf2f(w[1] >> 16);
+                    }
+                    if (a.act == 1)
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) o[e] = nps::gelu_erf(o[e]);
+                    if (a.accumulate) {
+                        const u32x2 w = *reinterpret_cast<const u32x2*>(op);
+                        o[0] += bf2f(w[0] & 0xffffu); o[1] += bf2f(w[0] >> 16);
+                        o[2] += bf2f(w[1] & 0xffffu); o[3] += bf2f(w[1] >> 16);
+                    }
+                    const u32x2 r = {f2bf(o[0]) | (f2bf(o[1]) << 16), f2bf(o[2]) | (f2bf(o[3]) << 16)};
+                    *reinterpret_cast<u32x2*>(op) = r;
                 } else {
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
@@ -381,46 +399,76 @@ __global__ void conv3d_pack_kernel(const float* __restrict__ w, T* __restrict__ 
     }
 }
 
-// per (b, group) fp64 (sum, sum of squares) of a core frame; one thread per voxel, groups in registers
+// per (b, group) fp64 (sum, sum of squares) of a core frame.  Each source is swept over its own voxels
+// (those inside the frame), one work item = 8 consecutive channels of one voxel, so consecutive threads read
+// consecutive 16-B (bf16) / 32-B (fp32) pieces; per-thread group sums in registers, one block reduction.
 template <typename T>
 __global__ __launch_bounds__(256) void gn_stats3d_kernel(const nps_conv3d_t a, int G, double* __restrict__ stats) {
     __shared__ double scratch[4];
     const int b = blockIdx.y;
-    const long nvox = (long)a.Dc * a.Hc * a.Wc;
     const int cpg = a.Cin / G;
     double s[8], q[8];
 #pragma unroll
     for (int g = 0; g < 8; ++g) s[g] = q[g] = 0.0;
-    for (long v = (long)blockIdx.x * 256 + threadIdx.x; v < nvox; v += (long)gridDim.x * 256) {
-        const int cw = (int)(v % a.Wc);
-        const long r = v / a.Wc;
-        const int ch = (int)(r % a.Hc), cd = (int)(r / a.Hc);
-        int lo = 0;
+    int lo = 0;
 #pragma unroll
-        for (int si = 0; si < NPS_MAX_SRC; ++si) {
-            if (si < a.nsrc) {
-                const nps_src3_t& src = a.src[si];
-                const int dd = cd - src.off_d, hh = ch - src.off_h, ww = cw - src.off_w;
-                if (dd >= 0 && dd < src.D && hh >= 0 && hh < src.H && ww >= 0 && ww < src.W) {
-                    const T* p = reinterpret_cast<const T*>(src.ptr) +
-                                 ((((size_t)b * src.D + dd) * src.H + hh) * src.W + ww) * src.C;
+    for (int si = 0; si < NPS_MAX_SRC; ++si) {
+        if (si < a.nsrc) {
+            const nps_src3_t& src = a.src[si];
+            const int nck = (src.C + 7) / 8;
+            const long nitem = (long)src.D * src.H * src.W * nck;
+            const T* base = reinterpret_cast<const T*>(src.ptr) + (size_t)b * src.D * src.H * src.W * src.C;
+            const bool vec = (src.C & 7) == 0;
+            for (long it = (long)blockIdx.x * 256 + threadIdx.x; it < nitem; it += (long)gridDim.x * 256) {
+                const int ck = (int)(it % nck);
+                const long vox = it / nck;
+                const int ww = (int)(vox % src.W);
+                const long r = vox / src.W;
+                const int hh = (int)(r % src.H), dd = (int)(r / src.H);
+                const int cd = dd + src.off_d, ch = hh + src.off_h, cw = ww + src.off_w;
+                if (cd < 0 || cd >= a.Dc || ch < 0 || ch >= a.Hc || cw < 0 || cw >= a.Wc) continue;
+                const T* p = base + (size_t)vox * src.C + ck * 8;
+                Vec8<T> v;
+                v.zero();
+                if (vec) {
+                    v.load(p);
+                } else {
 #pragma unroll
-                    for (int g = 0; g < 8; ++g) {
-                        if (g < G) {
-                            const int c1 = max(g * cpg, lo) - lo, c2 = min((g + 1) * cpg, lo + src.C) - lo;
-                            float fs = 0.f, fq = 0.f;
-                            for (int c = c1; c < c2; ++c) {
-                                const float x = ld1<T>(p + c);
-                                fs += x;
-                                fq = fmaf(x, x, fq);
-                            }
+                    for (int e = 0; e < 8; ++e)
+                        if (ck * 8 + e < src.C) v.load_elem(e, p + e);
+                }
+                const int c0 = lo + ck * 8;
+                if (vec && (cpg & 7) == 0) {  // the 8 channels lie in one group
+                    const int g0 = c0 / cpg;
+                    float fs = 0.f, fq = 0.f;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        const float x = v.get(e);
+                        fs += x;
+                        fq = fmaf(x, x, fq);
+                    }
+#pragma unroll
+                    for (int g = 0; g < 8; ++g)
+                        if (g == g0) {
                             s[g] += fs;
                             q[g] += fq;
                         }
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        if (ck * 8 + e >= src.C) continue;
+                        const float x = v.get(e);
+                        const int ge = (c0 + e) / cpg;
+#pragma unroll
+                        for (int g = 0; g < 8; ++g)
+                            if (g == ge) {
+                                s[g] += x;
+                                q[g] += (double)x * x;
+                            }
                     }
                 }
-                lo += src.C;
             }
+            lo += src.C;
         }
     }
 #pragma unroll
@@ -530,8 +578,10 @@ extern "C" int nps_gn_stats3d(const nps_conv3d_t* ap, int G, double* stats, void
     const nps_conv3d_t& a = *ap;
     if (check_frame(a, "gn_stats3d") < 0) return -1;
     NPS_CHECK_ARG(G >= 1 && G <= 8 && a.Cin % G == 0, "gn_stats3d: groups %d must divide Cin %d (<= 8)", G, a.Cin);
-    const long nvox = (long)a.Dc * a.Hc * a.Wc;
-    const long nb = (nvox + 255) / 256 < 1024 ? (nvox + 255) / 256 : 1024;
+    long nitem = 0;
+    for (int i = 0; i < a.nsrc; ++i) nitem += (long)a.src[i].D * a.src[i].H * a.src[i].W * ((a.src[i].C + 7) / 8);
+    nitem = nitem > 0 ? nitem : 1;  // items per sample (grid.y = sample)
+    const long nb = (nitem + 2047) / 2048 < 512 ? (nitem + 2047) / 2048 : 512;
     hipStream_t s = (hipStream_t)stream;
     if (a.bf16)
         gn_stats3d_kernel<bf16_t><<<dim3((unsigned)nb, (unsigned)a.B), 256, 0, s>>>(a, G, stats);
