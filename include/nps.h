@@ -410,6 +410,10 @@ size_t nps_conv3d_packed_bytes(int Cout, int Cin, int K, int transposed, int bf1
 int nps_conv3d_pack_weights(const float* w, void* wpack, int Cout, int Cin, int K, int transposed, int bf16,
                             void* stream);
 int nps_conv3d_fwd(const nps_conv3d_t* a, void* stream);
+/* act(GN(frame)) of a's core frame (sources, GroupNorm prologue, pre_act) materialised once as
+ * out[B][Dc][Hc][Wc][Cpad] (channels >= Cin zero, Cpad % 8 == 0): the conv that follows reads one aligned
+ * source without a prologue (the fused prologue recomputes each element for every depth tap and halo). */
+int nps_frame_pack3d(const nps_conv3d_t* a, void* out, int Cpad, void* stream);
 /* GroupNorm moments of a core frame (a's sources and B, Dc, Hc, Wc, Cin, bf16): ADDS per (b, group) the
  * fp64 (sum, sum of squares) of the frame's values (uncovered positions count as 0) to stats[B][G][2] */
 int nps_gn_stats3d(const nps_conv3d_t* a, int G, double* stats, void* stream);

@@ -126,7 +126,10 @@ struct Geo {
 
 __device__ __forceinline__ int swz(int row) { return (row >> 3) & 1; }
 
-template <typename T, int K, int S, int TH>
+// SIMPLE: one source covering the core frame at offset 0, channels a multiple of 16, no prologue (the
+// frame_pack3d output): a patch slot's address is fixed per tile (only the depth slice moves per stage), so
+// staging is one add + one 16-B load and one ds_write per slot
+template <typename T, int K, int S, int TH, bool SIMPLE>
 __global__ __launch_bounds__(256) void conv3d_kernel(const nps_conv3d_t a, int nchunk, int ntile) {
     using G = Geo<K, S, TH>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -146,7 +149,7 @@ __global__ __launch_bounds__(256) void conv3d_kernel(const nps_conv3d_t a, int n
     const int Dext = a.Dc + 2 * (a.circ + a.zpad), Hext = a.Hc + 2 * (a.circ + a.zpad),
               Wext = a.Wc + 2 * (a.circ + a.zpad);
     (void)Dext;
-    const bool pro = a.gn_stats != nullptr || a.pre_act != 0;
+    const bool pro = !SIMPLE && (a.gn_stats != nullptr || a.pre_act != 0);
 
     if (pro) {  // x' = x * scale[c] + shift[c] (GroupNorm affine of this sample), then the activation
         for (int c = tid; c < nchunk * 16; c += 256) {
@@ -170,12 +173,39 @@ __global__ __launch_bounds__(256) void conv3d_kernel(const nps_conv3d_t a, int n
     const int nstage = K * nchunk;
 
     Vec8<T> pr[G::PPT], wr[G::WPT];
+    // SIMPLE: per-slot element offset within a depth slice (-1: zero padding / past the patch)
+    int soff[G::PPT];
+    const T* sbase = reinterpret_cast<const T*>(a.src[0].ptr) + (size_t)b * a.Dc * a.Hc * a.Wc * a.Cin;
+    const size_t slice = (size_t)a.Hc * a.Wc * a.Cin;
+    if constexpr (SIMPLE) {
+#pragma unroll
+        for (int i = 0; i < G::PPT; ++i) {
+            const int idx = tid + 256 * i;
+            soff[i] = -1;
+            if (idx < G::NPP) {
+                const int pix = idx >> 1, half = idx & 1;
+                const int prr = pix / G::PC, pcc = pix - prr * G::PC;
+                const int fh = h0 * S + prr, fw = w0 * S + pcc;
+                const int ch = fh < Hext ? ext_to_core(fh, a.Hc, a.circ, a.zpad) : -1;
+                const int cw = fw < Wext ? ext_to_core(fw, a.Wc, a.circ, a.zpad) : -1;
+                if (ch >= 0 && cw >= 0) soff[i] = (ch * a.Wc + cw) * a.Cin + half * 8;
+            }
+        }
+    }
     auto fetch = [&](int st) {
         const int kd = st / nchunk, chunk = st - kd * nchunk;
         const int fd = md * S + kd;
         const int cd = ext_to_core(fd, a.Dc, a.circ, a.zpad);
+        if constexpr (SIMPLE) {
+            const T* sp = sbase + (size_t)(cd < 0 ? 0 : cd) * slice + chunk * 16;
 #pragma unroll
-        for (int i = 0; i < G::PPT; ++i) {
+            for (int i = 0; i < G::PPT; ++i) {
+                pr[i].zero();
+                if (cd >= 0 && soff[i] >= 0) pr[i].load(sp + soff[i]);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < (SIMPLE ? 0 : G::PPT); ++i) {
             const int idx = tid + 256 * i;
             pr[i].zero();
             if (idx < G::NPP) {
@@ -416,15 +446,41 @@ __global__ __launch_bounds__(256) void gn_stats3d_kernel(const nps_conv3d_t a, i
         if (si < a.nsrc) {
             const nps_src3_t& src = a.src[si];
             const int nck = (src.C + 7) / 8;
-            const long nitem = (long)src.D * src.H * src.W * nck;
+            const int nitem = src.D * src.H * src.W * nck;  // < 2^31 per sample (host-checked)
             const T* base = reinterpret_cast<const T*>(src.ptr) + (size_t)b * src.D * src.H * src.W * src.C;
             const bool vec = (src.C & 7) == 0;
-            for (long it = (long)blockIdx.x * 256 + threadIdx.x; it < nitem; it += (long)gridDim.x * 256) {
-                const int ck = (int)(it % nck);
-                const long vox = it / nck;
-                const int ww = (int)(vox % src.W);
-                const long r = vox / src.W;
-                const int hh = (int)(r % src.H), dd = (int)(r / src.H);
+            const bool inside = src.off_d >= 0 && src.off_h >= 0 && src.off_w >= 0 && src.off_d + src.D <= a.Dc &&
+                                src.off_h + src.H <= a.Hc && src.off_w + src.W <= a.Wc;
+            if (vec && inside && (cpg & 7) == 0) {
+                // the source lies wholly inside the frame: a linear sweep of its 8-channel pieces, the group of
+                // a piece from its channel chunk (no voxel decomposition)
+                for (int it = blockIdx.x * 256 + threadIdx.x; it < nitem; it += gridDim.x * 256) {
+                    Vec8<T> v;
+                    v.load(base + (size_t)it * 8);
+                    const int g0 = (lo + (it % nck) * 8) / cpg;
+                    float fs = 0.f, fq = 0.f;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        const float x = v.get(e);
+                        fs += x;
+                        fq = fmaf(x, x, fq);
+                    }
+#pragma unroll
+                    for (int g = 0; g < 8; ++g)
+                        if (g == g0) {
+                            s[g] += fs;
+                            q[g] += fq;
+                        }
+                }
+                lo += src.C;
+                continue;
+            }
+            for (int it = blockIdx.x * 256 + threadIdx.x; it < nitem; it += gridDim.x * 256) {
+                const int ck = it % nck;
+                const int vox = it / nck;
+                const int ww = vox % src.W;
+                const int r = vox / src.W;
+                const int hh = r % src.H, dd = r / src.H;
                 const int cd = dd + src.off_d, ch = hh + src.off_h, cw = ww + src.off_w;
                 if (cd < 0 || cd >= a.Dc || ch < 0 || ch >= a.Hc || cw < 0 || cw >= a.Wc) continue;
                 const T* p = base + (size_t)vox * src.C + ck * 8;
@@ -484,31 +540,89 @@ __global__ __launch_bounds__(256) void gn_stats3d_kernel(const nps_conv3d_t a, i
     }
 }
 
-template <typename T, int K, int S, int TH>
+// out[b][voxel][c] = act(GN(frame))[c] for c < Cin, 0 for Cin <= c < Cpad: the conv3d prologue applied once
+// per frame element (the fused prologue would apply it to every element K x ~1.3 times, once per depth tap
+// and halo); the conv then reads a single 16-channel-aligned source (conv3d_kernel SIMPLE).  One item = 8
+// channels of one voxel (16-B loads / stores for bf16).
+template <typename T>
+__global__ __launch_bounds__(256) void frame_pack3d_kernel(const nps_conv3d_t a, T* __restrict__ out, int Cpad) {
+    __shared__ float scl[512], sft[512];
+    const int b = blockIdx.y;
+    const bool gn = a.gn_stats != nullptr;
+    for (int c = threadIdx.x; c < Cpad; c += 256) {
+        float sc = 1.f, sh = 0.f;
+        if (gn && c < a.Cin) {
+            const int g = c / (a.Cin / a.gn_groups);
+            const double n = (double)a.Dc * a.Hc * a.Wc * (a.Cin / a.gn_groups);
+            const double mean = a.gn_stats[(b * a.gn_groups + g) * 2] / n;
+            const double var = fmax(a.gn_stats[(b * a.gn_groups + g) * 2 + 1] / n - mean * mean, 0.0);
+            const float rstd = (float)(1.0 / sqrt(var + (double)a.gn_eps));
+            sc = a.gn_gamma[c] * rstd;
+            sh = a.gn_beta[c] - (float)mean * sc;
+        }
+        scl[c] = sc;
+        sft[c] = sh;
+    }
+    __syncthreads();
+    const int npc = Cpad / 8;
+    const int nitem = a.Dc * a.Hc * a.Wc * npc;
+    T* ob = out + (size_t)b * a.Dc * a.Hc * a.Wc * Cpad;
+    for (int it = blockIdx.x * 256 + threadIdx.x; it < nitem; it += gridDim.x * 256) {
+        const int pc = it % npc;
+        const int vox = it / npc;
+        const int cw = vox % a.Wc, r = vox / a.Wc;
+        const int ch = r % a.Hc, cd = r / a.Hc;
+        Vec8<T> v;
+        load_piece<T>(v, a, b, cd, ch, cw, pc * 8);
+        if (gn || a.pre_act) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int c = pc * 8 + e;
+                float x = fmaf(v.get(e), scl[c], sft[c]);
+                if (a.pre_act == 1) x = nps::gelu_fast(x);
+                v.set(e, c < a.Cin ? x : 0.f);
+            }
+        }
+        v.store(ob + (size_t)vox * Cpad + pc * 8);
+    }
+}
+
+template <typename T, int K, int S, int TH, bool SIMPLE>
 int launch(const nps_conv3d_t& a, int nchunk, int ntile, hipStream_t s) {
     using G = Geo<K, S, TH>;
     const size_t lds = 2 * (size_t)G::BUF * sizeof(T) + 2 * (size_t)nchunk * 16 * sizeof(float);
     NPS_CHECK_ARG(lds <= 160 * 1024, "conv3d: %zu B of LDS (Cin too large for the GroupNorm table)", lds);
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)conv3d_kernel<T, K, S, TH>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
+        (void)hipFuncSetAttribute((const void*)conv3d_kernel<T, K, S, TH, SIMPLE>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = true;
     }
     const long ntiles = (long)a.B * a.Dout * ((a.Hout + TH - 1) / TH) * ((a.Wout + 31) / 32);
     NPS_CHECK_ARG(ntiles < (1L << 31), "conv3d: grid too large");
     const dim3 grid((unsigned)ntiles, (unsigned)ntile, a.transposed ? 8u : 1u);
-    conv3d_kernel<T, K, S, TH><<<grid, 256, lds, s>>>(a, nchunk, ntile);
+    conv3d_kernel<T, K, S, TH, SIMPLE><<<grid, 256, lds, s>>>(a, nchunk, ntile);
     NPS_CHECK_LAUNCH("conv3d");
     return 0;
 }
 
+bool simple_frame(const nps_conv3d_t& a) {
+    const nps_src3_t& s = a.src[0];
+    return a.nsrc == 1 && s.off_d == 0 && s.off_h == 0 && s.off_w == 0 && s.D == a.Dc && s.H == a.Hc &&
+           s.W == a.Wc && (a.Cin & 15) == 0 && a.gn_stats == nullptr && a.pre_act == 0;
+}
+
 template <typename T>
 int dispatch(const nps_conv3d_t& a, int nchunk, int ntile, hipStream_t s) {
-    if (a.K == 3 && a.stride == 1) return launch<T, 3, 1, 8>(a, nchunk, ntile, s);
-    if (a.K == 3 && a.stride == 2) return launch<T, 3, 2, 4>(a, nchunk, ntile, s);
-    if (a.K == 2 && a.stride == 1) return launch<T, 2, 1, 8>(a, nchunk, ntile, s);
-    if (a.K == 1 && a.stride == 1) return launch<T, 1, 1, 8>(a, nchunk, ntile, s);
+    const bool sim = simple_frame(a);
+    if (a.K == 3 && a.stride == 1)
+        return sim ? launch<T, 3, 1, 8, true>(a, nchunk, ntile, s) : launch<T, 3, 1, 8, false>(a, nchunk, ntile, s);
+    if (a.K == 3 && a.stride == 2)
+        return sim ? launch<T, 3, 2, 4, true>(a, nchunk, ntile, s) : launch<T, 3, 2, 4, false>(a, nchunk, ntile, s);
+    if (a.K == 2 && a.stride == 1)
+        return sim ? launch<T, 2, 1, 8, true>(a, nchunk, ntile, s) : launch<T, 2, 1, 8, false>(a, nchunk, ntile, s);
+    if (a.K == 1 && a.stride == 1)
+        return sim ? launch<T, 1, 1, 8, true>(a, nchunk, ntile, s) : launch<T, 1, 1, 8, false>(a, nchunk, ntile, s);
     NPS_CHECK_ARG(false, "conv3d: K=%d stride=%d not supported (K in {1,2,3}, stride 2 only for K=3)", a.K, a.stride);
 }
 
@@ -573,6 +687,26 @@ extern "C" int nps_conv3d_fwd(const nps_conv3d_t* ap, void* stream) {
     return a.bf16 ? dispatch<bf16_t>(a, nchunk, ntile, s) : dispatch<float>(a, nchunk, ntile, s);
 }
 
+extern "C" int nps_frame_pack3d(const nps_conv3d_t* ap, void* out, int Cpad, void* stream) {
+    NPS_CHECK_ARG(ap != nullptr && out != nullptr, "frame_pack3d: null args");
+    const nps_conv3d_t& a = *ap;
+    if (check_frame(a, "frame_pack3d") < 0) return -1;
+    NPS_CHECK_ARG(Cpad >= a.Cin && Cpad % 8 == 0 && Cpad <= 512, "frame_pack3d: Cpad %d (>= Cin, %% 8, <= 512)", Cpad);
+    NPS_CHECK_ARG(a.gn_stats == nullptr || (a.gn_gamma && a.gn_beta && a.gn_groups >= 1 && a.Cin % a.gn_groups == 0),
+                  "frame_pack3d: bad GroupNorm prologue");
+    const long nitem = (long)a.Dc * a.Hc * a.Wc * (Cpad / 8);
+    NPS_CHECK_ARG(nitem < (1L << 31), "frame_pack3d: frame too large");
+    const long nb = (nitem + 2047) / 2048 < 1024 ? (nitem + 2047) / 2048 : 1024;
+    hipStream_t s = (hipStream_t)stream;
+    const dim3 grid((unsigned)(nb > 0 ? nb : 1), (unsigned)a.B);
+    if (a.bf16)
+        frame_pack3d_kernel<bf16_t><<<grid, 256, 0, s>>>(a, reinterpret_cast<bf16_t*>(out), Cpad);
+    else
+        frame_pack3d_kernel<float><<<grid, 256, 0, s>>>(a, reinterpret_cast<float*>(out), Cpad);
+    NPS_CHECK_LAUNCH("frame_pack3d");
+    return 0;
+}
+
 extern "C" int nps_gn_stats3d(const nps_conv3d_t* ap, int G, double* stats, void* stream) {
     NPS_CHECK_ARG(ap != nullptr && stats != nullptr, "gn_stats3d: null args");
     const nps_conv3d_t& a = *ap;
@@ -580,6 +714,7 @@ extern "C" int nps_gn_stats3d(const nps_conv3d_t* ap, int G, double* stats, void
     NPS_CHECK_ARG(G >= 1 && G <= 8 && a.Cin % G == 0, "gn_stats3d: groups %d must divide Cin %d (<= 8)", G, a.Cin);
     long nitem = 0;
     for (int i = 0; i < a.nsrc; ++i) nitem += (long)a.src[i].D * a.src[i].H * a.src[i].W * ((a.src[i].C + 7) / 8);
+    NPS_CHECK_ARG(nitem < (1L << 31), "gn_stats3d: frame too large");
     nitem = nitem > 0 ? nitem : 1;  // items per sample (grid.y = sample)
     const long nb = (nitem + 2047) / 2048 < 512 ? (nitem + 2047) / 2048 : 512;
     hipStream_t s = (hipStream_t)stream;

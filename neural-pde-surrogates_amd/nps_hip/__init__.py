@@ -150,6 +150,7 @@ _SIGS = {
     "nps_conv3d_pack_weights": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp]),
     "nps_conv3d_fwd": (_i, [ctypes.POINTER(Conv3dArgs), _vp]),
     "nps_gn_stats3d": (_i, [ctypes.POINTER(Conv3dArgs), _i, _vp, _vp]),
+    "nps_frame_pack3d": (_i, [ctypes.POINTER(Conv3dArgs), _vp, _i, _vp]),
     "nps_last_error": (ctypes.c_char_p, []),
     "nps_version": (ctypes.c_char_p, []),
 }

@@ -728,6 +728,24 @@ def gn_stats3d(srcs: Sequence[Src3], frame_dhw, groups: int) -> torch.Tensor:
     return st
 
 
+# Materialise act(GN(frame)) before a K > 1 conv whose frame needs a prologue or several / offset / unaligned
+# sources (nps_frame_pack3d), so the conv runs its single-source fast path (dev knob NPS_CONV3D_PACK=0: off)
+CONV3D_PACK = os.environ.get("NPS_CONV3D_PACK", "1") == "1"
+
+
+def frame_pack3d(srcs: Sequence[Src3], frame_dhw, gn: Optional[GN] = None, pre_act=0) -> torch.Tensor:
+    """(B, Dc, Hc, Wc, Cpad) = act(GN(virtual frame)), channels zero-padded to a multiple of 16."""
+    a = _fill_frame3(Conv3dArgs(), srcs, frame_dhw)
+    if gn is not None:
+        a.gn_stats, a.gn_gamma, a.gn_beta = ptr(gn.stats), ptr(gn.gamma), ptr(gn.beta)
+        a.gn_groups, a.gn_eps = gn.groups, gn.eps
+    a.pre_act = pre_act
+    cpad = (a.Cin + 15) // 16 * 16
+    out = torch.empty((a.B, a.Dc, a.Hc, a.Wc, cpad), dtype=srcs[0].t.dtype, device=srcs[0].t.device)
+    check(lib.nps_frame_pack3d(ctypes_byref(a), ptr(out), cpad, stream_ptr()), "frame_pack3d")
+    return out
+
+
 def conv3d(srcs: Sequence[Src3], frame_dhw, wpack: torch.Tensor, bias: Optional[torch.Tensor], Cout: int, K: int,
            stride=1, transposed=False, circ=0, zpad=0, gn: Optional[GN] = None, pre_act=0,
            out: Optional[torch.Tensor] = None, out_os=1, out_off=(0, 0, 0), accumulate=False,
@@ -736,6 +754,11 @@ def conv3d(srcs: Sequence[Src3], frame_dhw, wpack: torch.Tensor, bias: Optional[
     `circ` circular then `zpad` zero voxels; valid K^3 conv (stride), or with `transposed` the 8 phase convs
     (K = 2) of a k4/s2 transposed conv written with out_os = 2.  Without `out` a tensor of the conv's
     output extent (x2 per axis when transposed) is allocated.  Returns `out`."""
+    simple = (len(srcs) == 1 and gn is None and not pre_act and tuple(srcs[0].t.shape[1:4]) == tuple(frame_dhw)
+              and not (srcs[0].off_d or srcs[0].off_h or srcs[0].off_w) and srcs[0].t.shape[4] % 16 == 0)
+    cin_alg = sum(s.t.shape[4] for s in srcs)  # algorithmic input channels (before channel padding)
+    if CONV3D_PACK and K > 1 and not simple:
+        srcs, gn, pre_act = [Src3(frame_pack3d(srcs, frame_dhw, gn, pre_act))], None, 0
     a = _fill_frame3(Conv3dArgs(), srcs, frame_dhw)
     ext = 2 * (circ + zpad)
     Dout, Hout, Wout = ((n + ext - K) // stride + 1 for n in (a.Dc, a.Hc, a.Wc))
@@ -771,8 +794,8 @@ def conv3d(srcs: Sequence[Src3], frame_dhw, wpack: torch.Tensor, bias: Optional[
         e1.record()
         nph = 8 if transposed else 1
         es = 2 if a.bf16 else 4
-        nbytes = es * (sum(s.t.numel() for s in srcs) + nph * Cout * a.Cin * K ** 3 + nph * a.B * Dout * Hout * Wout * Cout)
-        conv_probe.append((e0, e1, 2.0 * nph * a.B * Dout * Hout * Wout * Cout * a.Cin * K ** 3,
+        nbytes = es * (sum(s.t.numel() for s in srcs) + nph * Cout * cin_alg * K ** 3 + nph * a.B * Dout * Hout * Wout * Cout)
+        conv_probe.append((e0, e1, 2.0 * nph * a.B * Dout * Hout * Wout * Cout * cin_alg * K ** 3,
                            ("bf16_3d" if a.bf16 else "f32_3d", K ** 3, 4), nbytes))
     else:
         check(lib.nps_conv3d_fwd(ctypes_byref(a), stream_ptr()), "conv3d")
