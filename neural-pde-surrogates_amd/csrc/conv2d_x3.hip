@@ -42,6 +42,9 @@ __host__ __device__ constexpr int x3_patch_px_max(int ntaps, int tile_px) {
 #ifndef NPS_X3_REMAP
 #define NPS_X3_REMAP 0
 #endif
+#ifndef NPS_X3_ARING
+#define NPS_X3_ARING 2
+#endif
 // Producer slot -> (patch pixel, channel quad).  REMAP: the 16 lanes of one ds_write_b64 group take
 // pixels {0, 2, 4, 6} (lanes 16-31: {1, 3, 5, 7}) of a run of 8, whose 32-B [hi] / [lo] runs at the 80-B
 // pixel pitch land on disjoint banks (consecutive pixels collide: 20 p mod 32 repeats within 4).
@@ -57,9 +60,9 @@ __device__ __forceinline__ int x3_slot_px(int idx) {
 #ifdef NPS_X3_STAMP  // dev diagnostic: per-work-group s_memtime stamps of consumer wave 0
 __device__ unsigned long long x3_stamps[1 << 20];
 #define X3_STAMP(i) \
-    if (wave == 0 && lane == 0 && l < (1 << 17)) x3_stamps[l * 8 + (i)] = __builtin_amdgcn_s_memtime()
+    if (wave == 0 && lane == 0 && l < (1 << 16)) x3_stamps[l * 16 + (i)] = __builtin_amdgcn_s_memtime()
 #define X3_RSTAMP(i) \
-    if (wave == 0 && lane == 0 && l < (1 << 17)) x3_stamps[l * 8 + (i)] = __builtin_amdgcn_s_memrealtime()
+    if (wave == 0 && lane == 0 && l < (1 << 16)) x3_stamps[l * 16 + (i)] = __builtin_amdgcn_s_memrealtime()
 #else
 #define X3_STAMP(i)
 #define X3_RSTAMP(i)
@@ -74,7 +77,7 @@ __device__ __forceinline__ void static_for(F&& f) {
 }
 
 // NHWC output with 4-aligned channels: the epilogue goes through LDS (x3_store_phase)
-__device__ __forceinline__ bool x3_lds_epilogue(const nps_conv2d_t& a) {
+__host__ __device__ __forceinline__ bool x3_lds_epilogue(const nps_conv2d_t& a) {
     return !a.out_nchw && (a.out_C & 3) == 0 && (a.Cout & 3) == 0;
 }
 
@@ -180,6 +183,15 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
     if (wave >= 4) __builtin_amdgcn_s_setprio(1);
 #elif NPS_X3_PRIO == 2
     if (wave < 4) __builtin_amdgcn_s_setprio(1);
+#endif
+#if defined(NPS_X3_STAGGER) && NPS_X3_STAGGER > 1
+    // dev experiment: desynchronise the work-groups' store bursts — work-group group k (of NPS_X3_STAGGER,
+    // by XCD round) starts k/NPS_X3_STAGGER of a tile (NPS_X3_TILE_CYC cycles) late
+    if (WIDE && NTAPS == 9) {
+        const long dly = (long)((blockIdx.x >> 3) % NPS_X3_STAGGER) * NPS_X3_TILE_CYC / NPS_X3_STAGGER;
+        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+        while ((long)(__builtin_amdgcn_s_memtime() - t0) < dly) __builtin_amdgcn_s_sleep(8);
+    }
 #endif
     if (wave >= 4) {
         // ------------------------------------------------------------------ producers: patch only
@@ -379,7 +391,9 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
     const size_t gstride = (size_t)ncb * 2048;  // bytes per K-group (chunk, tap) of the packed weight
     const int G = nstages * NTAPS;
     const char* wbase = nullptr;
-    f16x8 Aw[2][CBW][2];
+    // weight fragments: a ring of NPS_X3_ARING K-groups (2: loaded one K-group ahead; 3: two ahead)
+    constexpr int AR = NPS_X3_ARING;
+    f16x8 Aw[AR][CBW][2];
     f16x8 Bh[2][PBW], Bl[2][PBW];
     auto loadA = [&](int gg, f16x8 (&d)[CBW][2]) {
         const char* p = wbase + (size_t)gg * gstride;
@@ -406,22 +420,22 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
 #ifdef NPS_X3_STAMP
     unsigned long long bar_cycles = 0;  // consumer wave 0: cycles spent in the stage barriers
 #endif
-    auto group = [&](int gg, const int r) {
-        loadA(gclamp(gg + 1), Aw[r ^ 1]);
+    auto group = [&](int gg, const int ra, const int r) {  // ra: weight slot of K-group gg, r: patch slot
+        loadA(gclamp(gg + AR - 1), Aw[(ra + AR - 1) % AR]);
         loadB(gclamp(gg + 1), Bh[r ^ 1], 0);
         loadB(gclamp(gg + 1), Bl[r ^ 1], 1);
 #pragma unroll
         for (int cb = 0; cb < CBW; ++cb)
 #pragma unroll
-            for (int pb = 0; pb < PBW; ++pb) acc[cb][pb] = X3_MFMA(Aw[r][cb][0], Bh[r][pb], acc[cb][pb], 0, 0, 0);
+            for (int pb = 0; pb < PBW; ++pb) acc[cb][pb] = X3_MFMA(Aw[ra][cb][0], Bh[r][pb], acc[cb][pb], 0, 0, 0);
 #pragma unroll
         for (int cb = 0; cb < CBW; ++cb)
 #pragma unroll
-            for (int pb = 0; pb < PBW; ++pb) acc[cb][pb] = X3_MFMA(Aw[r][cb][0], Bl[r][pb], acc[cb][pb], 0, 0, 0);
+            for (int pb = 0; pb < PBW; ++pb) acc[cb][pb] = X3_MFMA(Aw[ra][cb][0], Bl[r][pb], acc[cb][pb], 0, 0, 0);
 #pragma unroll
         for (int cb = 0; cb < CBW; ++cb)
 #pragma unroll
-            for (int pb = 0; pb < PBW; ++pb) acc[cb][pb] = X3_MFMA(Aw[r][cb][1], Bh[r][pb], acc[cb][pb], 0, 0, 0);
+            for (int pb = 0; pb < PBW; ++pb) acc[cb][pb] = X3_MFMA(Aw[ra][cb][1], Bh[r][pb], acc[cb][pb], 0, 0, 0);
 #pragma unroll
         for (int i = 0; i < 2 * CBW; ++i) {  // weights first: the longest latency gets the most cover
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
@@ -463,19 +477,39 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
         X3_STAMP(0);
         X3_RSTAMP(4);
         loadA(0, Aw[0]);
+        if constexpr (AR == 3) loadA(gclamp(1), Aw[1]);
         barrier();
         loadB(0, Bh[0], 0);
         loadB(0, Bl[0], 1);
         X3_STAMP(1);
         int g0 = 0;
-        for (; g0 + 2 <= G; g0 += 2) {
-            group(g0, 0);
-            group(g0 + 1, 1);
+        if constexpr (AR == 2) {
+            for (; g0 + 2 <= G; g0 += 2) {
+                group(g0, 0, 0);
+                group(g0 + 1, 1, 1);
+#ifdef NPS_X3_STAMP
+                if (g0 == 0) X3_STAMP(7);  // first two K-groups done (the first operand waits)
+#endif
+            }
+            if (g0 < G) group(g0, 0, 0);
+        } else {  // slots (gg % 3, gg % 2): 6 K-groups per iteration, the tail continues the same pattern
+            for (; g0 + 6 <= G; g0 += 6) {
+                static_for<6>([&](auto jc) {
+                    constexpr int j = decltype(jc)::value;
+                    group(g0 + j, j % 3, j % 2);
+                });
+#ifdef NPS_X3_STAMP
+                if (g0 == 0) X3_STAMP(7);
+#endif
+            }
+            static_for<6>([&](auto jc) {
+                constexpr int j = decltype(jc)::value;
+                if (g0 + j < G) group(g0 + j, j % 3, j % 2);
+            });
         }
-        if (g0 < G) group(g0, 0);
         X3_STAMP(2);
 #ifdef NPS_X3_STAMP
-        if (wave == 0 && lane == 0 && l < (1 << 17)) x3_stamps[l * 8 + 6] = bar_cycles;
+        if (wave == 0 && lane == 0 && l < (1 << 16)) x3_stamps[l * 16 + 6] = bar_cycles;
         bar_cycles = 0;
 #endif
         if (lds_epi) {
@@ -495,7 +529,9 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
                     }
             }
             barrier();
+            X3_STAMP(8);
             x3_store_phase<TILE_PX, NCO>(a, b, cob, oy0, ox0, g.T, T, tid, amax);
+            X3_STAMP(9);
         } else {
             static_for<PBW>([&](auto pbc) {  // compile-time pb: acc stays in registers
                 constexpr int pb = decltype(pbc)::value;
@@ -988,6 +1024,334 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// 1x1 as a persistent HBM stream: conv1x1_dma_kernel<NCB>.  A 1x1 conv moves (Cin + Cout) x 4 B per pixel
+// for 2 Cin Cout flops, so it is bound by how many bytes each CU keeps in flight, not by the MFMAs; the
+// register-staged kernels above hold one 32-channel stage per wave in flight and stall at every
+// work-group's prologue and store drain.  Here one 512-thread work-group per CU walks 128-pixel tiles:
+//   * waves 4-7 (loaders) copy each 32-channel stage of the tile's input (128 px x 128 B) and of the packed
+//     weights (2 chunks x NCB blocks x 2 KiB) HBM/L2 -> LDS with global_load_lds_dwordx4 (no VGPR round
+//     trip), input IA = NS - 1 = 4 stages and weights 2 stages ahead of the MFMA waves, across tile
+//     boundaries; a loader wave only ever issues DMAs, so one counted vmcnt per stage retires them;
+//   * waves 0-3 (MFMA) own 32 pixels x all NCB*32 output channels each: per 16-channel K-group a lane reads
+//     its pixel's 8 channels (2 ds_read_b128), splits them hi/lo and runs 3 MFMAs per 32-channel block
+//     against the weight fragments read from LDS; the tile's last stage is followed by the fused epilogue
+//     (store_tile: bias, addends, GELU, accumulate, range tag, GroupNorm moments) straight from the
+//     accumulators while the loaders' DMAs for the next tile are already in flight.
+// Input image per slot: [pixel][8 x 16-B chunks]; chunk c of pixel p lives at chunk c ^ ((p >> 1) & 7)
+// (the DMA writes lane-linearly, so the swizzle is on the source address): the 16 lanes of a
+// ds_read_b128 group read 16 distinct bank quads.
+__host__ __device__ constexpr int x1d_ns(int ncb) { return 5; }  // input ring slots (16 KiB)
+constexpr int X1D_NW = 3;                 // weight ring slots (NCB x 4 KiB)
+constexpr int X1D_ISLOT = 128 * 128;      // bytes of one input stage: 128 px x 32 ch x 4 B
+
+__host__ __device__ constexpr int x1d_lds_bytes(int ncb) {
+    return x1d_ns(ncb) * X1D_ISLOT + X1D_NW * ncb * 4096 + ncb * 32 * 4;
+}
+
+__device__ __forceinline__ void x1d_dma16(const void* g, void* lds) {
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const unsigned*>(g),
+                                     (__attribute__((address_space(3))) unsigned*)(lds), 16, 0, 0);
+}
+
+// Epilogue of one 32-channel accumulator block of a lane (channels co_base + 8m + 4h + [0, 4), m < 4) at
+// NHWC element offset `base` (4-aligned channels), whose accumulator started from bias x (weight scale x
+// input scale) — an exact power-of-2 multiple, so acc * inv is the conv plus the bias, rounded once: acc :=
+// the stored values (scale, addends, GELU, accumulate, as store_tile_s), max |value| into amax, their moments
+// (or, accumulating, the change they make) into (s1, s2).  epi_store writes them; no load follows it.
+__device__ __forceinline__ void epi_finish(const nps_conv2d_t& a, size_t base, int co_base, int h, float inv,
+                                           f32x16& acc, float& amax, double& s1, double& s2) {
+    const bool st = a.out_stats != nullptr;
+    float f1 = 0.f, f2 = 0.f;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const int co0 = co_base + 8 * m + 4 * h;
+        if (co0 >= a.Cout) continue;
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        const f32x4 a0 = a.addend0 ? *reinterpret_cast<const f32x4*>(a.addend0 + base + co0) : z;
+        const f32x4 a1 = a.addend1 ? *reinterpret_cast<const f32x4*>(a.addend1 + base + co0) : z;
+        const f32x4 o = a.accumulate ? *reinterpret_cast<const f32x4*>(a.out + base + co0) : z;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            float v = acc[4 * m + e] * inv;  // (the bias is in the accumulator: conv1x1_dma_kernel)
+            if (!a.add_after_act) v = v + a0[e] + a1[e];
+            if (a.act == 1) v = nps::gelu_erf(v);
+            if (a.add_after_act) v = v + a0[e] + a1[e];
+            if (a.accumulate) v += o[e];
+            acc[4 * m + e] = v;
+            amax = fmaxf(amax, fabsf(v));
+            if (st) {
+                f1 += a.accumulate ? v - o[e] : v;
+                f2 += a.accumulate ? (v - o[e]) * (v + o[e]) : v * v;
+            }
+        }
+    }
+    if (st) {
+        s1 += (double)f1;
+        s2 += (double)f2;
+    }
+}
+__device__ __forceinline__ void epi_store(const nps_conv2d_t& a, size_t base, int co_base, int h, const f32x16& v) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const int co0 = co_base + 8 * m + 4 * h;
+        if (co0 >= a.Cout) continue;
+        *reinterpret_cast<f32x4*>(a.out + base + co0) = f32x4{v[4 * m], v[4 * m + 1], v[4 * m + 2], v[4 * m + 3]};
+    }
+}
+
+template <int NCB>
+__global__ __launch_bounds__(512) void conv1x1_dma_kernel(const nps_conv2d_t a) {
+    constexpr int WSLOT = NCB * 4096;          // 2 chunks x NCB blocks x (hi, lo) x 1 KiB
+    constexpr int NS = x1d_ns(NCB), IA = NS - 1;  // input slots; input stages issued ahead
+    constexpr int VMC = NCB + 8;               // loader DMAs allowed in flight at a stage barrier (below)
+    static_assert(IA >= 3 && 2 * NCB * 2 % 4 == 0, "conv1x1_dma pipeline");
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    char* iring = reinterpret_cast<char*>(smem);
+    char* wring = iring + NS * X1D_ISLOT;
+    float* btab = reinterpret_cast<float*>(wring + X1D_NW * WSLOT);  // [NCB * 32] bias x scale (0 past Cout)
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int npx = a.Hout * a.Wout;
+    const int ptiles = (npx + 127) / 128;      // 128-pixel tiles per sample
+    const int ntiles = ptiles * a.B;
+    const int nst = (a.Cin + 31) / 32;         // 32-channel stages per tile
+    const int mytiles = blockIdx.x < ntiles ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+    const int U = mytiles * nst;               // stages this work-group runs (every wave: U + 1 barriers)
+    auto barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+
+    if (wave >= 4) {
+        // -------------------------------------------------------------- loaders: DMA only
+        const int pw = wave - 4;
+        const int lo1 = a.src[0].C, lo2 = a.src[0].C + (a.nsrc > 1 ? a.src[1].C : 0);
+        const size_t gstride = (size_t)packed_ncb(a.Cout) * 2048;  // bytes per packed 16-channel chunk
+        const char* wg = reinterpret_cast<const char*>(a.wpack);
+        // Input cursor (next stage to fetch; past the end it re-fetches the last stage into the freed slot,
+        // bytes nobody reads).  Per tile, each lane's 4 pixels (DMA instruction i: tile pixels
+        // 32 pw + 8 i + lane / 8) are located once in every source; a stage then selects the source of the
+        // lane's swizzled 16-B chunk (4 channels, inside one source: host-checked 4-aligned sources).
+        const float* pp[4][3];
+        int ki = 0, sti = 0, uin = 0;
+        auto locate = [&](int k) {
+            const int t = (int)blockIdx.x + k * (int)gridDim.x;
+            const int b = t / ptiles, P0 = (t - b * ptiles) * 128;
+            const nps_src_t S0 = a.src[0], S1 = a.src[1], S2 = a.src[2];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int P = P0 + 32 * pw + 8 * i + (lane >> 3);
+                const int oy = P / a.Wout, ox = P - (P / a.Wout) * a.Wout;
+                const int ye = oy - a.pad_y, xe = ox - a.pad_x;
+                const bool ok = P < npx && ye >= 0 && ye < a.Hin + 2 * a.circ && xe >= 0 && xe < a.Win + 2 * a.circ;
+                const int fy = a.circ ? nps::wrap_mod(ye - a.circ, a.Hin) : ye;
+                const int fx = a.circ ? nps::wrap_mod(xe - a.circ, a.Win) : xe;
+                auto at = [&](const nps_src_t& S) -> const float* {
+                    const int yy = fy - S.off_y, xx = fx - S.off_x;
+                    return (ok && yy >= 0 && yy < S.H && xx >= 0 && xx < S.W)
+                               ? S.ptr + ((size_t)(b * S.H + yy) * S.W + xx) * S.C
+                               : nullptr;
+                };
+                pp[i][0] = at(S0);
+                pp[i][1] = a.nsrc > 1 ? at(S1) : nullptr;
+                pp[i][2] = a.nsrc > 2 ? at(S2) : nullptr;
+            }
+        };
+        auto issue_in = [&](int u) {  // stage at the cursor -> the ring slot iteration u frees
+            if (uin < U && sti == 0) locate(ki);
+            char* dst = iring + (u % NS) * X1D_ISLOT;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int px = 32 * pw + 8 * i + (lane >> 3);
+                const int ch = sti * 32 + 4 * ((lane & 7) ^ ((px >> 1) & 7));  // the swizzled chunk's channels
+                const int si = (ch >= lo1 ? 1 : 0) + (ch >= lo2 ? 1 : 0);
+                const float* base = si == 0 ? pp[i][0] : (si == 1 ? pp[i][1] : pp[i][2]);
+                const int cl = ch - (si == 0 ? 0 : (si == 1 ? lo1 : lo2));
+                const float* src = (base != nullptr && ch < a.Cin) ? base + cl : x3_zero16;
+                x1d_dma16(src, dst + (32 * pw + 8 * i) * 128);
+            }
+            if (uin < U) {
+                ++uin;
+                if (++sti == nst) {
+                    sti = 0;
+                    ++ki;
+                }
+            }
+        };
+        int stw = 0, uw = 0;  // weight cursor
+        auto issue_w = [&](int u) {
+            char* dst = wring + (u % X1D_NW) * WSLOT;
+#pragma unroll
+            for (int j = 0; j < NCB; ++j) {
+                const int q = pw * NCB + j;                     // 1-KiB piece of the stage
+                const int k = q / (2 * NCB), rem = q - k * (2 * NCB);
+                x1d_dma16(wg + (size_t)(2 * stw + k) * gstride + rem * 1024 + lane * 16, dst + q * 1024);
+            }
+            if (uw < U) {
+                ++uw;
+                if (++stw == nst) stw = 0;
+                if (uw == U) stw = (U - 1) % nst;  // past the end: the last stage again
+            }
+        };
+        // Pipeline: before barrier B_u (after which the MFMA waves compute stage u + 1) stage u + 1's input
+        // and weights have landed.  Iteration u issues W(u + 2) then I(u + IA) into the slots stage u - 1
+        // freed at B_{u-1}; W(u + 1), the newest DMA group B_u depends on, was issued first in iteration
+        // u - 1, so at most (4) + (NCB + 4) = VMC DMAs issued after it may still be in flight; I(u + 1) is
+        // older.  The prologue I(0) .. I(IA - 3), W(0), I(IA - 2), W(1), I(IA - 1) keeps that shape, so one
+        // counted wait fits every barrier (4 input DMAs and NCB weight DMAs per loader wave and stage).
+        if (U > 0) {
+#pragma unroll
+            for (int i = 0; i + 2 < IA; ++i) issue_in(i);
+            issue_w(0);
+            issue_in(IA - 2);
+            issue_w(1);
+            issue_in(IA - 1);
+        }
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VMC) : "memory");
+        barrier();
+#ifdef NPS_X3_STAMP  // dev (tools/x1d_stamps.py): loader wave 4's cycles in its vmcnt waits and barriers
+        unsigned long long tv = 0, tb = 0;
+#endif
+        for (int u = 0; u < U; ++u) {
+            issue_w(u + 2);
+            issue_in(u + IA);
+#ifdef NPS_X3_STAMP
+            const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VMC) : "memory");
+            const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+            barrier();
+            tv += t1 - t0;
+            tb += __builtin_amdgcn_s_memtime() - t1;
+#else
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VMC) : "memory");
+            barrier();
+#endif
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the work-group's LDS
+#ifdef NPS_X3_STAMP
+        {
+            const int l = blockIdx.x;
+            if (wave == 4 && lane == 0 && l < (1 << 16)) {
+                x3_stamps[l * 16 + 5] = tv;
+                x3_stamps[l * 16 + 6] = tb;
+                x3_stamps[l * 16 + 7] = U;
+            }
+        }
+#endif
+        return;
+    }
+
+    // ------------------------------------------------------------------ MFMA waves
+    const float xs = in_scale_of(a);
+    const bool scaled = has_in_scale(a);
+    const float inv = 1.f / (pow2_scale_for(a.wpack[packed_body(a.Cout, a.Cin, 1)]) * xs);
+    const int h = lane >> 5;
+    const int px = 32 * wave + (lane & 31);                      // this lane's tile pixel
+    const int sw = (px >> 1) & 7;
+    for (int c = tid; c < NCB * 32; c += 256)
+        btab[c] = (a.bias != nullptr && c < a.Cout) ? a.bias[c] / inv : 0.f;
+    f32x16 acc[NCB];
+    float amax = 0.f;
+#ifdef NPS_X3_STAMP  // dev (tools/x1d_stamps.py): MFMA wave 0's cycles at barriers and in epilogues
+    const int l = blockIdx.x;
+    unsigned long long tbar = 0, tepi = 0;
+    X3_STAMP(0);
+    X3_RSTAMP(8);
+#endif
+    barrier();  // B_{-1}: stage 0 landed (and the bias table written)
+#ifdef NPS_X3_STAMP
+    X3_STAMP(1);
+#endif
+    for (int u = 0; u < U; ++u) {
+        const int k = u / nst, st = u - (u / nst) * nst;
+        if (st == 0) {  // accumulators start from the scaled bias (lane element r: co 8 (r / 4) + 4 h + r % 4)
+#pragma unroll
+            for (int i = 0; i < NCB; ++i)
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    const f32x4 bv = *reinterpret_cast<const f32x4*>(btab + i * 32 + 8 * m + 4 * h);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) acc[i][4 * m + e] = bv[e];
+                }
+        }
+        const char* ib = iring + (u % NS) * X1D_ISLOT + px * 128;
+        const char* wb = wring + (u % X1D_NW) * WSLOT + lane * 16;
+#pragma unroll
+        for (int kg = 0; kg < 2; ++kg) {
+            // K-group kg of the stage: lane half h holds channels 16 h + 8 kg + [0, 8) (the 1x1 packing)
+            const int c0 = 4 * h + 2 * kg;
+            f32x4 v0 = *reinterpret_cast<const f32x4*>(ib + ((c0 ^ sw) << 4));
+            f32x4 v1 = *reinterpret_cast<const f32x4*>(ib + (((c0 + 1) ^ sw) << 4));
+            if (scaled) {
+                v0 *= xs;
+                v1 *= xs;
+            }
+            // the K-group's weight fragments, all issued before the first MFMA (LDS returns in order: the
+            // MFMAs of block cb wait only for its own pair)
+            f16x8 Ah[NCB], Al[NCB];
+#pragma unroll
+            for (int cb = 0; cb < NCB; ++cb) {
+                Ah[cb] = *reinterpret_cast<const f16x8*>(wb + (kg * NCB + cb) * 2048);
+                Al[cb] = *reinterpret_cast<const f16x8*>(wb + (kg * NCB + cb) * 2048 + 1024);
+            }
+            f16x4 h0, l0, h1, l1;
+            split4(v0, h0, l0);
+            split4(v1, h1, l1);
+            const f16x8 Bh = f16x8{h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+            const f16x8 Bl = f16x8{l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+#pragma unroll
+            for (int cb = 0; cb < NCB; ++cb) {
+                acc[cb] = X3_MFMA(Ah[cb], Bh, acc[cb], 0, 0, 0);
+                acc[cb] = X3_MFMA(Ah[cb], Bl, acc[cb], 0, 0, 0);
+                acc[cb] = X3_MFMA(Al[cb], Bh, acc[cb], 0, 0, 0);
+            }
+        }
+#ifdef NPS_X3_STAMP
+        const unsigned long long tb0 = __builtin_amdgcn_s_memtime();
+        barrier();  // B_u
+        const unsigned long long tb1 = __builtin_amdgcn_s_memtime();
+        tbar += tb1 - tb0;
+#else
+        barrier();  // B_u: every read of stage u's slots is done; stage u + 1 has landed
+#endif
+        if (st == nst - 1) {
+            // the tile's epilogue, from the accumulators (the loaders' DMAs for the next stages are in flight).
+            // Two passes: every load (bias, addends, accumulate) and the arithmetic first, the stores last —
+            // vmcnt counts loads and stores in one in-order queue, so a load behind a store would wait for
+            // that store to reach memory.
+            const int t = (int)blockIdx.x + k * (int)gridDim.x;
+            const int b = t / ptiles, P = (t - b * ptiles) * 128 + px;
+            double s1 = 0.0, s2 = 0.0;
+            if (P < npx) {
+                const int oy = P / a.Wout, ox = P - (P / a.Wout) * a.Wout;
+                const int dy = oy * a.out_os + a.out_off_y, dx = ox * a.out_os + a.out_off_x;
+                if (dy >= 0 && dy < a.out_H && dx >= 0 && dx < a.out_W) {  // NHWC, 4-aligned (x1_dma_ok)
+                    const size_t base = (((size_t)b * a.out_H + dy) * a.out_W + dx) * a.out_C;
+                    static_for<NCB>([&](auto cbc) {  // compile-time cb: acc stays in registers
+                        constexpr int cb = decltype(cbc)::value;
+                        epi_finish(a, base, cb * 32, h, inv, acc[cb], amax, s1, s2);
+                        if (cb & 1) __builtin_amdgcn_sched_barrier(0);  // loads hoisted 2 blocks at most
+                    });
+                    static_for<NCB>([&](auto cbc) {
+                        constexpr int cb = decltype(cbc)::value;
+                        epi_store(a, base, cb * 32, h, acc[cb]);
+                    });
+                }
+            }
+            stats_publish(a, b, s1, s2);
+#ifdef NPS_X3_STAMP
+            tepi += __builtin_amdgcn_s_memtime() - tb1;
+#endif
+        }
+    }
+    nps::tag_publish(a.out_tag, amax, nps::wave_salt());
+#ifdef NPS_X3_STAMP
+    if (wave == 0 && lane == 0 && l < (1 << 16)) {
+        x3_stamps[l * 16 + 2] = tbar;
+        x3_stamps[l * 16 + 3] = tepi;
+    }
+    X3_STAMP(4);
+    X3_RSTAMP(9);
+#endif
+}
+
 template <int NT, int PB, bool PRO = false, bool WIDE = false>
 void launch_x3_one(const nps_conv2d_t& a, unsigned nwg, int lds, hipStream_t s) {
     static bool attr_set = false;
@@ -999,7 +1363,38 @@ void launch_x3_one(const nps_conv2d_t& a, unsigned nwg, int lds, hipStream_t s) 
     conv2d_x3_kernel<NT, PB, PRO, WIDE><<<nwg, 512, lds, s>>>(a);
 }
 
+template <int NCB>
+void launch_x1d(const nps_conv2d_t& a, unsigned grid, hipStream_t s) {
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)conv1x1_dma_kernel<NCB>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  x1d_lds_bytes(NCB));
+        attr_set = true;
+    }
+    conv1x1_dma_kernel<NCB><<<grid, 512, x1d_lds_bytes(NCB), s>>>(a);
+}
+
 }  // namespace
+
+// The DMA-stream 1x1 (conv1x1_dma_kernel) takes every split-fp16 1x1 with Cout <= 192 whose sources are
+// 4-channel aligned (16-B DMA pieces) and whose output is NHWC with 4-aligned channels; dev knob
+// NPS_X1_DMA=0: the register-staged kernels instead.
+static bool x1_dma_on() {
+    static int on = -1;
+    if (on < 0) {
+        const char* e = getenv("NPS_X1_DMA");
+        on = (e != nullptr && e[0] == '0') ? 0 : 1;
+    }
+    return on == 1;
+}
+bool x1_dma_ok(const nps_conv2d_t& a) {
+    if (!x1_dma_on() || a.KH * a.KW != 1 || a.stride != 1 || a.dil != 1 || a.Cout > 192 || !x3_lds_epilogue(a))
+        return false;
+    for (int i = 0; i < a.nsrc; ++i)
+        if ((a.src[i].C & 3) != 0) return false;
+    return true;
+}
+extern "C" int nps_conv2d_x1_dma(const nps_conv2d_t* a) { return a != nullptr && x1_dma_ok(*a) ? 1 : 0; }
 
 // test hook (nps_x3_set_grid): persistent-grid size override (> 0)
 static long g_x3_grid_override = 0;
@@ -1038,6 +1433,20 @@ int nps_launch_conv2d_x3(const nps_conv2d_t& a, int lds, hipStream_t s) {
     // stages match the 1x1 weight packing; work-group = min(ncob, 8) waves, blockIdx.z = 512-channel group
     if (a.KH * a.KW == 1) {
         NPS_CHECK_ARG(!pro, "conv2d_fwd (split-fp16): 1x1 prologue");
+        if (x1_dma_ok(a)) {
+            const int ncb = (a.Cout + 31) / 32;
+            const long ntiles = (((long)a.Hout * a.Wout + 127) / 128) * a.B;
+            NPS_CHECK_ARG(ntiles < (1L << 31), "conv2d_fwd: grid too large");
+            const unsigned g1 = (unsigned)(ntiles < ncu ? ntiles : ncu);  // persistent: one work-group per CU
+            if (ncb <= 2)
+                launch_x1d<2>(a, g1, s);
+            else if (ncb <= 4)
+                launch_x1d<4>(a, g1, s);
+            else
+                launch_x1d<6>(a, g1, s);
+            NPS_CHECK_LAUNCH("conv2d_fwd (split-fp16 1x1, DMA stream)");
+            return 0;
+        }
         static int cfg = -1;  // dev knob NPS_X3_1X1_CFG: 0 = (PB 2, D 2), 1 = (1, 4), 2 = (1, 2)
         if (cfg < 0) {
             const char* e = getenv("NPS_X3_1X1_CFG");

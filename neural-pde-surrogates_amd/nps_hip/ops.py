@@ -35,6 +35,7 @@ def conv_precision(KH, KW, stride=1, dil=1):
 # Optional live probe of the conv kernel (bench.py): when a list, every conv2d launch appends
 # (start_event, end_event, algorithmic_flops) recorded on the launching stream.
 conv_probe = None
+conv_shape_log = None  # dev (tools/call_shapes.py): with conv_probe, one launch-geometry dict per conv launch
 
 
 class Src(NamedTuple):
@@ -418,7 +419,8 @@ def conv2d(srcs: Sequence[Src], frame_hw, wpack: torch.Tensor, bias: Optional[to
         a.out_tag = out_tag(out, accumulate) if out_given else new_tag(out)
     if out_stats is not None:
         plain = not accumulate and not ads and act == 0
-        if (a.precision == PREC_X3F16 and (KH * KW != 1 or (Cout <= 192 and X1_LDS_WEIGHTS and plain))
+        x1_ok = lib.nps_conv2d_x1_dma(ctypes_byref(a)) == 1 or (Cout <= 192 and X1_LDS_WEIGHTS and plain)
+        if (a.precision == PREC_X3F16 and (KH * KW != 1 or x1_ok)
                 and not out_nchw and oC % 4 == 0 and Cout % 4 == 0):
             a.out_stats = ptr(out_stats)
         else:
@@ -433,6 +435,10 @@ def conv2d(srcs: Sequence[Src], frame_hw, wpack: torch.Tensor, bias: Optional[to
         nbytes = 4.0 * (sum(s.t.numel() for s in srcs) + Cout * cin_alg * KH * KW + B * Hout * Wout * Cout)
         conv_probe.append((e0, e1, 2.0 * B * Hout * Wout * Cout * cin_alg * KH * KW,
                            ("x3f16" if a.precision == PREC_X3F16 else "f32", KH * KW, a.waves), nbytes))
+        if conv_shape_log is not None:
+            conv_shape_log.append(dict(cin=cin_alg, cout=Cout, k=(KH, KW), hw=(Hin, Win), out=(Hout, Wout), B=B,
+                                       nsrc=len(srcs), acc=bool(accumulate), addends=len(ads), act=act,
+                                       gn=gn is not None, pre_act=pre_act, stats=out_stats is not None))
     else:
         check(lib.nps_conv2d_fwd(ctypes_byref(a), stream_ptr()), "conv2d_fwd")
     return out

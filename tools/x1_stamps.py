@@ -38,7 +38,7 @@ def main():
     fn = lib.nps_x3_stamps
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
     assert fn(ctypes.addressof(buf), n) == 0
-    st = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 8).astype(np.int64)
+    st = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 16).astype(np.int64)
     nwg = int(np.count_nonzero(st[:, 3]))
     st = st[:nwg]
     clk = (st[:, 3] - st[:, 0]) / np.maximum(st[:, 5] - st[:, 4], 1) * 100.0  # MHz

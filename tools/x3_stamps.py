@@ -43,7 +43,7 @@ def main():
     fn = lib.nps_x3_stamps
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
     assert fn(ctypes.addressof(buf), n) == 0
-    st = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 8).astype(np.int64)
+    st = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 16).astype(np.int64)
     wide = os.environ.get("NPS_X3_WIDE", "1") != "0" and a.k in (2, 3) and 128 < a.cout <= 192
     tile = 128 if wide else (512 if a.hw >= 64 else 256)
     nwg = int(np.count_nonzero(st[:, 3]))
@@ -57,6 +57,9 @@ def main():
     print(f"cycles per WG (median): prologue {np.median(pro):.0f}  loop {np.median(loop):.0f} "
           f"(MFMA-only {ideal})  epilogue {np.median(epi):.0f}; loop p10/p90 {np.percentile(loop, 10):.0f}/"
           f"{np.percentile(loop, 90):.0f}")
+    print(f"epilogue split (median cycles): acc->LDS + barrier {np.median(st[:, 8] - st[:, 2]):.0f}, store phase "
+          f"{np.median(st[:, 9] - st[:, 8]):.0f}, final barrier {np.median(st[:, 3] - st[:, 9]):.0f}; first 2 K-groups "
+          f"{np.median(st[:, 7] - st[:, 1]):.0f} (MFMA-only {2 * ideal // groups})")
     print(f"loop efficiency {ideal / np.median(loop) * 100:.1f}%; consumer wave 0 waits at stage barriers "
           f"{np.median(st[:, 6]):.0f} cycles per WG (median)")
 
