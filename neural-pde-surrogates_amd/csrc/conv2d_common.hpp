@@ -273,17 +273,19 @@ inline bool x3_wide_eligible(const nps_conv2d_t& a) {
     return (nt == 4 || nt == 9) && a.Cout > 128 && a.Cout <= 192 && (a.Cout & 31) == 0 && a.dil == 1 &&
            a.stride == 1 && !a.lattice;
 }
-inline bool x3_wide_tile(const nps_conv2d_t& a) { return a.TH * a.TW == 128; }
+__host__ __device__ inline bool x3_wide_tile(const nps_conv2d_t& a) { return a.TH * a.TW == 128; }
 
 // floats per pixel of the LDS-staged output tile: the work-group's channels + 4 (pad)
-inline int x3_tpitch(const nps_conv2d_t& a) { return (x3_wide_tile(a) ? 192 : 64) + 4; }
+__host__ __device__ inline int x3_tpitch(const nps_conv2d_t& a) { return (x3_wide_tile(a) ? 192 : 64) + 4; }
 
-inline int x3_lds_bytes(const nps_conv2d_t& a) {
+// bytes of the split-fp16 kernel's patch ring / epilogue tile region (they share it)
+__host__ __device__ inline int x3_region_bytes(const nps_conv2d_t& a) {
     const Geo g = make_geo(a);
     const int ring = X3_NST * ((g.PH * g.PW * X3_PIXB + 15) & ~15);
     const int tile = a.TH * a.TW * x3_tpitch(a) * 4;
-    return 128 + (ring > tile ? ring : tile);
+    return ring > tile ? ring : tile;
 }
+inline int x3_lds_bytes(const nps_conv2d_t& a) { return 128 + x3_region_bytes(a); }  // 128-B header + region
 
 }  // namespace
 

@@ -1376,14 +1376,15 @@ void launch_x1d(const nps_conv2d_t& a, unsigned grid, hipStream_t s) {
 
 }  // namespace
 
-// The DMA-stream 1x1 (conv1x1_dma_kernel) takes every split-fp16 1x1 with Cout <= 192 whose sources are
-// 4-channel aligned (16-B DMA pieces) and whose output is NHWC with 4-aligned channels; dev knob
-// NPS_X1_DMA=0: the register-staged kernels instead.
+// The DMA-stream 1x1 (conv1x1_dma_kernel) can take every split-fp16 1x1 with Cout <= 192 whose sources are
+// 4-channel aligned (16-B DMA pieces) and whose output is NHWC with 4-aligned channels.  Opt-in (dev knob
+// NPS_X1_DMA=1): measured at par with conv1x1_wl_kernel on the C3 shapes, slower with an addend epilogue
+// (profiles/r3/experiments/x1dma_*); both are bound by the epilogue's store issue.
 static bool x1_dma_on() {
     static int on = -1;
     if (on < 0) {
         const char* e = getenv("NPS_X1_DMA");
-        on = (e != nullptr && e[0] == '0') ? 0 : 1;
+        on = (e != nullptr && e[0] == '1') ? 1 : 0;
     }
     return on == 1;
 }

@@ -69,7 +69,7 @@ int main() {
     hipMemset(in, 0, ntiles * 196608);
     int ncu = 256;
     hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0);
-    for (int grid : {ncu, 2 * ncu}) {
+    for (int grid : {32, 64, 128, ncu}) {
         run<false, false>("coal", out, in, ntiles, sink, grid);
         run<true, false>("frag", out, in, ntiles, sink, grid);
         run<false, true>("coal_rd", out, in, ntiles, sink, grid);

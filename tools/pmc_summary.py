@@ -33,7 +33,7 @@ def klass(name):
     m = re.search(r"conv2d_x3_kernel<(\d+), \d+(?:, (?:true|false))*>", name)
     if m:
         return f"x3f16_{m.group(1)}tap"
-    if re.search(r"conv1x1_(?:x3|wl)_kernel<", name):
+    if re.search(r"conv1x1_(?:x3|wl|dma)_kernel<", name):
         return "x3f16_1tap"
     m = re.search(r"conv2d_pc_kernel<(\d+), \d+, \d+, \d+, \d+>", name)
     if m:
