@@ -112,6 +112,13 @@ typedef struct {
      * from `out`, without that pass.  Split-fp16 convs with NHWC output and Cout, out_C multiples of 4
      * only (1x1: Cout <= 192, bias-only epilogue); nps_conv2d_fwd refuses others. */
     double* out_stats;
+    /* The 4 output phases of a k4/s2 ConvTranspose2d in ONE launch (split-fp16 2x2 convs; 0 or 1 = a single
+     * conv): phase ph = 2 py + px uses the packed weight at wpack + ph * phase_wstride floats (its own
+     * power-of-2 scale in its trailer) and writes at out_off + (py, px) (out_os = 2).  The phases share
+     * the input patch: their work-groups are numbered phase-fastest on one XCD, so the patch is fetched
+     * from HBM once (replaces 4 launches of the Upsample, common.py:93-120). */
+    int nphase;
+    long phase_wstride;
 } nps_conv2d_t;
 
 /* Range tags (nps_conv2d_t.in_scale / in_tag* / out_tag): 64 sub-slots 256 B apart, so the atomics of

@@ -808,6 +808,8 @@ extern "C" int nps_conv2d_fwd(const nps_conv2d_t* ap, void* stream) {
     NPS_CHECK_ARG(a.out_stats == nullptr || (a.precision == NPS_PREC_X3F16 && (a.KH * a.KW != 1 || a.Cout <= 192) &&
                                              !a.out_nchw && (a.out_C & 3) == 0 && (a.Cout & 3) == 0),
                   "conv2d_fwd: out_stats needs a split-fp16 conv (1x1: Cout <= 192) with an NHWC, 4-aligned output");
+    NPS_CHECK_ARG(a.nphase <= 1 || a.precision == NPS_PREC_X3F16,
+                  "conv2d_fwd: merged transposed-conv phases (nphase > 1) need the split-fp16 kernel");
     const Geo g = make_geo(a);
     const int lds = lds_bytes(a);
     NPS_CHECK_ARG(lds <= 160 * 1024, "conv2d_fwd: LDS %d B too large", lds);

@@ -86,7 +86,8 @@ __host__ __device__ __forceinline__ bool x3_lds_epilogue(const nps_conv2d_t& a) 
 // the fused bias / addends / GELU / accumulate of store_tile, in the same float order.
 template <int TILE_PX, int NCO>
 __device__ __forceinline__ void x3_store_phase(const nps_conv2d_t& a, int b, int cob, int oy0, int ox0, int lat,
-                                               const float* T, int tid, float& amax) {
+                                               int ph, const float* T, int tid, float& amax) {
+    const int poy = a.out_off_y + (ph >> 1), pox = a.out_off_x + (ph & 1);  // transposed-conv phase offset
     constexpr int Q = NCO / 4;
     const bool st = a.out_stats != nullptr;
     double s1 = 0.0, s2 = 0.0;  // out_stats: fp64 sum / sum of squares of the stored values
@@ -96,7 +97,7 @@ __device__ __forceinline__ void x3_store_phase(const nps_conv2d_t& a, int b, int
         const int co0 = cob * NCO + q * 4;
         const int ti = P / a.TW, tj = P - (P / a.TW) * a.TW;
         const int oy = oy0 + ti * lat, ox = ox0 + tj * lat;  // lat: dilation-lattice step (1 unless dilated)
-        const int dy = oy * a.out_os + a.out_off_y, dx = ox * a.out_os + a.out_off_x;
+        const int dy = oy * a.out_os + poy, dx = ox * a.out_os + pox;
         if (co0 >= a.Cout || oy >= a.Hout || ox >= a.Wout || dy < 0 || dy >= a.out_H || dx < 0 || dx >= a.out_W)
             continue;
         const f32x4 acc = *reinterpret_cast<const f32x4*>(T + P * (NCO + 4) + q * 4);
@@ -151,13 +152,16 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
     const Geo g = make_geo(a);
     const int ncob = (a.Cout + NCO - 1) / NCO;
     const int ntiles = g.tiles_x * g.tiles_y;
-    const int nwg = ntiles * a.B * ncob;  // work-group tiles of the launch (the grid is persistent)
+    const int nph = a.nphase > 1 ? a.nphase : 1;  // transposed-conv phases in this launch
+    const int nwg = ntiles * a.B * ncob * nph;  // work-group tiles of the launch (the grid is persistent)
     // tile l -> (co block, sample, output origin): co block fastest; consecutive tiles of one XCD's
     // work-groups (l = i, i + G, ... with G % 8 == 0 stay on XCD i % 8) get consecutive numbers, so the 3
     // co-blocks of a tile and neighbouring tiles read the same patch bytes from that XCD's L2
-    auto decode = [&](int l, int& cob, int& b, int& oy0, int& ox0) {
+    auto decode = [&](int l, int& cob, int& b, int& oy0, int& ox0, int& ph) {
         const int full = nwg & ~7;
-        const int L = l < full ? (l & 7) * (full >> 3) + (l >> 3) : l;
+        const int L0 = l < full ? (l & 7) * (full >> 3) + (l >> 3) : l;
+        ph = L0 % nph;  // phase fastest: the phases of a tile share its patch bytes in one L2
+        const int L = L0 / nph;
         cob = L % ncob;
         const int rest = L / ncob;
         const int tile = rest % ntiles;
@@ -211,7 +215,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
         unsigned pixm = 0;  // slots whose pixel lies inside the current source
         unsigned finm = 0;  // slots whose pixel lies inside the (circularly extended) frame
         int cur_src = -1;
-        int fb = 0, fy0 = 0, fx0 = 0, fcob = 0;  // tile being fetched
+        int fb = 0, fy0 = 0, fx0 = 0, fcob = 0, fph = 0;  // tile being fetched
         auto locate = [&](int sidx) {
             const nps_src_t S0 = a.src[0], S1 = a.src[1], S2 = a.src[2];
             const float* sptr = sidx == 0 ? S0.ptr : (sidx == 1 ? S1.ptr : S2.ptr);
@@ -342,11 +346,11 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
         // every path), commits past the end skipped.  Barriers per tile: 1 + nstages + 2, as consumers.
         int l = blockIdx.x;
         float pmax = 0.f;  // max |stored value| of this thread's share of the store phases (out_tag)
-        decode(l, fcob, fb, fy0, fx0);
+        decode(l, fcob, fb, fy0, fx0, fph);
         unsigned m0 = issue(0, r0);
         unsigned m1 = issue(min(1, last), r1);
         for (;;) {
-            const int scob = fcob, sb = fb, soy0 = fy0, sox0 = fx0;  // tile being computed / stored
+            const int scob = fcob, sb = fb, soy0 = fy0, sox0 = fx0, sph = fph;  // tile being computed / stored
             commit(0, r0, m0);
             if (nstages > 1) commit(1, r1, m1);
             unsigned m = issue(min(2, last), r0);
@@ -359,14 +363,14 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
             const int ln = l + (int)gridDim.x;
             const bool more = ln < nwg;
             if (more) {  // the next tile's first two stages load while this tile is stored
-                decode(ln, fcob, fb, fy0, fx0);
+                decode(ln, fcob, fb, fy0, fx0, fph);
                 cur_src = -1;
                 m0 = issue(0, r0);
                 m1 = issue(min(1, last), r1);
             }
             barrier();  // the consumers' tile is in LDS
             if (lds_epi)
-                x3_store_phase<TILE_PX, NCO>(a, sb, scob, soy0, sox0, g.T, reinterpret_cast<const float*>(ring), tid,
+                x3_store_phase<TILE_PX, NCO>(a, sb, scob, soy0, sox0, g.T, sph, reinterpret_cast<const float*>(ring), tid,
                                              pmax);
             barrier();  // every read of the staged tile is done: the ring may be refilled
             if (!more) break;
@@ -459,15 +463,18 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
         }
         __builtin_amdgcn_sched_barrier(0);
     };
-    // epilogue scale: undo the exact power-of-2 scales of the weights and the input
-    const float inv = 1.f / (pow2_scale_for(a.wpack[packed_body(a.Cout, a.Cin, NTAPS)]) *
-                             ((PRO && a.gn_stats != nullptr) ? gn_prologue_scale(a) : in_scale_of(a)));
+    // epilogue scale: undo the power-of-2 scale of the input and of the phase's packed weight (its trailer)
+    const float xsc = (PRO && a.gn_stats != nullptr) ? gn_prologue_scale(a) : in_scale_of(a);
+    const size_t wbody = packed_body(a.Cout, a.Cin, NTAPS);
     const int h = lane >> 5;
     float amax = 0.f;  // max |stored value| over this thread's tiles (out_tag)
     for (int l = blockIdx.x; l < nwg; l += gridDim.x) {
         int cob, b, oy0, ox0;
-        decode(l, cob, b, oy0, ox0);
-        wbase = reinterpret_cast<const char*>(a.wpack) + (size_t)(cob * (NCO / 32) + cw0 / 32) * 2048 + lane * 16;
+        int ph;
+        decode(l, cob, b, oy0, ox0, ph);
+        const float* wph = a.wpack + (size_t)ph * a.phase_wstride;
+        const float inv = 1.f / (pow2_scale_for(wph[wbody]) * xsc);
+        wbase = reinterpret_cast<const char*>(wph) + (size_t)(cob * (NCO / 32) + cw0 / 32) * 2048 + lane * 16;
 #pragma unroll
         for (int i = 0; i < CBW; ++i)
 #pragma unroll
@@ -530,7 +537,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
             }
             barrier();
             X3_STAMP(8);
-            x3_store_phase<TILE_PX, NCO>(a, b, cob, oy0, ox0, g.T, T, tid, amax);
+            x3_store_phase<TILE_PX, NCO>(a, b, cob, oy0, ox0, g.T, ph, T, tid, amax);
             X3_STAMP(9);
         } else {
             static_for<PBW>([&](auto pbc) {  // compile-time pb: acc stays in registers
@@ -539,7 +546,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
                 const int ti = P / a.TW, tj = P - (P / a.TW) * a.TW;
                 const int oy = oy0 + ti * g.T, ox = ox0 + tj * g.T;
                 if (oy >= a.Hout || ox >= a.Wout) return;
-                const int dy = oy * a.out_os + a.out_off_y, dx = ox * a.out_os + a.out_off_x;
+                const int dy = oy * a.out_os + a.out_off_y + (ph >> 1), dx = ox * a.out_os + a.out_off_x + (ph & 1);
                 if (dy < 0 || dy >= a.out_H || dx < 0 || dx >= a.out_W) return;
 #pragma unroll
                 for (int cb = 0; cb < CBW; ++cb) {
@@ -1407,7 +1414,10 @@ extern "C" int nps_x3_set_grid(long wgs) {
 int nps_launch_conv2d_x3(const nps_conv2d_t& a, int lds, hipStream_t s) {
     const Geo g = make_geo(a);
     const bool wide = x3_wide_tile(a);  // 192-channel x 128-pixel work-groups (nps_conv2d_plan)
-    const long nwg = (long)g.tiles_x * g.tiles_y * a.B * ((a.Cout + (wide ? 191 : 63)) / (wide ? 192 : 64));
+    const long nwg = (long)g.tiles_x * g.tiles_y * a.B * ((a.Cout + (wide ? 191 : 63)) / (wide ? 192 : 64)) *
+                     (a.nphase > 1 ? a.nphase : 1);
+    NPS_CHECK_ARG(a.nphase <= 1 || (a.nphase == 4 && a.KH * a.KW == 4 && a.out_os == 2 && a.phase_wstride > 0),
+                  "conv2d_fwd (split-fp16): nphase = 4 is the k4/s2 transposed conv (2x2 phases, out_os 2)");
     NPS_CHECK_ARG(nwg < (1L << 31), "conv2d_fwd: grid too large");
     // persistent grid: one 512-thread work-group per CU (the LDS ring takes most of a CU), each walking
     // the tiles l = blockIdx.x, + gridDim.x, ...; a multiple of 8 keeps every work-group's tiles on one XCD

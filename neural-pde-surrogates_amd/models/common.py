@@ -151,6 +151,11 @@ class ConvTranspose2d(_PackedMixin, nn.ConvTranspose2d):
         out = ops.empty_nhwc(B, Ho, Wo, self.out_channels, x)
         phases = self._packed(ops.pack_convT_phases)
         st = ops.new_stats(B, x)  # the 4 phases store every output element once: GroupNorm(1) moments of out
+        if getattr(phases[0], "nps_precision", None) == ops.PREC_X3F16 and ops.MERGE_CONVT_PHASES:
+            # one launch: the phases' work-groups share each input patch (nps_conv2d_t.nphase)
+            ops.conv2d([ops.Src(x)], (H, W), phases[0], self.bias, self.out_channels, 2, 2, pad=(1, 1), circ=c,
+                       out_hw=(Hp + 1, Wp + 1), out=out, out_os=2, out_off=(-p, -p), act=act, out_stats=st, phases=4)
+            return ops.attach_stats(out, st)
         for ph in range(4):
             py, px = ph >> 1, ph & 1
             ops.conv2d([ops.Src(x)], (H, W), phases[ph], self.bias, self.out_channels, 2, 2, pad=(1, 1), circ=c,

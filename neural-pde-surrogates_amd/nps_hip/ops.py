@@ -24,6 +24,8 @@ PREC_F32, PREC_X3F16 = 0, 1
 FUSE_PROLOGUE = os.environ.get("NPS_FUSE_PROLOGUE", "1") == "1"
 CONV_PRECISION = PREC_F32 if os.environ.get("NPS_CONV_PRECISION", "x3f16") == "f32" else PREC_X3F16
 X1_LDS_WEIGHTS = os.environ.get("NPS_X3_1X1_WL", "1")[:1] != "0"  # (libnps_hip's dev knob of the same name)
+# split-fp16 transposed convs run their 4 phases in one launch (dev knob NPS_CONVT_MERGE=0: 4 launches)
+MERGE_CONVT_PHASES = os.environ.get("NPS_CONVT_MERGE", "1") == "1"
 
 
 def conv_precision(KH, KW, stride=1, dil=1):
@@ -296,10 +298,21 @@ def space_to_depth(x: torch.Tensor, pad: int, Hq: int, Wq: int) -> torch.Tensor:
 
 
 def pack_convT_phases(w: torch.Tensor) -> List[torch.Tensor]:
-    """nn.ConvTranspose2d(k=4, s=2) weight (Cin, Cout, 4, 4) -> 4 packed 2x2 phase convs."""
+    """nn.ConvTranspose2d(k=4, s=2) weight (Cin, Cout, 4, 4) -> 4 packed 2x2 phase convs, views of ONE buffer
+    (phase ph at ph * nps_phase_stride floats), so the split-fp16 kernel can run all 4 in one launch
+    (nps_conv2d_t.nphase, conv2d(phases=...))."""
     w = w.detach().contiguous()
     Cin, Cout = w.shape[0], w.shape[1]
-    return [_pack(w, Cout, Cin, 2, 2, ph, conv_precision(2, 2)) for ph in range(4)]
+    prec = conv_precision(2, 2)
+    n = lib.nps_conv2d_packed_size(Cout, Cin, 4)
+    buf = torch.cat([_pack(w, Cout, Cin, 2, 2, ph, prec) for ph in range(4)])
+    views = []
+    for ph in range(4):
+        v = buf[ph * n:(ph + 1) * n]
+        v.nps_precision = prec
+        v.nps_phase_stride = n
+        views.append(v)
+    return views
 
 
 def pack_spectral_weight(w1: torch.Tensor, w2: torch.Tensor, H: int) -> torch.Tensor:
@@ -346,11 +359,12 @@ def conv2d(srcs: Sequence[Src], frame_hw, wpack: torch.Tensor, bias: Optional[to
            KW: int, stride=1, dil=1, pad=(0, 0), circ=0, out_hw=None, gn: Optional[GN] = None, pre_act=0,
            out: Optional[torch.Tensor] = None, out_nchw=False, out_os=1, out_off=(0, 0), accumulate=False,
            addends: Sequence[torch.Tensor] = (), act=0, add_after_act=False, pad_bottom=None,
-           in_scale: Optional[torch.Tensor] = None, out_stats: Optional[torch.Tensor] = None):
+           in_scale: Optional[torch.Tensor] = None, out_stats: Optional[torch.Tensor] = None, phases: int = 1):
     """One fused conv launch.  `pad` = top/left zero padding (in the circularly
     extended frame), `pad_bottom` defaults to `pad`.  `out_stats`: a new_stats() buffer the launch adds
     the GroupNorm(1) moments of its stored values to (marked incomplete when this conv's kernel cannot;
-    attach_stats then ignores it).  Returns `out`."""
+    attach_stats then ignores it).  `phases` = 4: `wpack` is phase 0 of pack_convT_phases and the launch runs
+    all 4 transposed-conv phases, phase (py, px) written at out_off + (py, px) (split-fp16 only).  Returns `out`."""
     t0 = srcs[0].t
     B = t0.shape[0]
     Hin, Win = int(frame_hw[0]), int(frame_hw[1])
@@ -406,6 +420,10 @@ def conv2d(srcs: Sequence[Src], frame_hw, wpack: torch.Tensor, bias: Optional[to
     a.addend1 = ptr(ads[1]) if len(ads) > 1 else None
     a.act, a.add_after_act = act, (1 if add_after_act else 0)
     a.precision = getattr(wpack, "nps_precision", PREC_F32)
+    if phases > 1:
+        if a.precision != PREC_X3F16 or phases != 4 or out_os != 2:
+            raise ValueError("conv2d: merged transposed-conv phases need the split-fp16 2x2 packing and out_os 2")
+        a.nphase, a.phase_wstride = 4, wpack.nps_phase_stride
     reserve_tags(out.device, len(srcs) + 1)  # every tag this launch reads or writes, before any pointer
     if a.precision == PREC_X3F16:
         if in_scale is not None:  # explicit range (gradients): overrides the sources' tags
@@ -432,8 +450,9 @@ def conv2d(srcs: Sequence[Src], frame_hw, wpack: torch.Tensor, bias: Optional[to
         e0.record()
         check(lib.nps_conv2d_fwd(ctypes_byref(a), stream_ptr()), "conv2d_fwd")
         e1.record()
-        nbytes = 4.0 * (sum(s.t.numel() for s in srcs) + Cout * cin_alg * KH * KW + B * Hout * Wout * Cout)
-        conv_probe.append((e0, e1, 2.0 * B * Hout * Wout * Cout * cin_alg * KH * KW,
+        nph = max(phases, 1)
+        nbytes = 4.0 * (sum(s.t.numel() for s in srcs) + nph * (Cout * cin_alg * KH * KW + B * Hout * Wout * Cout))
+        conv_probe.append((e0, e1, 2.0 * nph * B * Hout * Wout * Cout * cin_alg * KH * KW,
                            ("x3f16" if a.precision == PREC_X3F16 else "f32", KH * KW, a.waves), nbytes))
         if conv_shape_log is not None:
             conv_shape_log.append(dict(cin=cin_alg, cout=Cout, k=(KH, KW), hw=(Hin, Win), out=(Hout, Wout), B=B,

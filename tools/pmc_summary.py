@@ -1,12 +1,11 @@
 """Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes per conv kernel class (dev tool).
 
-FETCH_SIZE scale per access shape, calibrated on this access pattern (tools/calib/pmc_calib.hip,
-profiles/r2s2/pmc_calib.txt): a wide coalesced 16 B/lane sweep reads 1 GiB and FETCH_SIZE reports 0.5 GiB
-(MI355X_MICROARCH.md § HBM: x 2), but the conv kernels' producers read 64 B (16 channels) of a pixel per
-stage — 64-B pieces of 128-B lines — and for that shape FETCH_SIZE reports the bytes 1:1 (0.5 GiB read,
-0.5 GiB reported, either half of the lines).  So the conv classes take FETCH x 1 (an upper bound: a
-64-B run that straddles two lines counts twice), every other kernel FETCH x 2.  Both counters are in KB
-(rocprofv3 derived metrics).
+FETCH_SIZE scale per access shape, calibrated on each access pattern (tools/calib/pmc_calib.hip,
+profiles/r3/pmc_calib.txt): a wide coalesced 16 B/lane sweep reads 1 GiB and FETCH_SIZE reports 0.5 GiB
+(MI355X_MICROARCH.md § HBM: x 2); so do LDS-DMA full-line reads and the 1x1 kernels' B operand (both 64-B
+halves of a line in one instruction); the 2x2/3x3/5x5 producers read ONE 64-B half of a pixel's line per
+stage and for that shape FETCH_SIZE reports the bytes 1:1.  WRITE_SIZE is 1:1 for coalesced and for
+MFMA-fragment stores.  Both counters are in KB (rocprofv3 derived metrics).
 usage: python tools/pmc_summary.py <fetch_dir> <write_dir> "<command>"
 """
 import csv
@@ -41,19 +40,33 @@ def klass(name):
     return None
 
 
+def fetch_scale(name):
+    """FETCH_SIZE -> bytes per access shape (tools/calib/pmc_calib.hip, profiles/r3/pmc_calib.txt): x 1 for the
+    patch producers of the 2x2 / 3x3 / 5x5 ring kernels (each stage reads one 64-B half of a pixel's 128-B
+    line, the other half a stage later: 1 GiB read, 1 GiB reported); x 2 for full 128-B lines read by one
+    instruction — 16 B/lane sweeps, LDS-DMA lines (conv1x1_dma_kernel) and the register-staged 1x1's B
+    operand (lane halves read both 64-B halves of a line in one instruction: 1 GiB read, 0.5 GiB reported)."""
+    c = klass(name)
+    if c is not None and c.startswith("x3f16_") and c != "x3f16_1tap":
+        return 1
+    return 2
+
+
 def main():
     fetch = load(sys.argv[1], "FETCH_SIZE")
     write = load(sys.argv[2], "WRITE_SIZE")
     out = {"command": sys.argv[3], "unit": "bytes per launch",
-           "note": "FETCH_SIZE x 1 for the conv classes (64-B-per-line producer reads, counted 1:1 on gfx950: "
-                   "tools/calib/pmc_calib.hip), x 2 for other kernels (16 B/lane sweeps, half-counted) + WRITE_SIZE, "
-                   "KB -> bytes; Infinity-Cache hits are counted by these fabric-side counters",
+           "note": "FETCH_SIZE x 1 for the 2x2/3x3/5x5 ring-kernel producers (64-B halves of 128-B lines read a "
+                   "stage apart, counted 1:1), x 2 for full-line reads by one instruction (16 B/lane sweeps, the "
+                   "1x1 kernels' B operand, LDS-DMA: half-counted), WRITE_SIZE x 1 (coalesced and MFMA-fragment "
+                   "stores both counted 1:1) — tools/calib/pmc_calib.hip, profiles/r3/pmc_calib.txt; KB -> bytes; "
+                   "Infinity-Cache hits are counted by these fabric-side counters",
            "kernels": {}}
     for name in sorted(set(fetch) | set(write)):
         fv, wv = fetch.get(name, []), write.get(name, [])
         if not fv or not wv:
             continue
-        fb = (1 if klass(name) else 2) * 1024 * sum(fv) / len(fv)
+        fb = fetch_scale(name) * 1024 * sum(fv) / len(fv)
         wb = 1024 * sum(wv) / len(wv)
         out["kernels"][name[:160]] = dict(launches=len(fv), fetch_bytes_per_launch=fb, write_bytes_per_launch=wb,
                                           hbm_bytes_per_launch=fb + wb, **({"class": klass(name)} if klass(name) else {}))
