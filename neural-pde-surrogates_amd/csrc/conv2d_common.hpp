@@ -285,7 +285,8 @@ __host__ __device__ inline int x3_region_bytes(const nps_conv2d_t& a) {
     const int tile = a.TH * a.TW * x3_tpitch(a) * 4;
     return ring > tile ? ring : tile;
 }
-inline int x3_lds_bytes(const nps_conv2d_t& a) { return 128 + x3_region_bytes(a); }  // 128-B header + region
+// 128-B header + region + the bias table of the LDS store phase (Cout floats, 16-B padded)
+inline int x3_lds_bytes(const nps_conv2d_t& a) { return 128 + x3_region_bytes(a) + ((a.Cout * 4 + 15) & ~15); }
 
 }  // namespace
 

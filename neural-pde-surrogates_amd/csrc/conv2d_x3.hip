@@ -76,6 +76,9 @@ __device__ __forceinline__ void static_for(F&& f) {
     }
 }
 
+// store target of the out-of-range items of the LDS store phase (never read)
+__device__ __attribute__((aligned(64))) float x3_sink[256];
+
 // NHWC output with 4-aligned channels: the epilogue goes through LDS (x3_store_phase)
 __host__ __device__ __forceinline__ bool x3_lds_epilogue(const nps_conv2d_t& a) {
     return !a.out_nchw && (a.out_C & 3) == 0 && (a.Cout & 3) == 0;
@@ -86,11 +89,52 @@ __host__ __device__ __forceinline__ bool x3_lds_epilogue(const nps_conv2d_t& a) 
 // the fused bias / addends / GELU / accumulate of store_tile, in the same float order.
 template <int TILE_PX, int NCO>
 __device__ __forceinline__ void x3_store_phase(const nps_conv2d_t& a, int b, int cob, int oy0, int ox0, int lat,
-                                               int ph, const float* T, int tid, float& amax) {
+                                               int ph, const float* T, const float* btab, int tid, float& amax) {
     const int poy = a.out_off_y + (ph >> 1), pox = a.out_off_x + (ph & 1);  // transposed-conv phase offset
     constexpr int Q = NCO / 4;
     const bool st = a.out_stats != nullptr;
     double s1 = 0.0, s2 = 0.0;  // out_stats: fp64 sum / sum of squares of the stored values
+    if (!a.accumulate && a.addend0 == nullptr && a.addend1 == nullptr) {
+        // No operand to read: the bias comes from the LDS table and out-of-range items store to a sink, so the
+        // loop holds no global load and no branch around a store.  (vmcnt retires loads and stores in one
+        // in-order queue; with a conditional store per item the compiler waited vmcnt(0) at every item —
+        // one store round trip each, 13-15k of a tile's ~115k cycles: DESIGN.md § Round 3.)
+#pragma unroll 4
+        for (int i = tid; i < TILE_PX * Q; i += 512) {
+            const int P = i / Q, q = i - (i / Q) * Q;
+            const int co0 = cob * NCO + q * 4;
+            const int ti = P / a.TW, tj = P - (P / a.TW) * a.TW;
+            const int oy = oy0 + ti * lat, ox = ox0 + tj * lat;
+            const int dy = oy * a.out_os + poy, dx = ox * a.out_os + pox;
+            const bool ok = !(co0 >= a.Cout || oy >= a.Hout || ox >= a.Wout || dy < 0 || dy >= a.out_H || dx < 0 ||
+                              dx >= a.out_W);
+            const f32x4 acc = *reinterpret_cast<const f32x4*>(T + P * (NCO + 4) + q * 4);
+            const f32x4 bi = *reinterpret_cast<const f32x4*>(btab + (ok ? co0 : 0));
+            f32x4 r;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float v = acc[e] + bi[e];
+                if (a.act == 1) v = nps::gelu_erf(v);
+                r[e] = v;
+                amax = ok ? fmaxf(amax, fabsf(v)) : amax;
+            }
+            float* dst = ok ? a.out + ((((size_t)b * a.out_H + dy) * a.out_W + dx) * a.out_C + co0)
+                            : x3_sink + 4 * (tid & 63);
+            *reinterpret_cast<f32x4*>(dst) = r;
+            if (st) {
+                float f1 = 0.f, f2 = 0.f;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    f1 += r[e];
+                    f2 += r[e] * r[e];
+                }
+                s1 += ok ? (double)f1 : 0.0;
+                s2 += ok ? (double)f2 : 0.0;
+            }
+        }
+        stats_publish(a, b, s1, s2);
+        return;
+    }
 #pragma unroll 4
     for (int i = tid; i < TILE_PX * Q; i += 512) {
         const int P = i / Q, q = i - (i / Q) * Q;
@@ -103,7 +147,7 @@ __device__ __forceinline__ void x3_store_phase(const nps_conv2d_t& a, int b, int
         const f32x4 acc = *reinterpret_cast<const f32x4*>(T + P * (NCO + 4) + q * 4);
         const size_t o = (((size_t)b * a.out_H + dy) * a.out_W + dx) * a.out_C + co0;
         const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-        const f32x4 bi = a.bias ? *reinterpret_cast<const f32x4*>(a.bias + co0) : z;
+        const f32x4 bi = *reinterpret_cast<const f32x4*>(btab + co0);
         const f32x4 a0 = a.addend0 ? *reinterpret_cast<const f32x4*>(a.addend0 + o) : z;
         const f32x4 a1 = a.addend1 ? *reinterpret_cast<const f32x4*>(a.addend1 + o) : z;
         const f32x4 ov = a.accumulate ? *reinterpret_cast<const f32x4*>(a.out + o) : z;
@@ -175,6 +219,10 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
     const int npix = g.PH * g.PW;
     const int stage_b = (npix * X3_PIXB + 15) & ~15;
     char* ring = reinterpret_cast<char*>(smem) + 128;
+    // bias table of the LDS store phase, behind the ring / tile region (x3_lds_bytes); first read after the
+    // first barrier of the tile loop
+    float* btab = reinterpret_cast<float*>(ring + x3_region_bytes(a));
+    for (int c = tid; c < a.Cout; c += 512) btab[c] = a.bias != nullptr ? a.bias[c] : 0.f;
     const int nstages = (a.Cin + CK - 1) / CK;
     const int last = nstages - 1;
     const bool lds_epi = x3_lds_epilogue(a);
@@ -187,15 +235,6 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
     if (wave >= 4) __builtin_amdgcn_s_setprio(1);
 #elif NPS_X3_PRIO == 2
     if (wave < 4) __builtin_amdgcn_s_setprio(1);
-#endif
-#if defined(NPS_X3_STAGGER) && NPS_X3_STAGGER > 1
-    // dev experiment: desynchronise the work-groups' store bursts — work-group group k (of NPS_X3_STAGGER,
-    // by XCD round) starts k/NPS_X3_STAGGER of a tile (NPS_X3_TILE_CYC cycles) late
-    if (WIDE && NTAPS == 9) {
-        const long dly = (long)((blockIdx.x >> 3) % NPS_X3_STAGGER) * NPS_X3_TILE_CYC / NPS_X3_STAGGER;
-        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-        while ((long)(__builtin_amdgcn_s_memtime() - t0) < dly) __builtin_amdgcn_s_sleep(8);
-    }
 #endif
     if (wave >= 4) {
         // ------------------------------------------------------------------ producers: patch only
@@ -370,7 +409,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
             }
             barrier();  // the consumers' tile is in LDS
             if (lds_epi)
-                x3_store_phase<TILE_PX, NCO>(a, sb, scob, soy0, sox0, g.T, sph, reinterpret_cast<const float*>(ring), tid,
+                x3_store_phase<TILE_PX, NCO>(a, sb, scob, soy0, sox0, g.T, sph, reinterpret_cast<const float*>(ring), btab, tid,
                                              pmax);
             barrier();  // every read of the staged tile is done: the ring may be refilled
             if (!more) break;
@@ -537,7 +576,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
             }
             barrier();
             X3_STAMP(8);
-            x3_store_phase<TILE_PX, NCO>(a, b, cob, oy0, ox0, g.T, ph, T, tid, amax);
+            x3_store_phase<TILE_PX, NCO>(a, b, cob, oy0, ox0, g.T, ph, T, btab, tid, amax);
             X3_STAMP(9);
         } else {
             static_for<PBW>([&](auto pbc) {  // compile-time pb: acc stays in registers
