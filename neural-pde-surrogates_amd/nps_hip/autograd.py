@@ -41,6 +41,19 @@ def wgrad(a: torch.Tensor, x: torch.Tensor, KH: int, KW: int, dil=1, pad=(0, 0),
     _, Hx, Wx, N = x.shape
     if g is None:
         g = torch.zeros((M, N, KH, KW), dtype=torch.float32, device=a.device)
+    if (ops.CONV_PRECISION == ops.PREC_X3F16 and KH == KW and KH <= 3 and dil == 1 and (M % 4 or N % 4)):
+        # channel counts off the split-fp16 kernel's 4-channel quads (the encoder's 81-channel input): zero-pad
+        # to a multiple of 4, run the split-fp16 weight gradient and add the real channels' block into g
+        def pad4(t):
+            c = t.shape[3]
+            if c % 4 == 0:
+                return t
+            tp = torch.zeros(t.shape[:3] + (c + (-c) % 4,), dtype=t.dtype, device=t.device)
+            tp[..., :c] = t
+            return tp
+        gp = wgrad(pad4(a), pad4(x), KH, KW, dil, pad, circ, None, None)
+        g += gp[:M, :N]
+        return g
     p = WgradArgs()
     p.a, p.B, p.Ha, p.Wa, p.M = ptr(a), B, Ha, Wa, M
     p.x, p.Hx, p.Wx, p.N = ptr(x), Hx, Wx, N

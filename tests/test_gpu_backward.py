@@ -100,6 +100,8 @@ WGRAD_X3_CASES = [
     (2, 64, 48, 3, 1, 0, 64, 64, 1e-4, 1e3),        # range: tiny gradients x large activations
     (2, 32, 40, 3, 1, 0, 24, 24, 1.5e5, 1e-3),      # range: gradients past fp16's max
     (3, 128, 128, 3, 0, 1, 96, 96, 1.0, 1.0),       # many pixel tiles per split
+    (2, 192, 81, 1, 0, 0, 32, 32, 1.0, 1.0),        # the encoder's 81-channel 1x1: zero-padded to 84
+    (2, 30, 22, 3, 1, 0, 20, 20, 1.0, 1.0),         # both channel counts off the 4-channel quads
 ]
 
 
