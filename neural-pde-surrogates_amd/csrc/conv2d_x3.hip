@@ -78,6 +78,9 @@ __device__ __forceinline__ void static_for(F&& f) {
 
 // store target of the out-of-range items of the LDS store phase (never read)
 __device__ __attribute__((aligned(64))) float x3_sink[256];
+// 64 zero bytes: the fetch address of B elements outside the frame or past the channel tail, so the
+// stage loop needs no masks (PMC: the 1x1 kernel issues 3-4k VALU instructions per wave)
+__device__ __attribute__((aligned(64))) float x3_zero16[16];
 
 // NHWC output with 4-aligned channels: the epilogue goes through LDS (x3_store_phase)
 __host__ __device__ __forceinline__ bool x3_lds_epilogue(const nps_conv2d_t& a) {
@@ -617,9 +620,6 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
 // K-groups — the packing (pack_weights_x3_kernel, ntaps == 1) orders the weights to match.  The
 // weights stream from L2 one stage ahead.  MFMA passes hi*hi, hi*lo, lo*hi as the ring kernel; the
 // epilogue goes through LDS (one contiguous channel run per pixel) or store_tile.
-// 64 zero bytes: the fetch address of B elements outside the frame or past the channel tail, so the
-// stage loop needs no masks (PMC: the 1x1 kernel issues 3-4k VALU instructions per wave)
-__device__ __attribute__((aligned(64))) float x3_zero16[16];
 
 template <int PB, int D>
 __global__ __launch_bounds__(512) void conv1x1_x3_kernel(const nps_conv2d_t a) {
@@ -962,6 +962,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
         for (int i = 0; i < WPT; ++i)
             *reinterpret_cast<f32x4*>(wl + buf * WSTAGE + (i * 256 + (int)threadIdx.x) * 16) = wr[i];
     };
+    if ((int)threadIdx.x < NCB * 32)  // the epilogue's bias table (zero past Cout), behind the first barrier
+        reinterpret_cast<float*>(wl + 2 * WSTAGE)[threadIdx.x] =
+            (a.bias != nullptr && (int)threadIdx.x < a.Cout) ? a.bias[threadIdx.x] : 0.f;
     f32x16 acc[NCB];
 #pragma unroll
     for (int i = 0; i < NCB; ++i)
@@ -1023,6 +1026,78 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     const int dy = oy * a.out_os + a.out_off_y, dx = ox * a.out_os + a.out_off_x;
     float amax = 0.f;
     const bool pout = P < npx && dy >= 0 && dy < a.out_H && dx >= 0 && dx < a.out_W;
+    if (x3_lds_epilogue(a) && a.addend1 == nullptr && !a.accumulate) {
+        // The fused epilogue in store_tile's float order (acc*inv + bias [+ a0 + a1] [GELU] [+ a0 + a1]
+        // [+ out]), the bias from the LDS table, every operand load issued before the stores it would
+        // otherwise queue behind, and no branch around a store (out-of-range quads go to a sink).  vmcnt
+        // retires loads and stores in one in-order queue, so a load issued after a store waits for it
+        // (DESIGN.md § Round 3); store_tile's per-block loads did exactly that.
+        const float* btab = reinterpret_cast<const float*>(wl + 2 * WSTAGE);
+        const size_t base = pout ? (((size_t)b * a.out_H + dy) * a.out_W + dx) * a.out_C : 0;
+        // per 32-channel block: apply the epilogue (its addend was loaded before the previous block's stores),
+        // load the next block's addend, store this block.  (Two addends or accumulate: store_tile below.)
+        double s1 = 0.0, s2 = 0.0;
+        auto epi = [&](auto opc) {
+            constexpr bool OP = decltype(opc)::value;
+            f32x4 a0[4];
+            auto load = [&](int cb) {
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    const int co0 = cb * 32 + 8 * m + 4 * h;
+                    const bool ok = pout && co0 < a.Cout;
+                    a0[m] = *reinterpret_cast<const f32x4*>(ok ? a.addend0 + base + co0 : x3_zero16);
+                }
+            };
+            if constexpr (OP) load(0);
+            static_for<NCB>([&](auto cbc) {
+                constexpr int cb = decltype(cbc)::value;
+                float f1 = 0.f, f2 = 0.f;  // out_stats (plain epilogue, host-checked): this block's moments
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    const int co0 = cb * 32 + 8 * m + 4 * h;
+                    const bool ok = pout && co0 < a.Cout;
+                    const f32x4 bi = *reinterpret_cast<const f32x4*>(btab + co0);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        float v = acc[cb][4 * m + e] * inv + bi[e];
+                        if constexpr (OP) {  // + a1 (0) as store_tile: v + a0 + 0 == v + a0
+                            if (!a.add_after_act) v = v + a0[m][e];
+                        }
+                        if (a.act == 1) v = nps::gelu_erf(v);
+                        if constexpr (OP) {
+                            if (a.add_after_act) v = v + a0[m][e];
+                        }
+                        acc[cb][4 * m + e] = v;
+                        amax = ok ? fmaxf(amax, fabsf(v)) : amax;
+                        f1 += ok ? v : 0.f;
+                        f2 += ok ? v * v : 0.f;
+                    }
+                }
+                s1 += (double)f1;
+                s2 += (double)f2;
+                if constexpr (OP && cb + 1 < NCB) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    load(cb + 1);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    const int co0 = cb * 32 + 8 * m + 4 * h;
+                    const bool ok = pout && co0 < a.Cout;
+                    const f32x4 r = {acc[cb][4 * m], acc[cb][4 * m + 1], acc[cb][4 * m + 2], acc[cb][4 * m + 3]};
+                    *reinterpret_cast<f32x4*>(ok ? a.out + base + co0 : x3_sink + 4 * lane) = r;
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            });
+        };
+        if (a.addend0 != nullptr)
+            epi(std::true_type{});
+        else
+            epi(std::false_type{});
+        nps::tag_publish(a.out_tag, amax, nps::wave_salt());
+        stats_publish(a, b, s1, s2);  // no-op without out_stats
+        return;
+    }
     if (pout) {
 #pragma unroll
         for (int cb = 0; cb < NCB; ++cb) {
@@ -1522,11 +1597,11 @@ int nps_launch_conv2d_x3(const nps_conv2d_t& a, int lds, hipStream_t s) {
             }
             const dim3 gw((unsigned)nb, a.B);
             if (wd == 2)
-                conv1x1_wl_kernel<6, 2><<<gw, 256, 2 * 2 * 6 * 2048, s>>>(a);
+                conv1x1_wl_kernel<6, 2><<<gw, 256, 2 * 2 * 6 * 2048 + 6 * 32 * 4, s>>>(a);
             else if (wd == 3)
-                conv1x1_wl_kernel<6, 3><<<gw, 256, 2 * 2 * 6 * 2048, s>>>(a);
+                conv1x1_wl_kernel<6, 3><<<gw, 256, 2 * 2 * 6 * 2048 + 6 * 32 * 4, s>>>(a);
             else
-                conv1x1_wl_kernel<6, 4><<<gw, 256, 2 * 2 * 6 * 2048, s>>>(a);
+                conv1x1_wl_kernel<6, 4><<<gw, 256, 2 * 2 * 6 * 2048 + 6 * 32 * 4, s>>>(a);
             NPS_CHECK_LAUNCH("conv2d_fwd (split-fp16 1x1, LDS weights)");
             return 0;
         }
