@@ -1145,6 +1145,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     }
 }
 
+#ifdef NPS_X1_DMA_KERNEL  // dev build only (tools/build_variant.sh -DNPS_X1_DMA_KERNEL): not in the default library
 // ---------------------------------------------------------------------------------------------
 // 1x1 as a persistent HBM stream: conv1x1_dma_kernel<NCB>.  A 1x1 conv moves (Cin + Cout) x 4 B per pixel
 // for 2 Cin Cout flops, so it is bound by how many bytes each CU keeps in flight, not by the MFMAs; the
@@ -1472,6 +1473,7 @@ __global__ __launch_bounds__(512) void conv1x1_dma_kernel(const nps_conv2d_t a) 
     X3_RSTAMP(9);
 #endif
 }
+#endif  // NPS_X1_DMA_KERNEL
 
 template <int NT, int PB, bool PRO = false, bool WIDE = false>
 void launch_x3_one(const nps_conv2d_t& a, unsigned nwg, int lds, hipStream_t s) {
@@ -1484,6 +1486,7 @@ void launch_x3_one(const nps_conv2d_t& a, unsigned nwg, int lds, hipStream_t s) 
     conv2d_x3_kernel<NT, PB, PRO, WIDE><<<nwg, 512, lds, s>>>(a);
 }
 
+#ifdef NPS_X1_DMA_KERNEL
 template <int NCB>
 void launch_x1d(const nps_conv2d_t& a, unsigned grid, hipStream_t s) {
     static bool attr_set = false;
@@ -1494,14 +1497,18 @@ void launch_x1d(const nps_conv2d_t& a, unsigned grid, hipStream_t s) {
     }
     conv1x1_dma_kernel<NCB><<<grid, 512, x1d_lds_bytes(NCB), s>>>(a);
 }
+#endif
 
 }  // namespace
 
 // The DMA-stream 1x1 (conv1x1_dma_kernel) can take every split-fp16 1x1 with Cout <= 192 whose sources are
-// 4-channel aligned (16-B DMA pieces) and whose output is NHWC with 4-aligned channels.  Opt-in (dev knob
-// NPS_X1_DMA=1): measured at par with conv1x1_wl_kernel on the C3 shapes, slower with an addend epilogue
+// 4-channel aligned (16-B DMA pieces) and whose output is NHWC with 4-aligned channels.  Opt-in (a dev build
+// with -DNPS_X1_DMA_KERNEL, then the knob NPS_X1_DMA=1): measured at par with conv1x1_wl_kernel on the C3 shapes, slower with an addend epilogue
 // (profiles/r3/experiments/x1dma_*); both are bound by the epilogue's store issue.
 static bool x1_dma_on() {
+#ifndef NPS_X1_DMA_KERNEL
+    return false;  // the kernel is not in this build
+#endif
     static int on = -1;
     if (on < 0) {
         const char* e = getenv("NPS_X1_DMA");
@@ -1558,6 +1565,7 @@ int nps_launch_conv2d_x3(const nps_conv2d_t& a, int lds, hipStream_t s) {
     // stages match the 1x1 weight packing; work-group = min(ncob, 8) waves, blockIdx.z = 512-channel group
     if (a.KH * a.KW == 1) {
         NPS_CHECK_ARG(!pro, "conv2d_fwd (split-fp16): 1x1 prologue");
+#ifdef NPS_X1_DMA_KERNEL
         if (x1_dma_ok(a)) {
             const int ncb = (a.Cout + 31) / 32;
             const long ntiles = (((long)a.Hout * a.Wout + 127) / 128) * a.B;
@@ -1572,6 +1580,7 @@ int nps_launch_conv2d_x3(const nps_conv2d_t& a, int lds, hipStream_t s) {
             NPS_CHECK_LAUNCH("conv2d_fwd (split-fp16 1x1, DMA stream)");
             return 0;
         }
+#endif
         static int cfg = -1;  // dev knob NPS_X3_1X1_CFG: 0 = (PB 2, D 2), 1 = (1, 4), 2 = (1, 2)
         if (cfg < 0) {
             const char* e = getenv("NPS_X3_1X1_CFG");

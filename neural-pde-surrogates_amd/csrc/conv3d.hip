@@ -451,7 +451,7 @@ __global__ __launch_bounds__(256) void gn_stats3d_kernel(const nps_conv3d_t a, i
             const bool vec = (src.C & 7) == 0;
             const bool inside = src.off_d >= 0 && src.off_h >= 0 && src.off_w >= 0 && src.off_d + src.D <= a.Dc &&
                                 src.off_h + src.H <= a.Hc && src.off_w + src.W <= a.Wc;
-            if (vec && inside && (cpg & 7) == 0) {
+            if (vec && inside && (cpg & 7) == 0 && (lo & 7) == 0) {  // 8-aligned pieces: one group each
                 // the source lies wholly inside the frame: a linear sweep of its 8-channel pieces, the group of
                 // a piece from its channel chunk (no voxel decomposition)
                 for (int it = blockIdx.x * 256 + threadIdx.x; it < nitem; it += gridDim.x * 256) {
@@ -494,7 +494,7 @@ __global__ __launch_bounds__(256) void gn_stats3d_kernel(const nps_conv3d_t a, i
                         if (ck * 8 + e < src.C) v.load_elem(e, p + e);
                 }
                 const int c0 = lo + ck * 8;
-                if (vec && (cpg & 7) == 0) {  // the 8 channels lie in one group
+                if (vec && (cpg & 7) == 0 && (lo & 7) == 0) {  // the 8 channels lie in one group
                     const int g0 = c0 / cpg;
                     float fs = 0.f, fq = 0.f;
 #pragma unroll

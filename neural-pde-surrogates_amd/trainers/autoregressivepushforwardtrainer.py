@@ -102,7 +102,8 @@ class AutoregressivePushforwardTrainer(TrainInterface):
                                           "nn.MSELoss(reduction='sum' | 'mean') criteria only")
             from trainers.distributed import global_sqrt_loss
             s_local = ad.mse_sum(pred, labels) if pred.is_cuda else torch.sum((pred - labels) ** 2)
-            return global_sqrt_loss(s_local, pred.numel() if c.reduction == "mean" else None)
+            return global_sqrt_loss(s_local, pred.numel() if c.reduction == "mean" else None,
+                                    grad_scale=self.grad_world_scale)
         if isinstance(c, nn.MSELoss) and c.reduction == "sum" and pred.is_cuda:
             return ad.sqrt_mse_sum(pred, labels)
         return torch.sqrt(c(pred, labels))

@@ -81,12 +81,20 @@ class TrainInterface:
         self.max_test_batches = max_test_batches
         self.epoch_callback = epoch_callback
         self.world, self.rank = _dist()
-        if self.world > 1 and grad_sync is None:
+        # the per-rank training loss is the rank's share of the global-batch loss (distributed.global_sqrt_loss);
+        # its gradients are right when the ranks SUM them.  A reducer that averages — GradAllReducer(average=True),
+        # or grad_sync=False with the caller's own torch DDP wrapper (which averages) — gets the share's gradient
+        # scaled by the world size, so every documented option trains the 1-process model.
+        self.grad_world_scale = 1.0
+        if self.world > 1:
             # data parallelism wired here, so an unchanged train.py under torchrun trains one model
             from trainers.distributed import GradAllReducer, sync_python_random
-            grad_sync = GradAllReducer(self.model.parameters())
-            grad_sync.broadcast_parameters(0)
-            sync_python_random()
+            sync_python_random()  # every rank draws rank 0's unroll depths / start steps, whatever the reducer
+            if grad_sync is None:
+                grad_sync = GradAllReducer(self.model.parameters())
+                grad_sync.broadcast_parameters(0)
+            if grad_sync is False or getattr(grad_sync, "average", False):
+                self.grad_world_scale = float(self.world)
         self.grad_sync = grad_sync if grad_sync is not False else None
         self.print_setting = getattr(self.config, "print_setting", dict(print_per_step=False))
         self.use_wandb = bool(use_wandb) and WANDB_AVAILABLE

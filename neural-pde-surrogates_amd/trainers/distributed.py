@@ -20,7 +20,7 @@ those of the 1-process run.
 Buckets are filled in reverse parameter order (the order backward produces
 gradients) and each is launched as one asynchronous all-reduce the moment its
 last gradient is accumulated, so RCCL's ring over xGMI overlaps the rest of
-backward; `finish()` waits and writes the averaged gradients back.  Buckets are
+backward; `finish()` waits and writes the reduced (summed) gradients back.  Buckets are
 launched strictly in index order so every rank issues the same collective
 sequence.  Complex parameters (SpectralConv2d weights1/weights2) are reduced as
 their float32 (re, im) pairs, the sum of which is the sum of the complex values.
@@ -47,12 +47,15 @@ def world_and_rank(group=None):
     return 1, 0
 
 
-def global_sqrt_loss(s_local: torch.Tensor, count_local: Optional[int] = None, group=None) -> torch.Tensor:
+def global_sqrt_loss(s_local: torch.Tensor, count_local: Optional[int] = None, group=None,
+                     grad_scale: float = 1.0) -> torch.Tensor:
     """sqrt of a sum over the GLOBAL batch from this rank's part of it, with this rank's share of the
     global gradient.  Value: sqrt(S) (or sqrt(S / N) with element counts, nn.MSELoss(reduction='mean')),
     S = Σ_r s_r all-reduced in fp64 before backward.  Gradient: ∇s_local / (2·sqrt(S)) (/ N) — the
     ranks' gradients, summed by GradAllReducer, are ∇sqrt(S) of the 1-process step on the concatenated
-    batch (autoregressivepushforwardtrainer.py:158-162: loss = torch.sqrt(criterion(pred, labels)))."""
+    batch (autoregressivepushforwardtrainer.py:158-162: loss = torch.sqrt(criterion(pred, labels))).
+    grad_scale multiplies the gradient only (not the value): the world size when the gradients are
+    AVERAGED instead of summed (GradAllReducer(average=True), torch DDP)."""
     world, _ = world_and_rank(group)
     tot = s_local.detach().to(torch.float64).reshape(1).clone()
     if count_local is not None:
@@ -64,7 +67,7 @@ def global_sqrt_loss(s_local: torch.Tensor, count_local: Optional[int] = None, g
     root = torch.sqrt(S)
     out_dtype = torch.float32 if s_local.dtype == torch.float64 else s_local.dtype
     # value root; d/ds_local = scale / (2 root)
-    share = (s_local - s_local.detach()).to(torch.float64) * (scale / (2.0 * root))
+    share = (s_local - s_local.detach()).to(torch.float64) * (scale * grad_scale / (2.0 * root))
     return (root + share).to(out_dtype).reshape(s_local.shape)
 
 

@@ -63,14 +63,14 @@ def _shard(batch, lo, hi):
     return tuple(t[lo:hi] for t in batch)
 
 
-def _trainer(model, batch_size):
+def _trainer(model, batch_size, grad_sync=None):
     from common.interfaces import D
     from trainers import AutoregressivePushforwardTrainer
     data = argparse.Namespace(data_interface=D.sim2d, pde=None, train=None, valid=None, test=None)
     config = argparse.Namespace(device="cpu", batch_size=batch_size, time_window=TW, base_resolution=(T, H, W),
                                 neighbors=3, lr_step_interval=1, unrolling=2, nr_gt_steps=1, num_epochs=1)
     return AutoregressivePushforwardTrainer(model=model, data=data, criterion=torch.nn.MSELoss(reduction="sum"),
-                                            config=config, save_path="unused")
+                                            config=config, save_path="unused", grad_sync=grad_sync)
 
 
 def _run(tr, train_loader, val_loader):
@@ -83,15 +83,24 @@ def _run(tr, train_loader, val_loader):
     return float(ep_loss), grads, params, float(val_loss), {k: float(v) for k, v in metrics.items()}
 
 
-def _worker(rank, world, init_file, q, done):
+def _worker(rank, world, init_file, q, done, mode="auto"):
     _paths()
     dist.init_process_group("gloo", init_method="file://" + init_file, rank=rank, world_size=world)
     torch.set_num_threads(1)
     torch.manual_seed(100 + rank)       # rank 1 builds different parameters: the trainer broadcasts rank 0's
     random.seed(1000 + rank)            # ... and a different Python RNG state: the trainer broadcasts rank 0's
     model = _GridToy()
-    tr = _trainer(model, GLOBAL_B // world)
-    assert tr.grad_sync is not None and not tr.grad_sync.average
+    if mode == "average":
+        # an explicit, AVERAGING reducer ("an explicit grad_sync replaces it"): the caller
+        # broadcasts the parameters; the trainer still syncs the Python RNG and scales the loss share's gradient
+        from trainers.distributed import GradAllReducer
+        gs = GradAllReducer(model.parameters(), average=True)
+        gs.broadcast_parameters(0)
+        tr = _trainer(model, GLOBAL_B // world, grad_sync=gs)
+        assert tr.grad_sync is gs and tr.grad_world_scale == world
+    else:
+        tr = _trainer(model, GLOBAL_B // world)
+        assert tr.grad_sync is not None and not tr.grad_sync.average and tr.grad_world_scale == 1
     b = _global_batch()
     lo, hi = rank * GLOBAL_B // world, (rank + 1) * GLOBAL_B // world
     train_loader = [_shard(b, lo, hi), _shard(_global_batch(seed=2), lo, hi)]
@@ -103,12 +112,13 @@ def _worker(rank, world, init_file, q, done):
     dist.destroy_process_group()
 
 
-def test_ddp_train_step_equals_one_process_global_batch(tmp_path):
+@pytest.mark.parametrize("mode", ["auto", "average"])
+def test_ddp_train_step_equals_one_process_global_batch(tmp_path, mode):
     world = 2
     ctx = mp.get_context("spawn")
     q, done = ctx.Queue(), ctx.Event()
     init_file = str(tmp_path / "pg_init")
-    procs = [ctx.Process(target=_worker, args=(r, world, init_file, q, done)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, init_file, q, done, mode)) for r in range(world)]
     for p in procs:
         p.start()
     try:

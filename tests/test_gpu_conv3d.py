@@ -91,6 +91,24 @@ def test_conv3d_gn_prologue_on_crop_frame(dt):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("inside", [True, False])
+def test_gn_stats3d_groups_across_unaligned_sources(dt, inside):
+    """GroupNorm(2) moments of a [4 | 8 | 4]-channel frame (8 channels per group): the 8-channel source starts at
+    channel 4, so each of its 8-channel pieces spans both groups — the per-element path, not the one-group-per-
+    piece fast paths (for a source inside the frame and for a cropped one)."""
+    from nps_hip import ops
+    torch.manual_seed(5)
+    B, dhw = 2, (4, 6, 10)
+    xs = [torch.randn(B, c, *dhw) + k for k, c in enumerate((4, 8, 4))]
+    offs = [(0, 0, 0), (0, 0, 0) if inside else (0, -1, 1), (0, 0, 0)]
+    fr = _frame([(_rt(x, dt), o) for x, o in zip(xs, offs)], B, dhw)
+    st = ops.gn_stats3d([ops.Src3(_ndhwc(x, dt), *o) for x, o in zip(xs, offs)], dhw, 2).cpu()
+    g = fr.view(B, 2, 8, *dhw)
+    torch.testing.assert_close(st[:, :, 0], g.sum((2, 3, 4, 5)), rtol=1e-6, atol=1e-3)
+    torch.testing.assert_close(st[:, :, 1], (g ** 2).sum((2, 3, 4, 5)), rtol=1e-6, atol=1e-3)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
 def test_conv3d_residual_accumulate_and_final_crop(dt):
     """ResidualBlock tail: conv2 accumulated at crop offset (2, 2, 2) into the 1x1 shortcut output; and the
     U-Net final GroupNorm(8) + GELU + 1x1 conv written at a negative crop offset with addend + GELU

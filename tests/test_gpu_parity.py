@@ -339,6 +339,51 @@ def test_c1_unet_cfg_simulate_golden():
     assert rel_l2(torch.stack([l.cpu() for l in losses]), g["sim_losses"]) < TOL
 
 
+@pytest.mark.parametrize("name", ["ufno", "unet", "drn"])
+def test_native_geometry_simulate_golden(name):
+    """The geometry an unchanged train.py feeds the drop-in: every twophase cfg sets base_resolution
+    (501, 96, 64) (reference cfg_twophase_ufno.py:6-7).  The full-width cfg model (U-FNO hidden 192 / U-Net
+    hidden 32 ch_mults [2,2,1,2] / DRN hidden 128), num_c = 1, B = 2, through the mirror's simulate on the GPU at
+    t_res = 110 — 3 calls, the partial last window skipped as at autoregressivepushforwardtrainer.py:354-358 —
+    against the reference's own simulate (tests/golden/make_golden_native.py), every window and every loss."""
+    import argparse
+    import types
+    from common.interfaces import D
+    from trainers.autoregressivepushforwardtrainer import AutoregressivePushforwardTrainer
+    from native_fixture import native_golden, native_inputs, native_model
+    g = native_golden(name)
+    u, cond, pos, sc = (t.to(DEV) for t in native_inputs(g))
+    m, pde = native_model(g)
+    m = m.to(DEV)
+    tw, T = g["cfg"]["time_window"], u.shape[2]
+    cfg = argparse.Namespace(time_window=tw, base_resolution=(T, u.shape[3], u.shape[4]), device=DEV, nr_gt_steps=1)
+    tr = AutoregressivePushforwardTrainer(model=m, data=types.SimpleNamespace(pde=pde, data_interface=D.sim2d),
+                                          criterion=nn.MSELoss(reduction="sum"), config=cfg)
+    with torch.no_grad():
+        losses, (gt, preds) = tr.simulate(u, cond, pos, compute_loss=True, include_data=True, nr_gt_steps=1, t_res=T,
+                                          spatial_conditioning=sc)
+    assert len(preds) == 4
+    for k in range(3):
+        assert rel_l2(preds[k + 1].cpu(), g["sim_pred"][:, :, k * tw:(k + 1) * tw]) < TOL, k
+    assert rel_l2(torch.stack([l.cpu() for l in losses]), g["sim_losses"]) < TOL
+
+
+def test_drn_c4_full_size_one_call():
+    """BASELINE C4: the cfg_twophase_drn model (DilatedResnet hidden 128, k 5, 2 blocks, dilations
+    1,2,4,8,4,2,1, circular; decoder kernel 5) at 256x256, 1 field, B=1 — one rollout model call vs the CPU
+    oracle (cf. test_ufno_c3_full_size_one_call)."""
+    import __graft_entry__  # noqa: F401
+    from bench import build_model
+    from trainers.synthetic import twophase_batch
+    m, ocfg, opde = build_model("drn", res=256, num_c=1, device=DEV)
+    u, cond, pos, sc = twophase_batch(1, 1, 25, 256, 256, seed=13, obstacle="disc")
+    with torch.no_grad():
+        y = m(u.to(DEV), cond=cond.to(DEV), bc=None, pos=pos.to(DEV), t_cond=None, spatial_cond=sc.to(DEV)).cpu()
+    ref = oracle.build_oracle_model(ocfg, opde, {k: v.cpu() for k, v in m.state_dict().items()})(
+        u, cond=cond, pos=pos, spatial_cond=sc)
+    assert rel_l2(y, ref) < TOL
+
+
 def test_ufno_c2_full_size_one_call():
     """BASELINE C2: U-FNO twophase cfg with 12 Fourier modes (hidden 192, 3 blocks) at 128x128, 1 field,
     B=2 — one rollout model call vs the CPU oracle (cf. test_ufno_c3_full_size_one_call)."""
