@@ -10,7 +10,12 @@ from conftest import load_golden
 
 
 def _checksums(sd):
-    return {k: torch.stack([v.detach().double().sum(), (v.detach().double() ** 2).sum()]) for k, v in sd.items()}
+    out = {}
+    for k, v in sd.items():
+        v = v.detach()
+        v = (torch.view_as_real(v) if v.is_complex() else v).double()  # both parts of complex weights count
+        out[k] = torch.stack([v.sum(), (v ** 2).sum()])
+    return out
 
 
 def assert_checksums(got, want, what):

@@ -45,7 +45,9 @@ def checksums(sd):
     import torch
     out = {}
     for k, v in sd.items():
-        v = v.detach().to(torch.float64)
+        v = v.detach()
+        v = torch.view_as_real(v) if v.is_complex() else v  # both parts of complex weights count
+        v = v.to(torch.float64)
         out[k] = torch.stack([v.sum(), (v * v).sum()])
     return out
 
