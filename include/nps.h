@@ -119,6 +119,14 @@ typedef struct {
      * from HBM once (replaces 4 launches of the Upsample, common.py:93-120). */
     int nphase;
     long phase_wstride;
+    /* Space-to-depth view (split-fp16 2x2 convs, one source, no prologue; 0 = off): the frame (Hin x Win x
+     * Cin, Cin = 4 C) is the space-to-depth of src[0] (H x W x C, C % 16 == 0): frame pixel (y, x) channel
+     * p C + c reads src[0] pixel (2 y + (p >> 1) - s2d_pad, 2 x + (p & 1) - s2d_pad) channel c, zero outside.
+     * The U-Net Downsample's valid 3x3/s2 conv with padding s2d_pad (proc_unet_modern.py:439-455) runs as
+     * a 2x2 stride-1 conv over this view (weight from nps_conv2d_pack_weights_x3 with transposed_phase = -2)
+     * without materialising the space-to-depth copy. */
+    int s2d;
+    int s2d_pad;
 } nps_conv2d_t;
 
 /* Range tags (nps_conv2d_t.in_scale / in_tag* / out_tag): 64 sub-slots 256 B apart, so the atomics of

@@ -785,7 +785,12 @@ extern "C" int nps_conv2d_fwd(const nps_conv2d_t* ap, void* stream) {
         NPS_CHECK_ARG(a.src[s].ptr && a.src[s].C > 0 && a.src[s].H > 0 && a.src[s].W > 0, "conv2d_fwd: bad src %d", s);
         csum += a.src[s].C;
     }
-    NPS_CHECK_ARG(csum == a.Cin, "conv2d_fwd: Cin=%d != sum of source channels %d", a.Cin, csum);
+    NPS_CHECK_ARG(csum * (a.s2d ? 4 : 1) == a.Cin, "conv2d_fwd: Cin=%d != sum of source channels %d%s", a.Cin, csum,
+                  a.s2d ? " x 4 (space-to-depth view)" : "");
+    NPS_CHECK_ARG(!a.s2d || (a.precision == NPS_PREC_X3F16 && a.nsrc == 1 && a.KH == 2 && a.KW == 2 && a.stride == 1 &&
+                             a.dil == 1 && a.circ == 0 && !a.gn_stats && !a.pre_act && (a.src[0].C & 15) == 0 &&
+                             a.src[0].off_y == 0 && a.src[0].off_x == 0 && a.nphase <= 1),
+                  "conv2d_fwd: the space-to-depth view is for split-fp16 2x2 convs of one 16-channel-aligned source");
     NPS_CHECK_ARG(a.B > 0 && a.Hout > 0 && a.Wout > 0 && a.Cout > 0 && a.wpack && a.out, "conv2d_fwd: bad shape");
     NPS_CHECK_ARG(a.KH > 0 && a.KW > 0 && a.stride > 0 && a.dil > 0, "conv2d_fwd: bad kernel geometry");
     NPS_CHECK_ARG(!a.gn_stats || (a.gn_groups > 0 && a.gn_groups <= 16 && a.Cin % a.gn_groups == 0 && a.gn_gamma &&

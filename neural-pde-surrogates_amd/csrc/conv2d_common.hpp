@@ -268,21 +268,30 @@ inline bool x3_sources_aligned(const nps_conv2d_t& a) {
 
 // The wide split-fp16 tile (192 output channels x 128 pixels per work-group, nps_conv2d_plan): 2x2 / 3x3
 // convs with 128 < Cout <= 192 (Cout % 32 == 0), planned as 128-pixel tiles.
+// Wide tiles always end in the LDS store phase (NHWC output with 4-aligned channels): the wide kernels carry
+// no register-direct epilogue, whose register demand spilled them.
 inline bool x3_wide_eligible(const nps_conv2d_t& a) {
     const int nt = a.KH * a.KW;
     return (nt == 4 || nt == 9) && a.Cout > 128 && a.Cout <= 192 && (a.Cout & 31) == 0 && a.dil == 1 &&
-           a.stride == 1 && !a.lattice;
+           a.stride == 1 && !a.lattice && !a.out_nchw && (a.out_C & 3) == 0;
 }
 __host__ __device__ inline bool x3_wide_tile(const nps_conv2d_t& a) { return a.TH * a.TW == 128; }
 
 // floats per pixel of the LDS-staged output tile: the work-group's channels + 4 (pad)
 __host__ __device__ inline int x3_tpitch(const nps_conv2d_t& a) { return (x3_wide_tile(a) ? 192 : 64) + 4; }
 
-// bytes of the split-fp16 kernel's patch ring / epilogue tile region (they share it)
-__host__ __device__ inline int x3_region_bytes(const nps_conv2d_t& a) {
+// bytes of the split-fp16 kernel's patch ring
+__host__ __device__ inline int x3_ring_bytes(const nps_conv2d_t& a) {
     const Geo g = make_geo(a);
-    const int ring = X3_NST * ((g.PH * g.PW * X3_PIXB + 15) & ~15);
+    return X3_NST * ((g.PH * g.PW * X3_PIXB + 15) & ~15);
+}
+// bytes of the patch ring + epilogue tile region: 64-channel tiles reuse the ring for the tile (store phase
+// after the main loop); wide tiles keep the tile in a region of its own behind the ring, because their
+// consumer waves store tile t during tile t + 1's main loop (conv2d_x3_kernel, "spread store")
+__host__ __device__ inline int x3_region_bytes(const nps_conv2d_t& a) {
+    const int ring = x3_ring_bytes(a);
     const int tile = a.TH * a.TW * x3_tpitch(a) * 4;
+    if (x3_wide_tile(a)) return ring + tile;
     return ring > tile ? ring : tile;
 }
 // 128-B header + region + the bias table of the LDS store phase (Cout floats, 16-B padded)

@@ -43,7 +43,13 @@ __host__ __device__ constexpr int x3_patch_px_max(int ntaps, int tile_px) {
 #define NPS_X3_REMAP 0
 #endif
 #ifndef NPS_X3_ARING
-#define NPS_X3_ARING 2
+#define NPS_X3_ARING 2  // weight-fragment ring depth of the 64-channel tiles
+#endif
+#ifndef NPS_X3_ARING_WIDE
+#define NPS_X3_ARING_WIDE 2  // ... of the wide tiles (3 fits without the spread store, not with it)
+#endif
+#ifndef NPS_X3_ABL
+#define NPS_X3_ABL 0  // dev ablations of the 3x3 main loop (tools/x3_abl.sh); 0 in every shipped build
 #endif
 // Producer slot -> (patch pixel, channel quad).  REMAP: the 16 lanes of one ds_write_b64 group take
 // pixels {0, 2, 4, 6} (lanes 16-31: {1, 3, 5, 7}) of a run of 8, whose 32-B [hi] / [lo] runs at the 80-B
@@ -228,7 +234,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
     for (int c = tid; c < a.Cout; c += 512) btab[c] = a.bias != nullptr ? a.bias[c] : 0.f;
     const int nstages = (a.Cin + CK - 1) / CK;
     const int last = nstages - 1;
-    const bool lds_epi = x3_lds_epilogue(a);
+    const bool lds_epi = WIDE || x3_lds_epilogue(a);  // wide tiles: always (x3_wide_eligible)
     auto barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
 
     // static priority for the producer half (MI355X_MICROARCH 'Two waves per SIMD' item 4): they win the
@@ -244,6 +250,8 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
         const int ptid = tid - 256;
         const int Hext = a.Hin + 2 * a.circ, Wext = a.Win + 2 * a.circ;
         const float xs = (PRO && a.gn_stats != nullptr) ? gn_prologue_scale(a) : in_scale_of(a);
+        // 1 / (elements per GroupNorm group), once per launch
+        const double gn_icnt = (PRO && a.gn_stats != nullptr) ? 1.0 / ((double)(a.Cin / a.gn_groups) * a.Hin * a.Win) : 0.0;
         // a register set: MAXP patch slots, then (PRO) the stage's GroupNorm operands gamma[4], beta[4]
         // and the group's (sum, sum of squares) as two doubles, fetched with the patch
         constexpr int NR = MAXP + (PRO ? 3 : 0);
@@ -260,13 +268,18 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
         int fb = 0, fy0 = 0, fx0 = 0, fcob = 0, fph = 0;  // tile being fetched
         auto locate = [&](int sidx) {
             const nps_src_t S0 = a.src[0], S1 = a.src[1], S2 = a.src[2];
-            const float* sptr = sidx == 0 ? S0.ptr : (sidx == 1 ? S1.ptr : S2.ptr);
-            const int sC = sidx == 0 ? S0.C : (sidx == 1 ? S1.C : S2.C);
-            const int sH = sidx == 0 ? S0.H : (sidx == 1 ? S1.H : S2.H);
-            const int sW = sidx == 0 ? S0.W : (sidx == 1 ? S1.W : S2.W);
-            const int soy = sidx == 0 ? S0.off_y : (sidx == 1 ? S1.off_y : S2.off_y);
-            const int sox = sidx == 0 ? S0.off_x : (sidx == 1 ? S1.off_x : S2.off_x);
+            const int si = a.s2d ? 0 : sidx;  // (the view's parities all read src[0])
+            const float* sptr = si == 0 ? S0.ptr : (si == 1 ? S1.ptr : S2.ptr);
+            const int sC = si == 0 ? S0.C : (si == 1 ? S1.C : S2.C);
+            const int sH = si == 0 ? S0.H : (si == 1 ? S1.H : S2.H);
+            const int sW = si == 0 ? S0.W : (si == 1 ? S1.W : S2.W);
+            const int soy = si == 0 ? S0.off_y : (si == 1 ? S1.off_y : S2.off_y);
+            const int sox = si == 0 ? S0.off_x : (si == 1 ? S1.off_x : S2.off_x);
             const int ybase = fy0 - a.pad_y, xbase = fx0 - a.pad_x;
+            // space-to-depth view (a.s2d): sidx is the view's parity p, the source is src[0] at (2 y + (p >> 1)
+            // - s2d_pad, 2 x + (p & 1) - s2d_pad)
+            const int s2m = a.s2d ? 2 : 1;
+            const int s2y = a.s2d ? (sidx >> 1) - a.s2d_pad : 0, s2x = a.s2d ? (sidx & 1) - a.s2d_pad : 0;
             pixm = 0;
             finm = 0;
 #pragma unroll
@@ -279,7 +292,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
                 finm = ok ? (finm | (1u << k)) : finm;
                 const int fy = a.circ ? nps::wrap_mod(ye - a.circ, a.Hin) : ye;
                 const int fx = a.circ ? nps::wrap_mod(xe - a.circ, a.Win) : xe;
-                const int yy = fy - soy, xx = fx - sox;
+                const int yy = fy * s2m + s2y - soy, xx = fx * s2m + s2x - sox;
                 ok = ok && yy >= 0 && yy < sH && xx >= 0 && xx < sW;
                 sbase[k] = sptr + (ok ? ((size_t)(fb * sH + yy) * sW + xx) * sC : (size_t)fb * sH * sW * sC);
                 pixm = ok ? (pixm | (1u << k)) : pixm;
@@ -290,7 +303,10 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
             const int c0 = st * CK;
             const int cend = min(c0 + CK, a.Cin);
             int sidx = 0, cbase = 0;
-            {
+            if (a.s2d) {  // space-to-depth view: the stage's parity (C % 16 == 0: one parity per stage)
+                sidx = c0 / a.src[0].C;
+                cbase = sidx * a.src[0].C;
+            } else {
                 int lo = 0;
 #pragma unroll
                 for (int si = 0; si < NPS_MAX_SRC; ++si) {  // unrolled: static kernarg indexing
@@ -334,19 +350,26 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
         };
         auto commit = [&](int st, const f32x4 (&rp)[NR], unsigned okm) {
             char* Pt = ring + (st % X3_NST) * stage_b;
-            float mean = 0.f, rstd = 0.f;
+            // GroupNorm as one FMA per element, y = x * gs + gb with gs = rstd * gamma, gb = beta - mean * gs
+            // (the form PyTorch's GroupNorm kernel evaluates): the group moments -> (mean, rstd) once per stage
+            // and lane (fp64 moments, one fp64 reciprocal of the count per launch, v_rsq_f32), not per element
+            f32x4 gs = {1.f, 1.f, 1.f, 1.f}, gb = {0.f, 0.f, 0.f, 0.f};
             if constexpr (PRO) {
                 if (a.gn_stats != nullptr) {  // as frame_pack_kernel / the reference's GroupNorm
                     const f32x4 sv = rp[MAXP + 2];
                     double s1, s2;
                     __builtin_memcpy(&s1, &sv, 8);
                     __builtin_memcpy(&s2, reinterpret_cast<const char*>(&sv) + 8, 8);
-                    const double cnt = (double)(a.Cin / a.gn_groups) * a.Hin * a.Win;
-                    const double mu = s1 / cnt;
-                    double var = s2 / cnt - mu * mu;
+                    const double mu = s1 * gn_icnt;
+                    double var = fma(s2, gn_icnt, -mu * mu);
                     var = var < 0.0 ? 0.0 : var;
-                    mean = (float)mu;
-                    rstd = (float)(1.0 / sqrt(var + (double)a.gn_eps));
+                    const float mean = (float)mu;
+                    const float rstd = __builtin_amdgcn_rsqf((float)(var + (double)a.gn_eps));
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        gs[e] = rstd * rp[MAXP][e];
+                        gb[e] = fmaf(-mean, gs[e], rp[MAXP + 1][e]);
+                    }
                 }
             }
 #pragma unroll
@@ -360,8 +383,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
                         if ((okm >> (16 + k)) & 1u) {
                             if (a.gn_stats != nullptr) {
 #pragma unroll
-                                for (int e = 0; e < 4; ++e)
-                                    v[e] = (v[e] - mean) * rstd * rp[MAXP][e] + rp[MAXP + 1][e];
+                                for (int e = 0; e < 4; ++e) v[e] = fmaf(v[e], gs[e], gb[e]);
                             }
                             if (a.pre_act == 1) {
 #pragma unroll
@@ -391,6 +413,45 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
         decode(l, fcob, fb, fy0, fx0, fph);
         unsigned m0 = issue(0, r0);
         unsigned m1 = issue(min(1, last), r1);
+        if constexpr (WIDE) {
+            // Wide tiles: the consumers store each tile during the next one's main loop, so the producers have
+            // no store phase: per tile 1 + nstages barriers, and the next tile's first two stages are fetched
+            // into r0 / r1 by the last stage iterations of this one (where the fetch of stage st + 3 would run
+            // past the end), then committed as soon as the last stage's barrier frees the ring.
+            for (;;) {
+                commit(0, r0, m0);
+                if (nstages > 1) commit(1, r1, m1);
+                unsigned m = issue(min(2, last), r0);
+                barrier();
+                const int ln = l + (int)gridDim.x;
+                const bool more = ln < nwg;
+                bool got0 = false, got1 = false;
+                for (int st = 0; st < nstages; ++st) {
+                    if (st + 2 < nstages) commit(st + 2, r0, m);
+                    if (st + 3 <= last) {
+                        m = issue(st + 3, r0);
+                    } else if (more && st == last - 2) {  // r0 is free after the commit of stage `last`
+                        decode(ln, fcob, fb, fy0, fx0, fph);
+                        cur_src = -1;
+                        m0 = issue(0, r0);
+                        got0 = true;
+                    } else if (got0 && st == last - 1) {  // r1 has been free since this tile's top
+                        m1 = issue(min(1, last), r1);
+                        got1 = true;
+                    }
+                    barrier();
+                }
+                if (!more) break;
+                if (!got0) {
+                    decode(ln, fcob, fb, fy0, fx0, fph);
+                    cur_src = -1;
+                    m0 = issue(0, r0);
+                }
+                if (!got1) m1 = issue(min(1, last), r1);
+                l = ln;
+            }
+            return;
+        }
         for (;;) {
             const int scob = fcob, sb = fb, soy0 = fy0, sox0 = fx0, sph = fph;  // tile being computed / stored
             commit(0, r0, m0);
@@ -398,6 +459,10 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
             unsigned m = issue(min(2, last), r0);
             barrier();
             for (int st = 0; st < nstages; ++st) {
+#if NPS_X3_ABL == 4  // dev ablation: the producers only keep the barriers (stale patch)
+                barrier();
+                continue;
+#endif
                 if (st + 2 < nstages) commit(st + 2, r0, m);
                 m = issue(min(st + 3, last), r0);
                 barrier();
@@ -438,7 +503,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
     const int G = nstages * NTAPS;
     const char* wbase = nullptr;
     // weight fragments: a ring of NPS_X3_ARING K-groups (2: loaded one K-group ahead; 3: two ahead)
-    constexpr int AR = NPS_X3_ARING;
+    constexpr int AR = WIDE ? NPS_X3_ARING_WIDE : NPS_X3_ARING;
     f16x8 Aw[AR][CBW][2];
     f16x8 Bh[2][PBW], Bl[2][PBW];
     auto loadA = [&](int gg, f16x8 (&d)[CBW][2]) {
@@ -466,8 +531,86 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
 #ifdef NPS_X3_STAMP
     unsigned long long bar_cycles = 0;  // consumer wave 0: cycles spent in the stage barriers
 #endif
-    auto group = [&](int gg, const int ra, const int r) {  // ra: weight slot of K-group gg, r: patch slot
+    // Spread store (wide tiles): wave w drops its own 96-channel x 64-pixel block of tile t into the epilogue
+    // tile region Tw (behind the ring), then stores that block during tile t + 1's main loop, one 64-lane item
+    // (16 B per lane: one pixel's 4 channels) every sp_every K-groups — no store phase, no barrier (a wave only
+    // ever reads back the block it wrote), and the output write stream is spread over the main loop instead of
+    // every CU bursting 96 KiB at once.  The item's epilogue is x3_store_phase's (bias from the LDS table,
+    // addends, GELU, accumulate, range tag, GroupNorm moments, same float order); its operand loads are issued
+    // before the K-group's MFMAs and consumed after them.
+    constexpr int SPQ = 24;                  // channel quads of a wave's 96-channel block
+    constexpr int SP_ITEMS = 64 * SPQ / 64;  // 64 pixels x 24 quads / 64 lanes
+    float* Tw = reinterpret_cast<float*>(ring + x3_ring_bytes(a));
+    const int tw_sh = __builtin_ctz((unsigned)a.TW);  // wide tiles: TW in {4, 8, 16, 32}
+    const bool sp_oper = a.accumulate || a.addend0 != nullptr || a.addend1 != nullptr;
+    int sp_n = 0, sp_next = 0, sp_every = 1;  // items left of the pending tile, next K-group with an item
+    int sp_b = 0, sp_cob = 0, sp_oy0 = 0, sp_ox0 = 0, sp_ph = 0;
+    double sp_s1 = 0.0, sp_s2 = 0.0;
+    float sp_amax = 0.f;
+    f32x4 sp_v, sp_a0, sp_a1, sp_ov;
+    size_t sp_off = 0;
+    int sp_co0 = 0;
+    bool sp_ok = false;
+    auto sp_issue = [&]() __attribute__((always_inline)) {
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        const int i = (SP_ITEMS - sp_n) * 64 + lane;
+        const int Pl = i / SPQ, q = i - (i / SPQ) * SPQ;
+        const int P = px0 + Pl, col = cw0 + 4 * q;
+        sp_co0 = sp_cob * NCO + col;
+        const int oy = sp_oy0 + (P >> tw_sh), ox = sp_ox0 + (P & (a.TW - 1));
+        const int dy = oy * a.out_os + a.out_off_y + (sp_ph >> 1), dx = ox * a.out_os + a.out_off_x + (sp_ph & 1);
+        sp_ok = sp_co0 < a.Cout && oy < a.Hout && ox < a.Wout && dy >= 0 && dy < a.out_H && dx >= 0 && dx < a.out_W;
+        sp_off = sp_ok ? (((size_t)sp_b * a.out_H + dy) * a.out_W + dx) * a.out_C + sp_co0 : 0;
+        sp_v = *reinterpret_cast<const f32x4*>(Tw + P * (NCO + 4) + col);
+        sp_a0 = z;
+        sp_a1 = z;
+        sp_ov = z;
+        if (sp_oper) {  // out-of-range lanes read the zero page
+            if (a.addend0 != nullptr)
+                sp_a0 = *reinterpret_cast<const f32x4*>(sp_ok ? a.addend0 + sp_off : x3_zero16);
+            if (a.addend1 != nullptr)
+                sp_a1 = *reinterpret_cast<const f32x4*>(sp_ok ? a.addend1 + sp_off : x3_zero16);
+            if (a.accumulate) sp_ov = *reinterpret_cast<const f32x4*>(sp_ok ? a.out + sp_off : x3_zero16);
+        }
+    };
+    auto sp_finish = [&]() __attribute__((always_inline)) {
+        const f32x4 bi = *reinterpret_cast<const f32x4*>(btab + (sp_ok ? sp_co0 : 0));
+        f32x4 r;
+        float f1 = 0.f, f2 = 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {  // x3_store_phase's float order
+            float v = sp_v[e] + bi[e];
+            if (!a.add_after_act) v = v + sp_a0[e] + sp_a1[e];
+            if (a.act == 1) v = nps::gelu_erf(v);
+            if (a.add_after_act) v = v + sp_a0[e] + sp_a1[e];
+            if (a.accumulate) v += sp_ov[e];
+            r[e] = v;
+            sp_amax = sp_ok ? fmaxf(sp_amax, fabsf(v)) : sp_amax;
+            f1 += a.accumulate ? v - sp_ov[e] : v;
+            f2 += a.accumulate ? (v - sp_ov[e]) * (v + sp_ov[e]) : v * v;
+        }
+        if (a.out_stats != nullptr) {
+            sp_s1 += sp_ok ? (double)f1 : 0.0;
+            sp_s2 += sp_ok ? (double)f2 : 0.0;
+        }
+        float* dst = sp_ok ? a.out + sp_off : x3_sink + 4 * lane;
+        *reinterpret_cast<f32x4*>(dst) = r;
+        if (--sp_n == 0) stats_publish(a, sp_b, sp_s1, sp_s2);  // the tile's moments: one pair per wave
+    };
+    auto group = [&](int gg, const int ra, const int r) __attribute__((always_inline)) {  // ra: weight slot of K-group gg, r: patch slot
+        bool sp = false;
+        if constexpr (WIDE) {
+            sp = sp_n > 0 && gg >= sp_next;  // uniform
+            if (sp) sp_issue();
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#if NPS_X3_ABL == 1  // dev ablation (wrong results, speed only): every K-group reads group 0's weights (L1-hot)
+        loadA(0, Aw[(ra + AR - 1) % AR]);
+#elif NPS_X3_ABL == 2  // dev ablation: waves 2, 3 read group 0's weights (L1-hot), waves 0, 1 the real stream
+        loadA(wave >= 2 ? 0 : gclamp(gg + AR - 1), Aw[(ra + AR - 1) % AR]);
+#else
         loadA(gclamp(gg + AR - 1), Aw[(ra + AR - 1) % AR]);
+#endif
         loadB(gclamp(gg + 1), Bh[r ^ 1], 0);
         loadB(gclamp(gg + 1), Bl[r ^ 1], 1);
 #pragma unroll
@@ -494,6 +637,13 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
         }
         __builtin_amdgcn_sched_group_barrier(0x008, 3 * CBW * PBW - 2 * PBW - 2 * CBW, 0);
         __builtin_amdgcn_sched_barrier(0);
+        if constexpr (WIDE) {
+            if (sp) {
+                sp_finish();
+                sp_next += sp_every;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
         if ((gg + 1) % NTAPS == 0) {
 #ifdef NPS_X3_STAMP
             const unsigned long long t0 = __builtin_amdgcn_s_memtime();
@@ -561,6 +711,39 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
         if (wave == 0 && lane == 0 && l < (1 << 16)) x3_stamps[l * 16 + 6] = bar_cycles;
         bar_cycles = 0;
 #endif
+        if constexpr (WIDE) {
+            // items of the previous tile the main loop had no K-group for (small Cin), then this tile's block
+            // into Tw: the wave's own block only, which it alone reads back — no barrier
+            while (sp_n > 0) {
+                sp_issue();
+                sp_finish();
+            }
+#pragma unroll
+            for (int pb = 0; pb < PBW; ++pb) {
+                const int P = px0 + pb * 32 + (lane & 31);
+#pragma unroll
+                for (int cb = 0; cb < CBW; ++cb)
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) {
+                        const f32x4 v = {acc[cb][pb][4 * m] * inv, acc[cb][pb][4 * m + 1] * inv,
+                                         acc[cb][pb][4 * m + 2] * inv, acc[cb][pb][4 * m + 3] * inv};
+                        *reinterpret_cast<f32x4*>(Tw + P * (NCO + 4) + cw0 + cb * 32 + 8 * m + 4 * h) = v;
+                    }
+            }
+            sp_n = SP_ITEMS;
+            sp_b = b;
+            sp_cob = cob;
+            sp_oy0 = oy0;
+            sp_ox0 = ox0;
+            sp_ph = ph;
+            sp_s1 = sp_s2 = 0.0;
+            sp_next = 0;
+            // the next tile (same Cin, so the same G) stores one item every sp_every K-groups
+            sp_every = G > SP_ITEMS ? (G - 1) / (SP_ITEMS - 1) : 1;
+            X3_STAMP(3);
+            X3_RSTAMP(5);
+            continue;
+        }
         if (lds_epi) {
             // the ring is free (every read of it completed before the last stage barrier): the consumers
             // drop the 64 x TILE_PX tile into LDS, then all 8 waves store it with coalesced 16-B accesses
@@ -581,7 +764,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
             X3_STAMP(8);
             x3_store_phase<TILE_PX, NCO>(a, b, cob, oy0, ox0, g.T, ph, T, btab, tid, amax);
             X3_STAMP(9);
-        } else {
+        } else if constexpr (!WIDE) {
             static_for<PBW>([&](auto pbc) {  // compile-time pb: acc stays in registers
                 constexpr int pb = decltype(pbc)::value;
                 const int P = px0 + pb * 32 + (lane & 31);
@@ -604,6 +787,13 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
         barrier();  // the staged tile is fully read: the producers may refill the ring
         X3_STAMP(3);
         X3_RSTAMP(5);
+    }
+    if constexpr (WIDE) {  // the last tile: no next main loop to spread it over
+        while (sp_n > 0) {
+            sp_issue();
+            sp_finish();
+        }
+        amax = fmaxf(amax, sp_amax);
     }
     nps::tag_publish(a.out_tag, amax, nps::wave_salt());
 }

@@ -110,12 +110,16 @@ class Conv2d(_PackedMixin, nn.Conv2d):
             p = lo[0]
             Ho = (frame_hw[0] + 2 * p - 3) // 2 + 1
             Wo = (frame_hw[1] + 2 * p - 3) // 2 + 1
-            xq = ops.space_to_depth(x, p, Ho + 1, Wo + 1)
             wk = self.weight
             key = ("s2d", wk.data_ptr(), wk._version, str(wk.device), ops.CONV_PRECISION)
             if getattr(self, "_pk2_key", None) != key:
                 self._pk2 = ops.pack_conv_weight_s2d(wk)
                 self._pk2_key = key
+            if ops.S2D_VIEW and x.shape[3] % 16 == 0 and self._pk2.nps_precision == ops.PREC_X3F16:
+                # the split-fp16 producers read the space-to-depth view straight from x (nps_conv2d_t.s2d)
+                return ops.conv2d([ops.Src(x)], (Ho + 1, Wo + 1), self._pk2, self.bias, self.out_channels, 2, 2,
+                                  out_hw=(Ho, Wo), s2d_pad=p, **kw)
+            xq = ops.space_to_depth(x, p, Ho + 1, Wo + 1)
             return ops.conv2d([ops.Src(xq)], (Ho + 1, Wo + 1), self._pk2, self.bias, self.out_channels, 2, 2,
                               out_hw=(Ho, Wo), **kw)
         return ops.conv2d(srcs, frame_hw, self._packed(lambda w: ops.pack_conv_weight(w, s, d)), self.bias,

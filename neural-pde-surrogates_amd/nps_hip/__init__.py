@@ -48,7 +48,7 @@ class Conv2dArgs(ctypes.Structure):
         ("TH", ctypes.c_int), ("TW", ctypes.c_int), ("lattice", ctypes.c_int), ("waves", ctypes.c_int),
         ("precision", ctypes.c_int), ("in_scale", ctypes.c_void_p), ("in_tag1", ctypes.c_void_p),
         ("in_tag2", ctypes.c_void_p), ("out_tag", ctypes.c_void_p), ("out_stats", ctypes.c_void_p),
-        ("nphase", ctypes.c_int), ("phase_wstride", ctypes.c_long),
+        ("nphase", ctypes.c_int), ("phase_wstride", ctypes.c_long), ("s2d", ctypes.c_int), ("s2d_pad", ctypes.c_int),
     ]
 
 

@@ -24,6 +24,9 @@ PREC_F32, PREC_X3F16 = 0, 1
 FUSE_PROLOGUE = os.environ.get("NPS_FUSE_PROLOGUE", "1") == "1"
 CONV_PRECISION = PREC_F32 if os.environ.get("NPS_CONV_PRECISION", "x3f16") == "f32" else PREC_X3F16
 X1_LDS_WEIGHTS = os.environ.get("NPS_X3_1X1_WL", "1")[:1] != "0"  # (libnps_hip's dev knob of the same name)
+# the Downsample's 2x2 conv reads the space-to-depth view of its input directly (nps_conv2d_t.s2d) instead of
+# a space_to_depth copy (dev knob NPS_S2D_VIEW=0: the copy)
+S2D_VIEW = os.environ.get("NPS_S2D_VIEW", "1") == "1"
 # split-fp16 transposed convs run their 4 phases in one launch (dev knob NPS_CONVT_MERGE=0: 4 launches)
 MERGE_CONVT_PHASES = os.environ.get("NPS_CONVT_MERGE", "1") == "1"
 
@@ -359,16 +362,24 @@ def conv2d(srcs: Sequence[Src], frame_hw, wpack: torch.Tensor, bias: Optional[to
            KW: int, stride=1, dil=1, pad=(0, 0), circ=0, out_hw=None, gn: Optional[GN] = None, pre_act=0,
            out: Optional[torch.Tensor] = None, out_nchw=False, out_os=1, out_off=(0, 0), accumulate=False,
            addends: Sequence[torch.Tensor] = (), act=0, add_after_act=False, pad_bottom=None,
-           in_scale: Optional[torch.Tensor] = None, out_stats: Optional[torch.Tensor] = None, phases: int = 1):
+           in_scale: Optional[torch.Tensor] = None, out_stats: Optional[torch.Tensor] = None, phases: int = 1,
+           s2d_pad: Optional[int] = None):
     """One fused conv launch.  `pad` = top/left zero padding (in the circularly
     extended frame), `pad_bottom` defaults to `pad`.  `out_stats`: a new_stats() buffer the launch adds
     the GroupNorm(1) moments of its stored values to (marked incomplete when this conv's kernel cannot;
     attach_stats then ignores it).  `phases` = 4: `wpack` is phase 0 of pack_convT_phases and the launch runs
-    all 4 transposed-conv phases, phase (py, px) written at out_off + (py, px) (split-fp16 only).  Returns `out`."""
+    all 4 transposed-conv phases, phase (py, px) written at out_off + (py, px) (split-fp16 only).  `s2d_pad`:
+    the frame (frame_hw, 4 C channels) is the space-to-depth view of the single source srcs[0] (C % 16 == 0)
+    with that padding (nps_conv2d_t.s2d; the Downsample's 3x3/s2 conv as a 2x2 conv).  Returns `out`."""
     t0 = srcs[0].t
     B = t0.shape[0]
     Hin, Win = int(frame_hw[0]), int(frame_hw[1])
     Cin = sum(s.t.shape[3] for s in srcs)
+    if s2d_pad is not None:
+        if len(srcs) != 1 or Cin % 16 or gn is not None or pre_act or KH != 2 or KW != 2:
+            raise ValueError("conv2d: the space-to-depth view takes one 16-channel-aligned source, a 2x2 kernel, "
+                             "no prologue")
+        Cin *= 4
     cin_alg = Cin  # algorithmic input channels (before any zero channel padding)
     x3 = getattr(wpack, "nps_precision", PREC_F32) == PREC_X3F16
     aligned = not x3 or lib.nps_conv2d_x3_sources_ok(_c_src(srcs), len(srcs))
@@ -403,6 +414,8 @@ def conv2d(srcs: Sequence[Src], frame_hw, wpack: torch.Tensor, bias: Optional[to
     a.nsrc = len(srcs)
     a.src = _c_src(srcs)
     a.B, a.Hin, a.Win, a.Cin = B, Hin, Win, Cin
+    if s2d_pad is not None:
+        a.s2d, a.s2d_pad = 1, int(s2d_pad)
     if gn is not None:
         a.gn_stats, a.gn_gamma, a.gn_beta = ptr(gn.stats), ptr(gn.gamma), ptr(gn.beta)
         a.gn_groups, a.gn_eps = gn.groups, gn.eps

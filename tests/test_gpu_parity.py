@@ -27,6 +27,9 @@ CONV_CASES = [
     (7, 5, 3, 1, 1, 1, "zeros", 17, 13),            # zero pad, odd channels (scalar gather path)
     (12, 12, 3, 2, 1, 0, "zeros", 31, 29),          # downsample s2 valid
     (12, 40, 3, 2, 1, 1, "zeros", 16, 16),          # downsample s2 pad 1
+    (32, 40, 3, 2, 1, 0, "zeros", 31, 29),          # downsample s2 valid, space-to-depth view (C % 16 == 0)
+    (48, 192, 3, 2, 1, 1, "zeros", 27, 30),         # downsample s2 pad 1, view, wide tile
+    (192, 192, 3, 2, 1, 0, "zeros", 65, 64),        # U-FNO Downsample shape, view
     (8, 8, 5, 1, 2, "same", "circular", 24, 24),    # DRN dilated circular
     (8, 8, 5, 1, 8, "same", "circular", 20, 20),    # dilation 8 > tile lattice
     (132, 128, 5, 1, 4, "same", "circular", 40, 36),
@@ -54,6 +57,26 @@ def test_conv2d_vs_torch(case):
     y = m.to(DEV)(x.to(DEV)).cpu()
     assert y.shape == ref.shape
     assert rel_l2(y, ref) < TOL
+
+
+@pytest.mark.parametrize("C,Cout,p,H,W", [(32, 40, 0, 31, 29), (192, 192, 0, 65, 64), (64, 192, 1, 20, 23)])
+def test_downsample_s2d_view_equals_copy(C, Cout, p, H, W):
+    """The Downsample's 2x2 conv reading the space-to-depth view of its input (nps_conv2d_t.s2d) gives the same
+    values as the same conv over the materialised space_to_depth copy (same kernel, same operands)."""
+    from models.common import Conv2d
+    from nps_hip import ops
+    torch.manual_seed(3)
+    m = Conv2d(C, Cout, 3, stride=2, padding=p).to(DEV)
+    x = ops.nchw_to_nhwc(torch.randn(2, C, H, W, device=DEV))
+    old = ops.S2D_VIEW
+    try:
+        ops.S2D_VIEW = True
+        y_view = m.run([ops.Src(x)], x.shape[1:3]).cpu()
+        ops.S2D_VIEW = False
+        y_copy = m.run([ops.Src(x)], x.shape[1:3]).cpu()
+    finally:
+        ops.S2D_VIEW = old
+    assert rel_l2(y_view, y_copy) < 1e-7
 
 
 @pytest.mark.parametrize("circ", [True, False])
