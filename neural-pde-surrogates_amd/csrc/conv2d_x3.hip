@@ -799,6 +799,456 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
 }
 
 
+// tile coordinates of conv2d_x3f_kernel
+struct X3Tile {
+    int cob, b, oy0, ox0, ph;
+};
+
+// ---------------------------------------------------------------------------------------------
+// Wide split-fp16 2x2 / 3x3 conv with fused roles: conv2d_x3f_kernel<NTAPS, PRO>.  The same 192-channel x
+// 128-pixel tiles, patch ring, weight stream and spread store as conv2d_x3_kernel<NTAPS, 2, PRO, true>, but
+// 4 waves (one per SIMD, up to 512 registers each) that are producers AND consumers: every wave stages a
+// quarter of the patch and computes its 96-channel x 64-pixel block.  In the 8-wave kernel the producer wave
+// and the MFMA wave of a SIMD compete for its instruction issue (the producer's fetch / GroupNorm / GELU /
+// split / LDS-write stream costs the MFMA stream 17-24 %: dev ablation NPS_X3_ABL=4, profiles/r4); here the
+// producer work of a stage is cut into NU units (half a patch slot each) placed inside the stage's K-groups,
+// each unit's ~50 VALU between that group's 18 MFMAs (`sched_group_barrier`: 1 MFMA, 3 VALU), where a wave's
+// own VALU issues in the MFMA pipe's shadow.  The stage stream runs across tiles: ring slot = stream stage %
+// 3, so the next tile's first stages are fetched and committed during this tile's last ones (no per-tile
+// producer prologue).  Three register sets, set = stream stage % 3: during stage s the units commit stage s + 2
+// and the last K-group fetches stage s + 4 (a full stage of lead); the fetch goes out after that group's
+// weight loads, because vmcnt retires in order and every weight load issued after it waits for it too.  The
+// loop body is three stages, so the sets are compile-time.
+template <int NTAPS, bool PRO>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void conv2d_x3f_kernel(
+    const nps_conv2d_t a) {
+    constexpr int KWT = NTAPS == 9 ? 3 : 2;
+    constexpr int CBW = 3, PBW = 2, NCO = 192;
+    constexpr int MAXP = (x3_patch_px_max(NTAPS, 128) * 4 + 255) / 256;  // patch slots per thread per stage
+    constexpr int RG = NTAPS == 9 ? 3 : 2;  // operand ring depth in K-groups (divides NTAPS)
+    constexpr int NU = 2 * MAXP;            // producer units per stage
+    static_assert(NTAPS % RG == 0 && (NTAPS == 9 || NTAPS == 4), "conv2d_x3f: 2x2 / 3x3");
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const Geo g = make_geo(a);
+    const int ncob = (a.Cout + NCO - 1) / NCO;
+    const int ntiles = g.tiles_x * g.tiles_y;
+    const int nph = a.nphase > 1 ? a.nphase : 1;
+    const int nwg = ntiles * a.B * ncob * nph;
+    auto decode = [&](int l, int& cob, int& b, int& oy0, int& ox0, int& ph) {  // as conv2d_x3_kernel
+        const int full = nwg & ~7;
+        const int L0 = l < full ? (l & 7) * (full >> 3) + (l >> 3) : l;
+        ph = L0 % nph;
+        const int L = L0 / nph;
+        cob = L % ncob;
+        const int rest = L / ncob;
+        const int tile = rest % ntiles;
+        b = rest / ntiles;
+        const int ty = tile / g.tiles_x, tx = tile - (tile / g.tiles_x) * g.tiles_x;
+        oy0 = ty * a.TH;
+        ox0 = tx * a.TW;
+    };
+    const int npix = g.PH * g.PW;
+    const int stage_b = (npix * X3_PIXB + 15) & ~15;
+    char* ring = reinterpret_cast<char*>(smem) + 128;
+    float* btab = reinterpret_cast<float*>(ring + x3_region_bytes(a));
+    for (int c = tid; c < a.Cout; c += 256) btab[c] = a.bias != nullptr ? a.bias[c] : 0.f;
+    const int nstages = (a.Cin + CK - 1) / CK;
+    const int last = nstages - 1;
+    const int mytiles = (int)blockIdx.x < nwg ? (nwg - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+    const int total = mytiles * nstages;  // stream stages of this work-group
+    auto barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+
+    // ------------------------------------------------------------------ producer state (all 256 threads)
+    const int Hext = a.Hin + 2 * a.circ, Wext = a.Win + 2 * a.circ;
+    // PRO: GroupNorm + GELU (host-checked: the fused kernel runs no other prologue), compile-time so the producer
+    // units are branch-free and share the MFMAs' basic block
+    const float xs = PRO ? gn_prologue_scale(a) : in_scale_of(a);
+    const double gn_icnt = PRO ? 1.0 / ((double)(a.Cin / a.gn_groups) * a.Hin * a.Win) : 0.0;
+    constexpr int NR = MAXP + (PRO ? 3 : 0);
+    f32x4 rS[3][NR];
+    unsigned mS[3] = {0u, 0u, 0u};
+    const int gq = tid & 3;
+    const float* sbase[MAXP];
+    unsigned pixm = 0, finm = 0;
+    int cur_src = -1;
+    int ftile = -1;                       // tile (of this work-group) the fetch cursor is in
+    int fb = 0, fy0 = 0, fx0 = 0;
+    auto locate = [&](int sidx) __attribute__((always_inline)) {
+        const nps_src_t S0 = a.src[0], S1 = a.src[1], S2 = a.src[2];
+        const int si = a.s2d ? 0 : sidx;
+        const float* sptr = si == 0 ? S0.ptr : (si == 1 ? S1.ptr : S2.ptr);
+        const int sC = si == 0 ? S0.C : (si == 1 ? S1.C : S2.C);
+        const int sH = si == 0 ? S0.H : (si == 1 ? S1.H : S2.H);
+        const int sW = si == 0 ? S0.W : (si == 1 ? S1.W : S2.W);
+        const int soy = si == 0 ? S0.off_y : (si == 1 ? S1.off_y : S2.off_y);
+        const int sox = si == 0 ? S0.off_x : (si == 1 ? S1.off_x : S2.off_x);
+        const int ybase = fy0 - a.pad_y, xbase = fx0 - a.pad_x;
+        const int s2m = a.s2d ? 2 : 1;
+        const int s2y = a.s2d ? (sidx >> 1) - a.s2d_pad : 0, s2x = a.s2d ? (sidx & 1) - a.s2d_pad : 0;
+        pixm = 0;
+        finm = 0;
+#pragma unroll
+        for (int k = 0; k < MAXP; ++k) {
+            const int p = x3_slot_px(tid + k * 256);
+            const int pr = p / g.PW, pc = p - pr * g.PW;
+            const int ye = ybase + pr, xe = xbase + pc;
+            bool ok = p < npix && ye >= 0 && ye < Hext && xe >= 0 && xe < Wext;
+            finm = ok ? (finm | (1u << k)) : finm;
+            const int fy = a.circ ? nps::wrap_mod(ye - a.circ, a.Hin) : ye;
+            const int fx = a.circ ? nps::wrap_mod(xe - a.circ, a.Win) : xe;
+            const int yy = fy * s2m + s2y - soy, xx = fx * s2m + s2x - sox;
+            ok = ok && yy >= 0 && yy < sH && xx >= 0 && xx < sW;
+            sbase[k] = sptr + (ok ? ((size_t)(fb * sH + yy) * sW + xx) * sC : (size_t)fb * sH * sW * sC);
+            pixm = ok ? (pixm | (1u << k)) : pixm;
+        }
+    };
+    // fetch stream stage s (tile s / nstages of this work-group) into rp; returns the slot masks (bits 0-15:
+    // data inside the source, 16-31: pixel inside the frame)
+    auto issue = [&](int s, f32x4 (&rp)[NR]) __attribute__((always_inline)) -> unsigned {
+        const int k = s / nstages, st = s - (s / nstages) * nstages;
+        if (k != ftile) {  // uniform
+            int fcob, fph;
+            decode((int)blockIdx.x + k * (int)gridDim.x, fcob, fb, fy0, fx0, fph);
+            ftile = k;
+            cur_src = -1;
+        }
+        const int c0 = st * CK;
+        const int cend = min(c0 + CK, a.Cin);
+        int sidx = 0, cbase = 0;
+        if (a.s2d) {
+            sidx = c0 / a.src[0].C;
+            cbase = sidx * a.src[0].C;
+        } else {
+            int lo = 0;
+#pragma unroll
+            for (int si = 0; si < NPS_MAX_SRC; ++si) {
+                if (si < a.nsrc) {
+                    const int hi = lo + a.src[si].C;
+                    if (c0 >= lo && cend <= hi) {
+                        sidx = si;
+                        cbase = lo;
+                    }
+                    lo = hi;
+                }
+            }
+        }
+        if (sidx != cur_src) {
+            locate(sidx);
+            cur_src = sidx;
+        }
+        const bool chok = c0 + gq * 4 < cend;
+        const unsigned chm = chok ? ~0u : 0u;
+        const int cs = chok ? c0 - cbase + gq * 4 : 0;
+#pragma unroll
+        for (int q = 0; q < MAXP; ++q) rp[q] = *reinterpret_cast<const f32x4*>(sbase[q] + cs);
+        if constexpr (PRO) {
+            const int c = chok ? c0 + gq * 4 : 0;
+            rp[MAXP] = *reinterpret_cast<const f32x4*>(a.gn_gamma + c);
+            rp[MAXP + 1] = *reinterpret_cast<const f32x4*>(a.gn_beta + c);
+            rp[MAXP + 2] = *reinterpret_cast<const f32x4*>(
+                a.gn_stats + ((size_t)fb * a.gn_groups + c / (a.Cin / a.gn_groups)) * 2);
+        }
+        return (pixm & chm) | ((finm & chm) << 16);
+    };
+    // commit of a stream stage, unit u (slot u / 2, elements 2 (u & 1) .. +2): GroupNorm (one FMA, gs / gb
+    // derived at unit 0), GELU, then at the slot's second unit the scale, the hi / lo split and one LDS write
+    f32x4 gs = {1.f, 1.f, 1.f, 1.f}, gb = {0.f, 0.f, 0.f, 0.f};
+    f32x4 cv = {0.f, 0.f, 0.f, 0.f};
+    auto commit_unit = [&](int s, const f32x4 (&rp)[NR], unsigned okm, int u) __attribute__((always_inline)) {
+        const int k = u >> 1, hh = u & 1;
+        if constexpr (PRO) {
+            if (u == 0) {
+                const f32x4 sv = rp[MAXP + 2];
+                double s1, s2;
+                __builtin_memcpy(&s1, &sv, 8);
+                __builtin_memcpy(&s2, reinterpret_cast<const char*>(&sv) + 8, 8);
+                const double mu = s1 * gn_icnt;
+                double var = fma(s2, gn_icnt, -mu * mu);
+                var = var < 0.0 ? 0.0 : var;
+                const float mean = (float)mu;
+                const float rstd = __builtin_amdgcn_rsqf((float)(var + (double)a.gn_eps));
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    gs[e] = rstd * rp[MAXP][e];
+                    gb[e] = fmaf(-mean, gs[e], rp[MAXP + 1][e]);
+                }
+            }
+        }
+        const bool dat = (okm >> k) & 1u, inf = (okm >> (16 + k)) & 1u;
+#pragma unroll
+        for (int e = 2 * hh; e < 2 * hh + 2; ++e) {
+            float v = dat ? rp[k][e] : 0.f;
+            if constexpr (PRO) {
+                v = nps::gelu_fast(fmaf(v, gs[e], gb[e]));
+                v = inf ? v : 0.f;  // the conv's own zero padding (and channels past Cin)
+            }
+            cv[e] = v;
+        }
+        if (hh == 1) {
+            f16x4 hi, lo;
+            split4(cv * xs, hi, lo);
+            const int idx = tid + k * 256;
+            const int p = x3_slot_px(idx);
+            // a slot past the patch writes into the (unused) 128-B header instead: no branch around the writes
+            const bool inp = p < npix;
+            char* base = inp ? ring + (s % X3_NST) * stage_b + p * X3_PIXB + (idx & 3) * 8
+                             : reinterpret_cast<char*>(smem) + (lane & 3) * 32;
+            *reinterpret_cast<f16x4*>(base) = hi;
+            *reinterpret_cast<f16x4*>(base + (inp ? 32 : 16)) = lo;
+        }
+    };
+
+    // ------------------------------------------------------------------ consumer state
+    int boff[PBW];
+    const int px0 = (wave >> 1) * 64;
+    const int cw0 = (wave & 1) * 96;
+#pragma unroll
+    for (int pb = 0; pb < PBW; ++pb) {
+        const int P = px0 + pb * 32 + (lane & 31);
+        const int ti = P / a.TW, tj = P - (P / a.TW) * a.TW;
+        boff[pb] = (ti * g.PW + tj) * X3_PIXB + (lane >> 5) * 16;
+    }
+    f32x16 acc[CBW][PBW];
+    const int ncb = packed_ncb(a.Cout);
+    const size_t gstride = (size_t)ncb * 2048;
+    const int G = nstages * NTAPS;
+    const char* wbase = nullptr;
+    f16x8 Aw[RG][CBW][2];
+    f16x8 Bh[RG][PBW], Bl[RG][PBW];
+    auto loadA = [&](int gg, f16x8 (&d)[CBW][2]) __attribute__((always_inline)) {
+        const char* p = wbase + (size_t)gg * gstride;
+#pragma unroll
+        for (int cb = 0; cb < CBW; ++cb) {
+            d[cb][0] = *reinterpret_cast<const f16x8*>(p + cb * 2048);
+            d[cb][1] = *reinterpret_cast<const f16x8*>(p + cb * 2048 + 1024);
+        }
+    };
+    // K-group gg of the tile whose stage 0 is stream stage s0: patch window in ring slot (s0 + gg / NTAPS) % 3
+    auto loadB = [&](int s0, int gg, f16x8 (&dh)[PBW], f16x8 (&dl)[PBW]) __attribute__((always_inline)) {
+        const int st = gg / NTAPS, tap = gg - (gg / NTAPS) * NTAPS;
+        const char* p = ring + ((s0 + st) % X3_NST) * stage_b + ((tap / KWT) * g.PW + tap % KWT) * X3_PIXB;
+#pragma unroll
+        for (int pb = 0; pb < PBW; ++pb) {
+            dh[pb] = *reinterpret_cast<const f16x8*>(p + boff[pb]);
+            dl[pb] = *reinterpret_cast<const f16x8*>(p + boff[pb] + 32);
+        }
+    };
+    auto gclamp = [&](int x) { return x < G ? x : G - 1; };
+    const float xsc = xs;
+    const size_t wbody = packed_body(a.Cout, a.Cin, NTAPS);
+    const int h = lane >> 5;
+    float amax = 0.f;
+    float inv = 0.f;
+    int s0 = 0;  // stream stage of the current tile's stage 0
+    // spread store (as conv2d_x3_kernel's wide path)
+    constexpr int SPQ = 24;
+    constexpr int SP_ITEMS = 64 * SPQ / 64;
+    float* Tw = reinterpret_cast<float*>(ring + x3_ring_bytes(a));
+    const int tw_sh = __builtin_ctz((unsigned)a.TW);
+    const bool sp_oper = a.accumulate || a.addend0 != nullptr || a.addend1 != nullptr;
+    int sp_n = 0, sp_next = 0, sp_every = 1;
+    int sp_b = 0, sp_cob = 0, sp_oy0 = 0, sp_ox0 = 0, sp_ph = 0;
+    double sp_s1 = 0.0, sp_s2 = 0.0;
+    f32x4 sp_v, sp_a0, sp_a1, sp_ov;
+    size_t sp_off = 0;
+    int sp_co0 = 0;
+    bool sp_ok = false;
+    auto sp_issue = [&]() __attribute__((always_inline)) {
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        const int i = (SP_ITEMS - sp_n) * 64 + lane;
+        const int Pl = i / SPQ, q = i - (i / SPQ) * SPQ;
+        const int P = px0 + Pl, col = cw0 + 4 * q;
+        sp_co0 = sp_cob * NCO + col;
+        const int oy = sp_oy0 + (P >> tw_sh), ox = sp_ox0 + (P & (a.TW - 1));
+        const int dy = oy * a.out_os + a.out_off_y + (sp_ph >> 1), dx = ox * a.out_os + a.out_off_x + (sp_ph & 1);
+        sp_ok = sp_co0 < a.Cout && oy < a.Hout && ox < a.Wout && dy >= 0 && dy < a.out_H && dx >= 0 && dx < a.out_W;
+        sp_off = sp_ok ? (((size_t)sp_b * a.out_H + dy) * a.out_W + dx) * a.out_C + sp_co0 : 0;
+        sp_v = *reinterpret_cast<const f32x4*>(Tw + P * (NCO + 4) + col);
+        sp_a0 = z;
+        sp_a1 = z;
+        sp_ov = z;
+        if (sp_oper) {
+            if (a.addend0 != nullptr) sp_a0 = *reinterpret_cast<const f32x4*>(sp_ok ? a.addend0 + sp_off : x3_zero16);
+            if (a.addend1 != nullptr) sp_a1 = *reinterpret_cast<const f32x4*>(sp_ok ? a.addend1 + sp_off : x3_zero16);
+            if (a.accumulate) sp_ov = *reinterpret_cast<const f32x4*>(sp_ok ? a.out + sp_off : x3_zero16);
+        }
+    };
+    auto sp_finish = [&]() __attribute__((always_inline)) {
+        const f32x4 bi = *reinterpret_cast<const f32x4*>(btab + (sp_ok ? sp_co0 : 0));
+        f32x4 r;
+        float f1 = 0.f, f2 = 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            float v = sp_v[e] + bi[e];
+            if (!a.add_after_act) v = v + sp_a0[e] + sp_a1[e];
+            if (a.act == 1) v = nps::gelu_erf(v);
+            if (a.add_after_act) v = v + sp_a0[e] + sp_a1[e];
+            if (a.accumulate) v += sp_ov[e];
+            r[e] = v;
+            amax = sp_ok ? fmaxf(amax, fabsf(v)) : amax;
+            f1 += a.accumulate ? v - sp_ov[e] : v;
+            f2 += a.accumulate ? (v - sp_ov[e]) * (v + sp_ov[e]) : v * v;
+        }
+        if (a.out_stats != nullptr) {
+            sp_s1 += sp_ok ? (double)f1 : 0.0;
+            sp_s2 += sp_ok ? (double)f2 : 0.0;
+        }
+        float* dst = sp_ok ? a.out + sp_off : x3_sink + 4 * lane;
+        *reinterpret_cast<f32x4*>(dst) = r;
+        if (--sp_n == 0) stats_publish(a, sp_b, sp_s1, sp_s2);
+    };
+    // a tile starts (its stage 0 is stream stage s): decode, zero the accumulators, first operands
+    auto tile_start = [&](int s) __attribute__((always_inline)) {
+        int cob, b, oy0, ox0, ph;
+        decode((int)blockIdx.x + (s / nstages) * (int)gridDim.x, cob, b, oy0, ox0, ph);
+        const float* wph = a.wpack + (size_t)ph * a.phase_wstride;
+        inv = 1.f / (pow2_scale_for(wph[wbody]) * xsc);
+        wbase = reinterpret_cast<const char*>(wph) + (size_t)(cob * (NCO / 32) + cw0 / 32) * 2048 + lane * 16;
+        s0 = s;
+#pragma unroll
+        for (int i = 0; i < CBW; ++i)
+#pragma unroll
+            for (int j = 0; j < PBW; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+        static_for<RG - 1>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            loadA(gclamp(i), Aw[i]);
+        });
+        loadB(s0, 0, Bh[0], Bl[0]);
+        return X3Tile{cob, b, oy0, ox0, ph};
+    };
+    // a tile ends: the previous tile's leftover items, then this tile's block into Tw and the spread state
+    auto tile_end = [&](const X3Tile& t) __attribute__((always_inline)) {
+        while (sp_n > 0) {
+            sp_issue();
+            sp_finish();
+        }
+#pragma unroll
+        for (int pb = 0; pb < PBW; ++pb) {
+            const int P = px0 + pb * 32 + (lane & 31);
+#pragma unroll
+            for (int cb = 0; cb < CBW; ++cb)
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    const f32x4 v = {acc[cb][pb][4 * m] * inv, acc[cb][pb][4 * m + 1] * inv,
+                                     acc[cb][pb][4 * m + 2] * inv, acc[cb][pb][4 * m + 3] * inv};
+                    *reinterpret_cast<f32x4*>(Tw + P * (NCO + 4) + cw0 + cb * 32 + 8 * m + 4 * h) = v;
+                }
+        }
+        sp_n = SP_ITEMS;
+        sp_cob = t.cob;
+        sp_b = t.b;
+        sp_oy0 = t.oy0;
+        sp_ox0 = t.ox0;
+        sp_ph = t.ph;
+        sp_s1 = sp_s2 = 0.0;
+        sp_next = 0;
+        sp_every = G > SP_ITEMS ? (G - 1) / (SP_ITEMS - 1) : 1;
+    };
+
+    // ------------------------------------------------------------------ prologue: stream stages 0 .. 3
+    if (total > 0) {
+        mS[0] = issue(0, rS[0]);
+        if (total > 1) mS[1] = issue(1, rS[1]);
+        static_for<NU>([&](auto uc) { commit_unit(0, rS[0], mS[0], decltype(uc)::value); });
+        if (total > 1) static_for<NU>([&](auto uc) { commit_unit(1, rS[1], mS[1], decltype(uc)::value); });
+        if (total > 2) mS[2] = issue(2, rS[2]);
+        if (total > 3) mS[0] = issue(3, rS[0]);
+    }
+    barrier();
+    X3Tile cur{0, 0, 0, 0, 0};
+    // stream stage s (s % 3 == P): the consumers compute it (tile s / nstages, stage s - s0); the producer units
+    // commit stage s + 2 from set (P + 2) % 3 and the last K-group fetches stage s + 4 into set (P + 1) % 3
+    auto stage = [&](int s, auto Pc) __attribute__((always_inline)) {
+        constexpr int P = decltype(Pc)::value;
+        constexpr int SC = (P + 2) % 3, SF = (P + 1) % 3;
+        const int st = s - s0;
+        const bool do_fetch = s + 4 < total;
+        static_for<NTAPS>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            const int gg = st * NTAPS + j;
+            const bool sp = sp_n > 0 && gg >= sp_next;
+            if (sp) sp_issue();
+            __builtin_amdgcn_sched_barrier(0);
+            // one basic block per K-group: loads, the producer units and the MFMAs are all unconditional (a
+            // branch would split the block, and sched_group_barrier only interleaves inside one): the operand
+            // indices clamp, and past the end of the stream the units commit stale registers into the ring slot
+            // of stage s + 2, which nothing reads any more
+            loadA(gclamp(gg + RG - 1), Aw[(j + RG - 1) % RG]);
+            loadB(s0, gclamp(gg + 1), Bh[(j + 1) % RG], Bl[(j + 1) % RG]);
+            // this group's producer units (unit u runs in group u * NTAPS / NU)
+            static_for<NU>([&](auto uc) {
+                constexpr int u = decltype(uc)::value;
+                if constexpr (u * NTAPS / NU == j) commit_unit(s + 2, rS[SC], mS[SC], u);
+            });
+            constexpr int ra = j % RG;
+#pragma unroll
+            for (int cb = 0; cb < CBW; ++cb)
+#pragma unroll
+                for (int pb = 0; pb < PBW; ++pb)
+                    acc[cb][pb] = X3_MFMA(Aw[ra][cb][0], Bh[ra][pb], acc[cb][pb], 0, 0, 0);
+#pragma unroll
+            for (int cb = 0; cb < CBW; ++cb)
+#pragma unroll
+                for (int pb = 0; pb < PBW; ++pb)
+                    acc[cb][pb] = X3_MFMA(Aw[ra][cb][0], Bl[ra][pb], acc[cb][pb], 0, 0, 0);
+#pragma unroll
+            for (int cb = 0; cb < CBW; ++cb)
+#pragma unroll
+                for (int pb = 0; pb < PBW; ++pb)
+                    acc[cb][pb] = X3_MFMA(Aw[ra][cb][1], Bh[ra][pb], acc[cb][pb], 0, 0, 0);
+#pragma unroll
+            for (int i = 0; i < 2 * CBW; ++i) {  // weights first, then the patch, VALU in every gap
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+            }
+#pragma unroll
+            for (int i = 0; i < 2 * PBW; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+            }
+#pragma unroll
+            for (int i = 0; i < 3 * CBW * PBW - 2 * PBW - 2 * CBW; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (j == NTAPS - 1) {  // after this group's weight loads (see above)
+                if (do_fetch) mS[SF] = issue(s + 4, rS[SF]);
+            }
+            if (sp) {
+                sp_finish();
+                sp_next += sp_every;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        });
+        barrier();  // stage s + 2 committed by every wave; every read of stage s's slot done
+    };
+    auto step = [&](int s, auto Pc) __attribute__((always_inline)) {
+        if (s >= total) return;
+        if (s == 0 || s - s0 == nstages) {
+            if (s > 0) tile_end(cur);
+            cur = tile_start(s);
+        }
+        stage(s, Pc);
+    };
+    for (int s = 0; s < total; s += 3) {
+        step(s, std::integral_constant<int, 0>{});
+        step(s + 1, std::integral_constant<int, 1>{});
+        step(s + 2, std::integral_constant<int, 2>{});
+    }
+    if (total > 0) tile_end(cur);
+    while (sp_n > 0) {
+        sp_issue();
+        sp_finish();
+    }
+    nps::tag_publish(a.out_tag, amax, nps::wave_salt());
+}
+
 // ---------------------------------------------------------------------------------------------
 // Split-fp16 1x1 conv without a patch ring: every wave is its own producer.  A 1x1 stage has 9x less
 // MFMA work per staged byte than a 3x3 one, so the ring kernel's single fetch in flight per work-group
@@ -1676,6 +2126,17 @@ void launch_x3_one(const nps_conv2d_t& a, unsigned nwg, int lds, hipStream_t s) 
     conv2d_x3_kernel<NT, PB, PRO, WIDE><<<nwg, 512, lds, s>>>(a);
 }
 
+template <int NT, bool PRO>
+void launch_x3f_one(const nps_conv2d_t& a, unsigned nwg, int lds, hipStream_t s) {
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)conv2d_x3f_kernel<NT, PRO>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        attr_set = true;
+    }
+    conv2d_x3f_kernel<NT, PRO><<<nwg, 256, lds, s>>>(a);
+}
+
 #ifdef NPS_X1_DMA_KERNEL
 template <int NCB>
 void launch_x1d(const nps_conv2d_t& a, unsigned grid, hipStream_t s) {
@@ -1817,6 +2278,22 @@ int nps_launch_conv2d_x3(const nps_conv2d_t& a, int lds, hipStream_t s) {
         else
             conv1x1_x3_kernel<2, 2><<<grid1, 64 * waves, lds1, s>>>(a);
         NPS_CHECK_LAUNCH("conv2d_fwd (split-fp16 1x1)");
+        return 0;
+    }
+    static int fused = -1;  // dev knob NPS_X3_FUSED=0: the 8-wave producer/consumer kernel for wide tiles
+    if (fused < 0) {
+        const char* e = getenv("NPS_X3_FUSED");
+        fused = (e != nullptr && e[0] == '0') ? 0 : 1;
+    }
+    // (the fused kernel's prologue is GroupNorm + GELU or none)
+    if (wide && fused && (!pro || (a.gn_stats != nullptr && a.pre_act == 1))) {
+        if (a.KH * a.KW == 9)
+            pro ? launch_x3f_one<9, true>(a, grid, lds, s) : launch_x3f_one<9, false>(a, grid, lds, s);
+        else if (a.KH * a.KW == 4)
+            launch_x3f_one<4, false>(a, grid, lds, s);
+        else
+            NPS_CHECK_ARG(false, "conv2d_fwd (split-fp16): wide tiles are 2x2 / 3x3 only");
+        NPS_CHECK_LAUNCH("conv2d_fwd (split-fp16, wide, fused roles)");
         return 0;
     }
     if (wide) {
