@@ -49,6 +49,11 @@ def fetch_scale(name):
     c = klass(name)
     if c is not None and c.startswith("x3f16_") and c != "x3f16_1tap":
         return 1
+    if "timeconv_fast_kernel" in name:
+        # each block stages PX = 16 pixels of every planar pre-decoder row: 64-B halves of 128-B lines, the
+        # other half read by the neighbouring block — the producers' counted-1:1 shape (round 4: the x 2 here
+        # made the kernel read as 3.4x its algorithmic bytes; it reads them once)
+        return 1
     return 2
 
 
