@@ -280,6 +280,13 @@ __host__ __device__ inline bool x3_wide_tile(const nps_conv2d_t& a) { return a.T
 // floats per pixel of the LDS-staged output tile: the work-group's channels + 4 (pad)
 __host__ __device__ inline int x3_tpitch(const nps_conv2d_t& a) { return (x3_wide_tile(a) ? 192 : 64) + 4; }
 
+#ifndef NPS_X3_SPREAD
+// wide tiles of conv2d_x3_kernel: 1 = spread store (the consumers store tile t during tile t + 1's main loop),
+// 0 = the store phase after the main loop.  Round 4 A/B (profiles/r4/x3_fused_spread_ab.txt): the spread store is
+// 8-10 % slower — every weight load issued after a store waits for it (vmcnt retires in order) — so 0 ships.
+#define NPS_X3_SPREAD 0
+#endif
+
 // bytes of the split-fp16 kernel's patch ring
 __host__ __device__ inline int x3_ring_bytes(const nps_conv2d_t& a) {
     const Geo g = make_geo(a);
@@ -291,7 +298,7 @@ __host__ __device__ inline int x3_ring_bytes(const nps_conv2d_t& a) {
 __host__ __device__ inline int x3_region_bytes(const nps_conv2d_t& a) {
     const int ring = x3_ring_bytes(a);
     const int tile = a.TH * a.TW * x3_tpitch(a) * 4;
-    if (x3_wide_tile(a)) return ring + tile;
+    if (NPS_X3_SPREAD && x3_wide_tile(a)) return ring + tile;
     return ring > tile ? ring : tile;
 }
 // 128-B header + region + the bias table of the LDS store phase (Cout floats, 16-B padded)

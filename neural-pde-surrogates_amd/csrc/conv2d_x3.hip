@@ -48,6 +48,10 @@ __host__ __device__ constexpr int x3_patch_px_max(int ntaps, int tile_px) {
 #ifndef NPS_X3_ARING_WIDE
 #define NPS_X3_ARING_WIDE 2  // ... of the wide tiles (3 fits without the spread store, not with it)
 #endif
+#ifndef NPS_X3F_ABL
+#define NPS_X3F_ABL 0  // dev ablations of conv2d_x3f_kernel (speed only): 1 no patch fetch, 2 no spread stores,
+                       // 3 no producer units, 4 = 1 + 2
+#endif
 #ifndef NPS_X3_ABL
 #define NPS_X3_ABL 0  // dev ablations of the 3x3 main loop (tools/x3_abl.sh); 0 in every shipped build
 #endif
@@ -200,6 +204,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
     constexpr int NCO = WIDE ? 192 : 64;       // output channels per work-group
     constexpr int TILE_PX = WIDE ? 128 : 4 * PB * 32;
     constexpr int MAXP = (x3_patch_px_max(NTAPS, TILE_PX) * 4 + 255) / 256;
+    constexpr bool SPREAD = WIDE && NPS_X3_SPREAD;  // wide tiles: spread store (dev knob: the store phase)
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const Geo g = make_geo(a);
@@ -413,7 +418,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
         decode(l, fcob, fb, fy0, fx0, fph);
         unsigned m0 = issue(0, r0);
         unsigned m1 = issue(min(1, last), r1);
-        if constexpr (WIDE) {
+        if constexpr (SPREAD) {
             // Wide tiles: the consumers store each tile during the next one's main loop, so the producers have
             // no store phase: per tile 1 + nstages barriers, and the next tile's first two stages are fetched
             // into r0 / r1 by the last stage iterations of this one (where the fetch of stage st + 3 would run
@@ -599,7 +604,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
     };
     auto group = [&](int gg, const int ra, const int r) __attribute__((always_inline)) {  // ra: weight slot of K-group gg, r: patch slot
         bool sp = false;
-        if constexpr (WIDE) {
+        if constexpr (SPREAD) {
             sp = sp_n > 0 && gg >= sp_next;  // uniform
             if (sp) sp_issue();
             __builtin_amdgcn_sched_barrier(0);
@@ -637,7 +642,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
         }
         __builtin_amdgcn_sched_group_barrier(0x008, 3 * CBW * PBW - 2 * PBW - 2 * CBW, 0);
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (WIDE) {
+        if constexpr (SPREAD) {
             if (sp) {
                 sp_finish();
                 sp_next += sp_every;
@@ -711,7 +716,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
         if (wave == 0 && lane == 0 && l < (1 << 16)) x3_stamps[l * 16 + 6] = bar_cycles;
         bar_cycles = 0;
 #endif
-        if constexpr (WIDE) {
+        if constexpr (SPREAD) {
             // items of the previous tile the main loop had no K-group for (small Cin), then this tile's block
             // into Tw: the wave's own block only, which it alone reads back — no barrier
             while (sp_n > 0) {
@@ -788,7 +793,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
         X3_STAMP(3);
         X3_RSTAMP(5);
     }
-    if constexpr (WIDE) {  // the last tile: no next main loop to spread it over
+    if constexpr (SPREAD) {  // the last tile: no next main loop to spread it over
         while (sp_n > 0) {
             sp_issue();
             sp_finish();
@@ -799,6 +804,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
 }
 
 
+#ifdef NPS_X3F_KERNEL  // dev build only (tools/build_variant.sh -DNPS_X3F_KERNEL): not in the default library
 // tile coordinates of conv2d_x3f_kernel
 struct X3Tile {
     int cob, b, oy0, ox0, ph;
@@ -1095,7 +1101,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             sp_s2 += sp_ok ? (double)f2 : 0.0;
         }
         float* dst = sp_ok ? a.out + sp_off : x3_sink + 4 * lane;
+#if NPS_X3F_ABL != 2 && NPS_X3F_ABL != 4
         *reinterpret_cast<f32x4*>(dst) = r;
+#else
+        (void)dst;
+#endif
         if (--sp_n == 0) stats_publish(a, sp_b, sp_s1, sp_s2);
     };
     // a tile starts (its stage 0 is stream stage s): decode, zero the accumulators, first operands
@@ -1181,7 +1191,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             // this group's producer units (unit u runs in group u * NTAPS / NU)
             static_for<NU>([&](auto uc) {
                 constexpr int u = decltype(uc)::value;
-                if constexpr (u * NTAPS / NU == j) commit_unit(s + 2, rS[SC], mS[SC], u);
+                if constexpr (u * NTAPS / NU == j && NPS_X3F_ABL != 3) commit_unit(s + 2, rS[SC], mS[SC], u);
             });
             constexpr int ra = j % RG;
 #pragma unroll
@@ -1217,7 +1227,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                 __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
             }
             __builtin_amdgcn_sched_barrier(0);
-            if constexpr (j == NTAPS - 1) {  // after this group's weight loads (see above)
+            if constexpr (j == NTAPS - 1 && NPS_X3F_ABL != 1 && NPS_X3F_ABL != 4) {  // after this group's weight loads
                 if (do_fetch) mS[SF] = issue(s + 4, rS[SF]);
             }
             if (sp) {
@@ -1248,6 +1258,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
     nps::tag_publish(a.out_tag, amax, nps::wave_salt());
 }
+
+#endif  // NPS_X3F_KERNEL
 
 // ---------------------------------------------------------------------------------------------
 // Split-fp16 1x1 conv without a patch ring: every wave is its own producer.  A 1x1 stage has 9x less
@@ -2126,6 +2138,7 @@ void launch_x3_one(const nps_conv2d_t& a, unsigned nwg, int lds, hipStream_t s) 
     conv2d_x3_kernel<NT, PB, PRO, WIDE><<<nwg, 512, lds, s>>>(a);
 }
 
+#ifdef NPS_X3F_KERNEL
 template <int NT, bool PRO>
 void launch_x3f_one(const nps_conv2d_t& a, unsigned nwg, int lds, hipStream_t s) {
     static bool attr_set = false;
@@ -2136,6 +2149,7 @@ void launch_x3f_one(const nps_conv2d_t& a, unsigned nwg, int lds, hipStream_t s)
     }
     conv2d_x3f_kernel<NT, PRO><<<nwg, 256, lds, s>>>(a);
 }
+#endif
 
 #ifdef NPS_X1_DMA_KERNEL
 template <int NCB>
@@ -2280,10 +2294,11 @@ int nps_launch_conv2d_x3(const nps_conv2d_t& a, int lds, hipStream_t s) {
         NPS_CHECK_LAUNCH("conv2d_fwd (split-fp16 1x1)");
         return 0;
     }
-    static int fused = -1;  // dev knob NPS_X3_FUSED=0: the 8-wave producer/consumer kernel for wide tiles
+#ifdef NPS_X3F_KERNEL
+    static int fused = -1;  // dev build knob NPS_X3_FUSED=1: the fused-role kernel for wide tiles
     if (fused < 0) {
         const char* e = getenv("NPS_X3_FUSED");
-        fused = (e != nullptr && e[0] == '0') ? 0 : 1;
+        fused = (e != nullptr && e[0] == '1') ? 1 : 0;
     }
     // (the fused kernel's prologue is GroupNorm + GELU or none)
     if (wide && fused && (!pro || (a.gn_stats != nullptr && a.pre_act == 1))) {
@@ -2296,6 +2311,7 @@ int nps_launch_conv2d_x3(const nps_conv2d_t& a, int lds, hipStream_t s) {
         NPS_CHECK_LAUNCH("conv2d_fwd (split-fp16, wide, fused roles)");
         return 0;
     }
+#endif
     if (wide) {
         if (a.KH * a.KW == 9)
             pro ? launch_x3_one<9, 2, true, true>(a, grid, lds, s) : launch_x3_one<9, 2, false, true>(a, grid, lds, s);

@@ -3,7 +3,7 @@
 # usage: tools/r4_ab.sh TAG VARIANT [VARIANT2 ...]
 #   VARIANT = LIB[:ENV=VAL[,ENV=VAL]]: libnps_<LIB>.so (built by tools/build_variant.sh; "hip" = the in-tree
 #   library) run with those environment settings.  libnps_base.so (if present) = the reference build of an
-#   earlier commit, run without the s2d view.  TESTS=0 skips the parity tests.
+#   earlier commit, run without the s2d view.  TESTS=0 skips the parity tests, CONV_ONLY=1 the bench too.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 TAG=$1; shift
@@ -27,6 +27,7 @@ for r in 1 2; do
     done
   done
 done | tee gpurun_out/${TAG}_conv.txt
+[ "${CONV_ONLY:-0}" = 1 ] && exit 0
 for r in 1 2; do
   for V in $VARS; do
     N=$(echo $V | tr ':=,' '___')

@@ -1,0 +1,31 @@
+#!/bin/bash
+# Round-4 GPU pass (gpurun): parity suite, C3 bench + rocprof, B=2 line, training lines (B=2, B=16) + rocprof of
+# the B=16 step, C5 (ufno3d bf16) line + rocprof, N=2 training rehearsal.  Outputs: gpurun_out/${TAG}_*.
+# usage: tools/r4_full.sh TAG [steps...]   steps: tests bench prof b2 train trainprof c5 c5prof reh (default: all)
+set -o pipefail
+TAG=${1:-r4full}; shift
+STEPS="${@:-tests bench prof b2 train trainprof c5 c5prof reh}"
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+O=gpurun_out/$TAG
+for s in $STEPS; do
+  case $s in
+    tests) timeout -k 10 600 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread > ${O}_tests.log 2>&1 \
+             || { echo "tests failed"; tail -30 ${O}_tests.log; exit 1; }; tail -2 ${O}_tests.log ;;
+    bench) timeout -k 10 400 python -u bench.py > ${O}_bench.json 2> ${O}_bench.err || { echo "bench failed"; tail -20 ${O}_bench.err; exit 1; }; tail -c 600 ${O}_bench.json ;;
+    prof)  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d ${O}_prof -o run -- python3 bench.py --steps 3 --warmup 1 --cpu-calls 0 \
+             > ${O}_prof.log 2>&1 || { echo "prof failed"; tail -20 ${O}_prof.log; exit 1; } ;;
+    b2)    timeout -k 10 300 python -u bench.py --global-batch 2 --cpu-calls 0 > ${O}_b2.json 2> ${O}_b2.err || { echo "b2 failed"; tail -20 ${O}_b2.err; exit 1; }; tail -c 300 ${O}_b2.json ;;
+    train) for gb in 2 16; do timeout -k 10 400 python -u bench.py --mode train --steps 5 --warmup 2 --global-batch $gb > ${O}_train_b$gb.json 2> ${O}_train_b$gb.err \
+             || { echo "train $gb failed"; tail -20 ${O}_train_b$gb.err; exit 1; }; tail -c 300 ${O}_train_b$gb.json; done ;;
+    trainprof) timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d ${O}_tprof -o run -- python3 bench.py --mode train --steps 3 --warmup 1 --global-batch 16 --cpu-calls 0 \
+             > ${O}_tprof.log 2>&1 || { echo "train prof failed"; tail -20 ${O}_tprof.log; exit 1; } ;;
+    c5)    timeout -k 10 400 python -u bench.py --model ufno3d --dtype bf16 > ${O}_c5.json 2> ${O}_c5.err || { echo "c5 failed"; tail -20 ${O}_c5.err; exit 1; }; tail -c 300 ${O}_c5.json ;;
+    c5prof) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d ${O}_c5prof -o run -- python3 bench.py --model ufno3d --dtype bf16 --steps 3 --warmup 1 --cpu-calls 0 \
+             > ${O}_c5prof.log 2>&1 || { echo "c5 prof failed"; tail -20 ${O}_c5prof.log; exit 1; } ;;
+    reh)   NPS_BENCH_REHEARSAL=1 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 \
+             bench.py --mode train --gpus 2 --steps 3 --warmup 1 --global-batch 4 --cpu-calls 0 > ${O}_reh_train.json 2> ${O}_reh_train.err \
+             || { echo "rehearsal failed"; tail -20 ${O}_reh_train.err; exit 1; }; tail -c 400 ${O}_reh_train.json ;;
+  esac
+  echo "step $s ok"
+done
