@@ -1350,7 +1350,11 @@ __global__ __launch_bounds__(512) void conv1x1_x3_kernel(const nps_conv2d_t a) {
     };
     const int ncb = packed_ncb(a.Cout);
     const size_t gstride = (size_t)ncb * 2048;  // bytes per chunk of the packed weight
-    const char* wbase = reinterpret_cast<const char*>(a.wpack) + (size_t)cob * CBW * 2048 + lane * 16;
+    // the last 512-channel group's waves past the packed blocks (Cout = 600: 12 packed 64-channel blocks, waves
+    // of blocks 12-15) read the last packed block instead of bytes past the buffer; they store nothing
+    // (co >= Cout in either epilogue)
+    const int wcob = cob < ncb / CBW ? cob : ncb / CBW - 1;
+    const char* wbase = reinterpret_cast<const char*>(a.wpack) + (size_t)wcob * CBW * 2048 + lane * 16;
     f16x8 Aw[2][2][CBW][2];  // [slot][chunk of the pair][cb][hi, lo]
     auto loadA = [&](int st, f16x8 (&d)[2][CBW][2]) {
 #pragma unroll
