@@ -569,8 +569,10 @@ def run_train(args):
     mine = time.perf_counter() - t0
     elapsed = max_over_ranks(mine, dev)
     times = per_rank_times(mine, dev)
+    # the probe step runs on every rank: under a process group a training step holds collectives (the global
+    # loss and the gradient all-reduce), which a rank-0-only step would leave unmatched
+    roof = probe_roofline(lambda: tr.train_one_epoch([batch], epoch=0))
     if rank == 0:
-        roof = probe_roofline(lambda: tr.train_one_epoch([batch], epoch=0))
         cpu = cpu_baseline_train(model, args) if (args.cpu_calls > 0 and world == 1) else None
         print(json.dumps({
             "metric": "pushforward training samples/sec (train_step + backward + all-reduce + Adam)",
