@@ -2,6 +2,8 @@
 // post-processing, reductions and layout transforms for gfx950 (see include/nps.h).
 #include "nps_common.hpp"
 
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 namespace nps {
@@ -398,6 +400,332 @@ __global__ __launch_bounds__(64) void timeconv_bwd_kernel(
         }
 }
 
+// GELU and its derivative from one branch-free erfc (nps_common.hpp gelu_fast's Numerical Recipes
+// polynomial, < 1.2e-7 relative): Phi(z) = 0.5 erfc(-z / sqrt 2), GELU = z Phi, GELU' = Phi + z phi(z).
+__device__ __forceinline__ void gelu_and_grad(float z, float& g, float& gp) {
+    const float x = fabsf(z) * 0.70710678118654752440f;
+    const float t = __builtin_amdgcn_rcpf(fmaf(0.5f, x, 1.0f));
+    float p = fmaf(t, 0.17087277f, -0.82215223f);
+    p = fmaf(t, p, 1.48851587f);
+    p = fmaf(t, p, -1.13520398f);
+    p = fmaf(t, p, 0.27886807f);
+    p = fmaf(t, p, -0.18628806f);
+    p = fmaf(t, p, 0.09678418f);
+    p = fmaf(t, p, 0.37409196f);
+    p = fmaf(t, p, 1.00002368f);
+    p = fmaf(t, p, -1.26551223f);
+    const float hx2 = -x * x;  // -z^2 / 2
+    const float half_erfc = 0.5f * t * __expf(hx2 + p);
+    const float phi = z < 0.f ? half_erfc : 1.0f - half_erfc;
+    g = z * phi;
+    gp = fmaf(z * 0.39894228040143267794f, __expf(hx2), phi);
+}
+
+// TimeConvDense backward for a compile-time (num_c, tw) — the twophase cfgs (tw = 25).  Same chain as
+// timeconv_bwd_kernel (dec_grid.py:126-146 + add_delta :8-31 + tanh + mask), laid out for throughput:
+//  * a block of 256 threads walks pixel groups of PX pixels (grid-stride, so a block keeps its parameter-
+//    gradient accumulators in registers over many groups and writes ONE ws row at the end);
+//  * thread = (slot, pixel): the PX lanes of a slot are PX pixels, the NSLOT = 256 / PX slots split each
+//    phase's work items (an output channel x a run of positions), so every LDS row read is PX consecutive
+//    floats and every item keeps its input window in registers;
+//  * LDS per block: the group's planar `pre` rows, GELU(conv1), GELU' -> conv1 gradient (rows zero-padded
+//    so the stride-2 transpose in the `pre` gradient needs no bounds tests), the conv2-output gradient
+//    (zero-padded for the conv2 transpose) and the weights.
+// Phases per group (barrier between): stage pre | A conv1 -> GELU, GELU' | B conv2 -> tanh', mask, dt ->
+// g2 | C conv2^T(g2) * GELU' -> gz, D w2/b2 partials | E w1/b1 partials, F conv1^T(gz) -> gpre.
+template <int NC, int TW, int PX>
+__global__ __launch_bounds__(256, 2) void timeconv_bwd_fast_kernel(
+    const float* __restrict__ pre, const float* __restrict__ u, const float* __restrict__ w1,
+    const float* __restrict__ b1, const float* __restrict__ w2, const float* __restrict__ b2,
+    const float* __restrict__ dtcum, const float* __restrict__ mask, int mask_S, int mask_ch,
+    const float* __restrict__ gout, float* __restrict__ gpre, float* __restrict__ ws, int HW, int ngroups,
+    int nrows, int act_tanh) {
+    constexpr int L = 3 * TW;
+    constexpr int KA = (TW + 1) / 2;
+    constexpr int KB = (TW + 3) / 4 + 1 + (TW % 4 == 0 ? 1 : 0);
+    constexpr int L1 = (L - KA) / 2 + 1;
+    constexpr int C2 = 2 * NC;
+    constexpr int NSLOT = 256 / PX, PP = PX + 1;
+    constexpr int RA = 4, RB = 5, RM = 4;          // run lengths: conv1 / conv2 positions, gpre pairs
+    constexpr int QN = (KA + 1) / 2;               // taps of one parity
+    constexpr int GZ0 = QN - 1;                    // left zero pad of a gz row
+    constexpr int MR = ((L + 1) / 2 + RM - 1) / RM * RM;
+    constexpr int GZW = MR + GZ0;                  // padded gz row (t1 = m - q over m < MR, q < QN)
+    constexpr int G2W = TW + 2 * (KB - 1);         // padded g2 row
+    constexpr int KH = KB / 2, KAH = (KA + 1) / 2; // tap halves of the w2 / w1 partial items
+    constexpr int NW1 = C2 * NC * KA, NW2 = NC * C2 * KB;
+    constexpr int NPAR = NW1 + C2 + NW2 + NC;
+    static_assert(L1 - KB + 1 == TW && L1 % RA == 0 && TW % RB == 0 && KB % 2 == 0, "TimeConvDense sizes");
+    static_assert(GZW >= GZ0 + L1, "gz padding");
+    constexpr int NA = C2 * (L1 / RA), NB = NC * (TW / RB), ND = NC * C2 * 2, NE = C2 * NC * 2,
+                  NF = NC * (MR / RM);
+    constexpr int NDI = (ND + NSLOT - 1) / NSLOT, NEI = (NE + NSLOT - 1) / NSLOT;
+
+    extern __shared__ float lds[];
+    float* xs = lds;                    // [NC*L][PP]
+    float* d1 = xs + NC * L * PP;       // [C2*L1][PP]
+    float* gz = d1 + C2 * L1 * PP;      // [C2*GZW][PP]   GELU' then the conv1 pre-activation gradient
+    float* g2 = gz + C2 * GZW * PP;     // [NC*G2W][PP]
+    float* w1s = g2 + NC * G2W * PP;    // [C2][NC][KA]
+    float* w2s = w1s + NW1;             // [NC][C2][KB]
+    float* b1s = w2s + NW2;
+    float* b2s = b1s + C2;
+    float* dts = b2s + NC;
+
+    const int tid = threadIdx.x;
+    const int p = tid % PX, slot = tid / PX;
+    for (int i = tid; i < C2 * GZW * PP + NC * G2W * PP; i += 256) gz[i] = 0.f;  // gz and g2 (pads stay 0)
+    for (int i = tid; i < NW1; i += 256) w1s[i] = w1[i];
+    for (int i = tid; i < NW2; i += 256) w2s[i] = w2[i];
+    if (tid < C2) b1s[tid] = b1[tid];
+    if (tid < NC) b2s[tid] = b2[tid];
+    if (tid < TW) dts[tid] = dtcum[tid];
+
+    double accD[NDI][KH], accE[NEI][KAH], accb2[NDI], accb1[NEI];
+#pragma unroll
+    for (int i = 0; i < NDI; ++i)
+#pragma unroll
+        for (int k = 0; k < KH; ++k) accD[i][k] = accb2[i] = 0.0;
+#pragma unroll
+    for (int i = 0; i < NEI; ++i)
+#pragma unroll
+        for (int k = 0; k < KAH; ++k) accE[i][k] = accb1[i] = 0.0;
+
+    const int gpb = (HW + PX - 1) / PX;  // groups per sample
+    for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+        const int b = grp / gpb;
+        const int p0 = (grp - b * gpb) * PX;
+        const int np = min(PX, HW - p0);
+        const bool valid = p < np;
+        const int pix = p0 + (valid ? p : 0);
+        __syncthreads();  // previous group's readers of xs / gz / g2 are done
+        {
+            const float* src = pre + (size_t)b * NC * L * HW + p0;
+            for (int i = tid; i < NC * L * PX; i += 256) {
+                const int r = i / PX, q = i % PX;
+                xs[r * PP + q] = q < np ? src[(size_t)r * HW + q] : 0.f;
+            }
+        }
+        __syncthreads();
+        // A. conv1 (stride 2) -> GELU into d1, GELU' into gz
+        for (int j = slot; j < NA; j += NSLOT) {
+            const int o = j / (L1 / RA), t0 = (j - o * (L1 / RA)) * RA;
+            float acc[RA];
+#pragma unroll
+            for (int r = 0; r < RA; ++r) acc[r] = b1s[o];
+#pragma unroll
+            for (int ci = 0; ci < NC; ++ci) {
+                float xw[2 * (RA - 1) + KA];
+                const float* xr = xs + (ci * L + 2 * t0) * PP + p;
+#pragma unroll
+                for (int k = 0; k < 2 * (RA - 1) + KA; ++k) xw[k] = xr[k * PP];
+                const float* wr = w1s + (o * NC + ci) * KA;
+#pragma unroll
+                for (int k = 0; k < KA; ++k) {
+                    const float wk = wr[k];
+#pragma unroll
+                    for (int r = 0; r < RA; ++r) acc[r] = fmaf(wk, xw[2 * r + k], acc[r]);
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < RA; ++r) {
+                float g, gp;
+                gelu_and_grad(acc[r], g, gp);
+                d1[(o * L1 + t0 + r) * PP + p] = g;
+                gz[(o * GZW + GZ0 + t0 + r) * PP + p] = gp;
+            }
+        }
+        __syncthreads();
+        // B. conv2, add_delta, tanh, mask -> g2 = d loss / d conv2 output (x dt)
+        {
+            const float m = (mask && valid) ? mask[((size_t)b * mask_S + mask_ch) * HW + pix] : 0.f;
+            for (int j = slot; j < NB; j += NSLOT) {
+                const int o2 = j / (TW / RB), t0 = (j - o2 * (TW / RB)) * RB;
+                float acc[RB];
+#pragma unroll
+                for (int r = 0; r < RB; ++r) acc[r] = b2s[o2];
+#pragma unroll
+                for (int o = 0; o < C2; ++o) {
+                    float dw[RB - 1 + KB];
+                    const float* dr = d1 + (o * L1 + t0) * PP + p;
+#pragma unroll
+                    for (int k = 0; k < RB - 1 + KB; ++k) dw[k] = dr[k * PP];
+                    const float* wr = w2s + (o2 * C2 + o) * KB;
+#pragma unroll
+                    for (int k = 0; k < KB; ++k) {
+                        const float wk = wr[k];
+#pragma unroll
+                        for (int r = 0; r < RB; ++r) acc[r] = fmaf(wk, dw[r + k], acc[r]);
+                    }
+                }
+                const float ulast = u[(((size_t)b * NC + o2) * TW + (TW - 1)) * HW + pix];
+                const float* gr = gout + (((size_t)b * NC + o2) * TW + t0) * HW + pix;
+#pragma unroll
+                for (int r = 0; r < RB; ++r) {
+                    const float dt = dts[t0 + r];
+                    float g = valid ? gr[(size_t)r * HW] : 0.f;
+                    if (mask) g = g - m * g;
+                    if (act_tanh) {
+                        const float y = tanhf(ulast + dt * acc[r]);
+                        g *= 1.f - y * y;
+                    }
+                    g2[(o2 * G2W + KB - 1 + t0 + r) * PP + p] = g * dt;
+                }
+            }
+        }
+        __syncthreads();
+        // C. gz = GELU' * conv2^T(g2)   (in place over GELU')
+        for (int j = slot; j < NA; j += NSLOT) {
+            const int o = j / (L1 / RA), t0 = (j - o * (L1 / RA)) * RA;
+            float acc[RA];
+#pragma unroll
+            for (int r = 0; r < RA; ++r) acc[r] = 0.f;
+#pragma unroll
+            for (int o2 = 0; o2 < NC; ++o2) {
+                // t1 - k + KB - 1 over t1 in [t0, t0 + RA), k < KB: padded g2 index t0 .. t0 + RA + KB - 2
+                float gw[RA + KB - 1];
+                const float* gr = g2 + (o2 * G2W + t0) * PP + p;
+#pragma unroll
+                for (int i = 0; i < RA + KB - 1; ++i) gw[i] = gr[i * PP];
+                const float* wr = w2s + (o2 * C2 + o) * KB;
+#pragma unroll
+                for (int k = 0; k < KB; ++k) {
+                    const float wk = wr[k];
+#pragma unroll
+                    for (int r = 0; r < RA; ++r) acc[r] = fmaf(wk, gw[r - k + KB - 1], acc[r]);
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < RA; ++r) gz[(o * GZW + GZ0 + t0 + r) * PP + p] *= acc[r];
+        }
+        // D. w2 / b2 partials: item (o2, o, tap half); b2 rides on (o2, 0, 0)
+#pragma unroll
+        for (int ii = 0; ii < NDI; ++ii) {
+            const int j = slot + ii * NSLOT;
+            if (j < ND) {
+                const int o2 = j / (2 * C2), o = (j / 2) % C2, kh = j & 1;
+                const float* gr = g2 + (o2 * G2W + KB - 1) * PP + p;
+                const float* dr = d1 + (o * L1 + kh * KH) * PP + p;
+                float acc[KH], sb = 0.f;
+#pragma unroll
+                for (int k = 0; k < KH; ++k) acc[k] = 0.f;
+#pragma unroll
+                for (int t = 0; t < TW; ++t) {
+                    const float g = gr[t * PP];
+                    sb += g;
+#pragma unroll
+                    for (int k = 0; k < KH; ++k) acc[k] = fmaf(g, dr[(t + k) * PP], acc[k]);
+                }
+#pragma unroll
+                for (int k = 0; k < KH; ++k) accD[ii][k] += (double)acc[k];
+                if (o == 0 && kh == 0) accb2[ii] += (double)sb;
+            }
+        }
+        __syncthreads();
+        // E. w1 / b1 partials: item (o, ci, tap half); b1 rides on (o, 0, 0)
+#pragma unroll
+        for (int ii = 0; ii < NEI; ++ii) {
+            const int j = slot + ii * NSLOT;
+            if (j < NE) {
+                const int o = j / (2 * NC), ci = (j / 2) % NC, kh = j & 1;
+                const float* gr = gz + (o * GZW + GZ0) * PP + p;
+                const float* xr = xs + (ci * L + kh * KAH) * PP + p;
+                float acc[KAH], sb = 0.f;
+#pragma unroll
+                for (int k = 0; k < KAH; ++k) acc[k] = 0.f;
+#pragma unroll 8
+                for (int t1 = 0; t1 < L1; ++t1) {
+                    const float g = gr[t1 * PP];
+                    sb += g;
+#pragma unroll
+                        for (int k = 0; k < KAH; ++k)  // (KA odd: the second half's tap KA is unused; it reads
+                        acc[k] = fmaf(g, xr[(2 * t1 + k) * PP], acc[k]);  // at most one row past xs, into d1)
+                }
+#pragma unroll
+                for (int k = 0; k < KAH; ++k) accE[ii][k] += (double)acc[k];
+                if (ci == 0 && kh == 0) accb1[ii] += (double)sb;
+            }
+        }
+        // F. gpre[ci][2m + par] = sum_o sum_q gz[o][m - q] w1[o][ci][2q + par]
+        for (int j = slot; j < NF; j += NSLOT) {
+            const int ci = j / (MR / RM), m0 = (j - ci * (MR / RM)) * RM;
+            float acc[RM][2];
+#pragma unroll
+            for (int r = 0; r < RM; ++r) acc[r][0] = acc[r][1] = 0.f;
+#pragma unroll
+            for (int o = 0; o < C2; ++o) {
+                float gw[RM + QN - 1];  // padded gz index m0 + i  <->  t1 = m0 + i - GZ0
+                const float* gr = gz + (o * GZW + m0) * PP + p;
+#pragma unroll
+                for (int i = 0; i < RM + QN - 1; ++i) gw[i] = gr[i * PP];
+                const float* wr = w1s + (o * NC + ci) * KA;
+#pragma unroll
+                for (int q = 0; q < QN; ++q)
+#pragma unroll
+                    for (int par = 0; par < 2; ++par) {
+                        if (2 * q + par >= KA) continue;
+                        const float wk = wr[2 * q + par];
+#pragma unroll
+                        for (int r = 0; r < RM; ++r) acc[r][par] = fmaf(wk, gw[r - q + QN - 1], acc[r][par]);
+                    }
+            }
+            if (valid) {
+                float* gp = gpre + ((size_t)b * NC * L + ci * L) * HW + pix;
+#pragma unroll
+                for (int r = 0; r < RM; ++r)
+#pragma unroll
+                    for (int par = 0; par < 2; ++par) {
+                        const int jo = 2 * (m0 + r) + par;
+                        if (jo < L) gp[(size_t)jo * HW] = acc[r][par];
+                    }
+            }
+        }
+    }
+    // one ws row per block: each parameter has exactly one owning slot; sum its PX lanes
+    float* row = ws + (size_t)blockIdx.x * NPAR;
+    constexpr int OB1 = NW1, OW2 = OB1 + C2, OB2 = OW2 + NW2;
+    auto lane_sum = [](double v) {
+#pragma unroll
+        for (int o = PX / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        return v;
+    };
+#pragma unroll
+    for (int ii = 0; ii < NDI; ++ii) {
+        const int j = slot + ii * NSLOT;
+        if (j < ND) {  // slot-uniform: the PX lanes of the shuffle take the branch together
+            const int o2 = j / (2 * C2), o = (j / 2) % C2, kh = j & 1;
+#pragma unroll
+            for (int k = 0; k < KH; ++k) {
+                const double s = lane_sum(accD[ii][k]);
+                if (p == 0) row[OW2 + (o2 * C2 + o) * KB + kh * KH + k] = (float)s;
+            }
+            if (o == 0 && kh == 0) {
+                const double s = lane_sum(accb2[ii]);
+                if (p == 0) row[OB2 + o2] = (float)s;
+            }
+        }
+    }
+#pragma unroll
+    for (int ii = 0; ii < NEI; ++ii) {
+        const int j = slot + ii * NSLOT;
+        if (j < NE) {
+            const int o = j / (2 * NC), ci = (j / 2) % NC, kh = j & 1;
+#pragma unroll
+            for (int k = 0; k < KAH; ++k) {
+                const double s = lane_sum(accE[ii][k]);
+                if (p == 0 && kh * KAH + k < KA) row[(o * NC + ci) * KA + kh * KAH + k] = (float)s;
+            }
+            if (ci == 0 && kh == 0) {
+                const double s = lane_sum(accb1[ii]);
+                if (p == 0) row[OB1 + o] = (float)s;
+            }
+        }
+    }
+    // rows past the grid (the ABI sizes ws for one row per 64 pixels) are zero
+    for (int r = gridDim.x + blockIdx.x; r < nrows; r += gridDim.x)
+        for (int i = tid; i < NPAR; i += 256) ws[(size_t)r * NPAR + i] = 0.f;
+}
+
 // D[plane] = sum_hw g*(1-m) * u   (planes (b, c, t); m = spatial-cond mask of sample b or none)
 __global__ void plane_dot_kernel(const float* __restrict__ g, const float* __restrict__ u,
                                  const float* __restrict__ mask, int mask_S, int mask_ch, int nct, int HW,
@@ -567,6 +895,42 @@ extern "C" int nps_nhwc_to_nchw(const float* in, float* out, int B, int C, int H
     return 0;
 }
 
+namespace {
+template <int NC, int TW, int PX>
+constexpr size_t tc_bwd_lds() {
+    constexpr int L = 3 * TW, KA = (TW + 1) / 2, KB = (TW + 3) / 4 + 1 + (TW % 4 == 0 ? 1 : 0);
+    constexpr int L1 = (L - KA) / 2 + 1, C2 = 2 * NC, PP = PX + 1, QN = (KA + 1) / 2, RM = 4;
+    constexpr int MR = ((L + 1) / 2 + RM - 1) / RM * RM, GZW = MR + QN - 1, G2W = TW + 2 * (KB - 1);
+    return sizeof(float) * ((size_t)(NC * L + C2 * L1 + C2 * GZW + NC * G2W) * PP + C2 * NC * KA + NC * C2 * KB +
+                            C2 + NC + TW);
+}
+
+// resident blocks of the tw = 25 backward kernel over the whole device (its grid: one pass, no tail)
+template <int NC, int PX>
+int tc_bwd_blocks() {
+    static int n = 0;
+    if (n == 0) {
+        const void* f = (const void*)timeconv_bwd_fast_kernel<NC, 25, PX>;
+        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        int per_cu = 0, dev = 0, ncu = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, 256, tc_bwd_lds<NC, 25, PX>());
+        n = std::max(1, per_cu) * std::max(1, ncu);
+    }
+    return n;
+}
+
+// NPS_TC_BWD_GENERIC=1 routes every shape through the one-wave generic kernel (A/B and parity checks)
+bool tc_bwd_generic() {
+    static const int g = [] {
+        const char* e = std::getenv("NPS_TC_BWD_GENERIC");
+        return e && e[0] == '1' ? 1 : 0;
+    }();
+    return g != 0;
+}
+}  // namespace
+
 extern "C" int nps_timeconv_decode_bwd(const float* pre, const float* u, const float* w1, const float* b1,
                                        const float* w2, const float* b2, const float* dtcum, const float* mask,
                                        int mask_S, int mask_ch, const float* gout, float* gpre, float* ws, int B,
@@ -594,7 +958,19 @@ extern "C" int nps_timeconv_decode_bwd(const float* pre, const float* u, const f
     const int HW = H * W;
     const dim3 grid((HW + 63) / 64, B);
     hipStream_t s = (hipStream_t)stream;
-    if (num_c == 3 && tw == 25)  // the twophase cfgs (3 fields / 1 field, time_window 25)
+    if ((num_c == 3 || num_c == 1) && tw == 25 && !tc_bwd_generic()) {  // the twophase cfgs
+        constexpr int PX = 16;
+        const int ngroups = B * ((HW + PX - 1) / PX);
+        const int nrows = B * ((HW + 63) / 64);
+        const int par = num_c == 3 ? tc_bwd_blocks<3, PX>() : tc_bwd_blocks<1, PX>();
+        const int G = std::min(std::min(ngroups, nrows), par);
+        if (num_c == 3)
+            timeconv_bwd_fast_kernel<3, 25, PX><<<G, 256, tc_bwd_lds<3, 25, PX>(), s>>>(
+                pre, u, w1, b1, w2, b2, dtcum, mask, mask_S, mask_ch, gout, gpre, ws, HW, ngroups, nrows, act_tanh);
+        else
+            timeconv_bwd_fast_kernel<1, 25, PX><<<G, 256, tc_bwd_lds<1, 25, PX>(), s>>>(
+                pre, u, w1, b1, w2, b2, dtcum, mask, mask_S, mask_ch, gout, gpre, ws, HW, ngroups, nrows, act_tanh);
+    } else if (num_c == 3 && tw == 25)
         timeconv_bwd_kernel<3, 25><<<grid, 64, lds, s>>>(pre, u, w1, b1, w2, b2, dtcum, mask, mask_S, mask_ch, gout,
                                                          gpre, ws, num_c, tw, HW, ka, kb, L1, act_tanh, nparams);
     else if (num_c == 1 && tw == 25)
