@@ -46,7 +46,7 @@ __host__ __device__ constexpr int x3_patch_px_max(int ntaps, int tile_px) {
 #define NPS_X3_ARING 2  // weight-fragment ring depth of the 64-channel tiles
 #endif
 #ifndef NPS_X3_ARING_WIDE
-#define NPS_X3_ARING_WIDE 2  // ... of the wide tiles (3 fits without the spread store, not with it)
+#define NPS_X3_ARING_WIDE 3  // ... of the wide tiles: two K-groups ahead (3x3 class -3.5 %, profiles/r4/experiments)
 #endif
 #ifndef NPS_X3F_ABL
 #define NPS_X3F_ABL 0  // dev ablations of conv2d_x3f_kernel (speed only): 1 no patch fetch, 2 no spread stores,
