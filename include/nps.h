@@ -325,6 +325,10 @@ int nps_channel_sums(const float* x, long rows, int C, float* out, void* stream)
  * when the prologue has a GroupNorm; work = [B][2][Cin] fp64 scratch. */
 int nps_frame_pack_bwd(const nps_conv2d_t* a, const float* gy, float* const* dsrc, float* dgamma, float* dbeta,
                        double* work, void* stream);
+/* The same, also raising the range tag dtag[i] (NPS_TAG_FLOATS floats, or NULL; dtag itself may be NULL) to
+ * cover |dsrc[i]| — the range of the gradient the next conv backward reads as its dy. */
+int nps_frame_pack_bwd_tagged(const nps_conv2d_t* a, const float* gy, float* const* dsrc, float* const* dtag,
+                              float* dgamma, float* dbeta, double* work, void* stream);
 
 /* element-wise pieces of the differentiated graph */
 int nps_gelu(const float* x, float* y, long n, void* stream);                                /* nn.GELU() */

@@ -523,9 +523,12 @@ __global__ void frame_bwd_reduce4_kernel(nps_conv2d_t a, const float* __restrict
     }
 }
 
+// dtag[i] (or NULL): a range tag raised to cover |dsrc[i]| (one atomic per wave), so the conv backward that reads
+// the source gradient as its dy needs no absmax pass (nps_hip autograd: range tags)
 __global__ void frame_bwd_apply4_kernel(nps_conv2d_t a, const float* __restrict__ gy, const double* __restrict__ PQ,
                                         float* d0, float* d1, float* d2, float* __restrict__ dgamma,
-                                        float* __restrict__ dbeta, int px_per_block) {
+                                        float* __restrict__ dbeta, int px_per_block, float* t0, float* t1,
+                                        float* t2) {
     __shared__ float2 tab[16];
     __shared__ float s12[16][2];
     const int b = blockIdx.y, si = blockIdx.z;
@@ -561,7 +564,8 @@ __global__ void frame_bwd_apply4_kernel(nps_conv2d_t a, const float* __restrict_
     const int q = threadIdx.x % Q, lr = threadIdx.x / Q;
     const int npix = S.H * S.W;
     const int p0 = blockIdx.x * px_per_block, p1 = min(npix, p0 + px_per_block);
-    if (lr >= per || p0 + lr >= p1) return;
+    float amax = 0.f;
+    if (!(lr >= per || p0 + lr >= p1)) {  // (no early return: the tag publish below is wave-collective)
     const int c0 = lo + 4 * q;
     const int gidx = c0 / cpg;
     const float2 mr = a.gn_stats ? tab[gidx] : make_float2(0.f, 1.f);
@@ -596,6 +600,7 @@ __global__ void frame_bwd_apply4_kernel(nps_conv2d_t a, const float* __restrict_
             }
         }
         *reinterpret_cast<f32x4*>(dp + (size_t)pix * S.C) = d;
+        amax = fmaxf(amax, fmaxf(fmaxf(fabsf(d[0]), fabsf(d[1])), fmaxf(fabsf(d[2]), fabsf(d[3]))));
         xs += dx;
         ys += dy;
         if (xs >= S.W) {
@@ -603,6 +608,8 @@ __global__ void frame_bwd_apply4_kernel(nps_conv2d_t a, const float* __restrict_
             ++ys;
         }
     }
+    }
+    nps::tag_publish(si == 0 ? t0 : (si == 1 ? t1 : t2), amax, nps::wave_salt());
 }
 
 inline int grid_for(long n, int per_block = 256 * 8, int cap = 4096) {
@@ -714,6 +721,12 @@ extern "C" int nps_scaled_diff(const float* a, const float* b, const double* sca
 
 extern "C" int nps_frame_pack_bwd(const nps_conv2d_t* ap, const float* gy, float* const* dsrc, float* dgamma,
                                   float* dbeta, double* work, void* stream) {
+    return nps_frame_pack_bwd_tagged(ap, gy, dsrc, nullptr, dgamma, dbeta, work, stream);
+}
+
+extern "C" int nps_frame_pack_bwd_tagged(const nps_conv2d_t* ap, const float* gy, float* const* dsrc,
+                                         float* const* dtag, float* dgamma, float* dbeta, double* work,
+                                         void* stream) {
     NPS_CHECK_ARG(ap && gy && dsrc, "frame_pack_bwd: null");
     const nps_conv2d_t& a = *ap;
     NPS_CHECK_ARG(a.nsrc >= 1 && a.nsrc <= NPS_MAX_SRC && a.B > 0 && a.Hin > 0 && a.Win > 0 && a.Cin > 0,
@@ -754,12 +767,19 @@ extern "C" int nps_frame_pack_bwd(const nps_conv2d_t* ap, const float* gy, float
         pmax = std::max(pmax, (long)a.src[i].H * a.src[i].W);
     }
     float* d[3] = {dsrc[0], a.nsrc > 1 ? dsrc[1] : nullptr, a.nsrc > 2 ? dsrc[2] : nullptr};
-    if (quad)
+    float* t[3] = {nullptr, nullptr, nullptr};
+    for (int i = 0; dtag != nullptr && i < a.nsrc; ++i) t[i] = d[i] != nullptr ? dtag[i] : nullptr;
+    if (quad) {
         frame_bwd_apply4_kernel<<<dim3((unsigned)((pmax + PXB - 1) / PXB), a.B, a.nsrc), 256, 0, s>>>(
-            a, gy, work, d[0], d[1], d[2], dgamma, dbeta, PXB);
-    else
-        frame_bwd_apply_kernel<<<dim3(grid_for(nmax, 256 * 8, 2048), a.B, a.nsrc), 256, 0, s>>>(a, gy, work, d[0], d[1],
-                                                                                               d[2], dgamma, dbeta);
+            a, gy, work, d[0], d[1], d[2], dgamma, dbeta, PXB, t[0], t[1], t[2]);
+        NPS_CHECK_LAUNCH("frame_pack_bwd apply");
+        return 0;
+    }
+    frame_bwd_apply_kernel<<<dim3(grid_for(nmax, 256 * 8, 2048), a.B, a.nsrc), 256, 0, s>>>(a, gy, work, d[0], d[1],
+                                                                                           d[2], dgamma, dbeta);
     NPS_CHECK_LAUNCH("frame_pack_bwd apply");
+    for (int i = 0; i < a.nsrc; ++i)  // (the element-wise kernel publishes no tags: one absmax pass per source)
+        if (t[i] != nullptr && nps_absmax(d[i], (long)a.B * a.src[i].H * a.src[i].W * a.src[i].C, t[i], stream) != 0)
+            return -2;
     return 0;
 }

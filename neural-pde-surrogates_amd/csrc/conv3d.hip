@@ -20,6 +20,7 @@ namespace {
 typedef unsigned short bf16_t;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ float bf2f(unsigned v) { return __uint_as_float(v << 16); }
 __device__ __forceinline__ unsigned f2bf(float v) { return (unsigned)__builtin_bit_cast(bf16_t, (__bf16)v); }
@@ -44,6 +45,12 @@ template <> struct Vec8<bf16_t> {
         a[e >> 1] = (e & 1) ? ((w & 0xffffu) | (h << 16)) : ((w & 0xffff0000u) | h);
     }
     __device__ __forceinline__ void store(bf16_t* p) const { *reinterpret_cast<u32x4*>(p) = a; }
+    // channels [4h, 4h + 4) from p (8-B aligned: a 4-channel run of a source with C % 4 == 0)
+    __device__ __forceinline__ void load_half(int h, const bf16_t* p) {
+        const u32x2 w = *reinterpret_cast<const u32x2*>(p);
+        a[2 * h] = w[0];
+        a[2 * h + 1] = w[1];
+    }
 };
 template <> struct Vec8<float> {
     u32x4 a, b;
@@ -57,6 +64,9 @@ template <> struct Vec8<float> {
         b = reinterpret_cast<const u32x4*>(p)[1];
     }
     __device__ __forceinline__ void load_elem(int e, const float* p) { set(e, *p); }
+    __device__ __forceinline__ void load_half(int h, const float* p) {
+        if (h == 0) a = *reinterpret_cast<const u32x4*>(p); else b = *reinterpret_cast<const u32x4*>(p);
+    }
     __device__ __forceinline__ void store(float* p) const {
         reinterpret_cast<u32x4*>(p)[0] = a;
         reinterpret_cast<u32x4*>(p)[1] = b;
@@ -94,6 +104,14 @@ __device__ __forceinline__ void load_piece(Vec8<T>& r, const nps_conv3d_t& a, in
                                  ((((size_t)b * s.D + dd) * s.H + hh) * s.W + ww) * s.C;
                     if (c0 >= lo && c0 + 8 <= lo + s.C && (s.C & 7) == 0 && ((c0 - lo) & 7) == 0) {
                         r.load(p + (c0 - lo));
+                    } else if ((s.C & 3) == 0 && ((c0 - lo) & 3) == 0) {
+                        // 4-channel runs (C % 4 == 0, e.g. 64 + 4 channels): one 8-B (bf16) / 16-B load per
+                        // half inside the source instead of 8 element loads
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            const int c = c0 + 4 * h;
+                            if (c >= lo && c + 4 <= lo + s.C) r.load_half(h, p + (c - lo));
+                        }
                     } else {
 #pragma unroll
                         for (int e = 0; e < 8; ++e) {
@@ -369,7 +387,6 @@ __global__ __launch_bounds__(256) void conv3d_kernel(const nps_conv3d_t a, int n
                     if (a.accumulate) o += *reinterpret_cast<const f32x4*>(op);
                     *reinterpret_cast<f32x4*>(op) = o;
                 } else if (vec4) {  // bf16: 4 channels = one 8-B access
-                    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
                     float o[4] = {v[0], v[1], v[2], v[3]};
                     if (ap) {
                         const u32x2 w = *reinterpret_cast<const u32x2*>(ap);
@@ -451,76 +468,130 @@ __global__ __launch_bounds__(256) void gn_stats3d_kernel(const nps_conv3d_t a, i
             const bool vec = (src.C & 7) == 0;
             const bool inside = src.off_d >= 0 && src.off_h >= 0 && src.off_w >= 0 && src.off_d + src.D <= a.Dc &&
                                 src.off_h + src.H <= a.Hc && src.off_w + src.W <= a.Wc;
-            if (vec && inside && (cpg & 7) == 0 && (lo & 7) == 0) {  // 8-aligned pieces: one group each
-                // the source lies wholly inside the frame: a linear sweep of its 8-channel pieces, the group of
-                // a piece from its channel chunk (no voxel decomposition)
-                for (int it = blockIdx.x * 256 + threadIdx.x; it < nitem; it += gridDim.x * 256) {
-                    Vec8<T> v;
-                    v.load(base + (size_t)it * 8);
-                    const int g0 = (lo + (it % nck) * 8) / cpg;
-                    float fs = 0.f, fq = 0.f;
+            const long nel = (long)src.D * src.H * src.W * src.C;  // elements per sample
+            if (inside && (src.C & 3) == 0 && (cpg & 3) == 0 && (lo & 3) == 0 && (nel & 7) == 0 &&
+                nel < (1L << 31)) {
+                // the source lies wholly inside the frame: a linear sweep of its elements 8 at a time (16-B loads
+                // for bf16 whatever C % 8 is), each 4-element half in one group (C, the channels per group and the
+                // source's first channel all % 4 == 0)
+                const int nfl = (int)(nel / 8);
+                auto acc8 = [&](const Vec8<T>& v, int it) {
+                    if (G == 1) {  // one group (GroupNorm(1)): no channel index at all
+                        float fs = 0.f, fq = 0.f;
 #pragma unroll
-                    for (int e = 0; e < 8; ++e) {
-                        const float x = v.get(e);
-                        fs += x;
-                        fq = fmaf(x, x, fq);
+                        for (int e = 0; e < 8; ++e) {
+                            const float x = v.get(e);
+                            fs += x;
+                            fq = fmaf(x, x, fq);
+                        }
+                        s[0] += fs;
+                        q[0] += fq;
+                        return;
                     }
 #pragma unroll
-                    for (int g = 0; g < 8; ++g)
-                        if (g == g0) {
-                            s[g] += fs;
-                            q[g] += fq;
+                    for (int h = 0; h < 2; ++h) {
+                        const int g0 = (lo + (int)((unsigned)(it * 8 + 4 * h) % (unsigned)src.C)) / cpg;
+                        float fs = 0.f, fq = 0.f;
+#pragma unroll
+                        for (int e = 4 * h; e < 4 * h + 4; ++e) {
+                            const float x = v.get(e);
+                            fs += x;
+                            fq = fmaf(x, x, fq);
                         }
+#pragma unroll
+                        for (int g = 0; g < 8; ++g)
+                            if (g == g0) {
+                                s[g] += fs;
+                                q[g] += fq;
+                            }
+                    }
+                };
+                // U pieces per thread in flight (one 16-B load per piece): with one, a wave kept 1 KiB in flight
+                // and the sweep ran at ~1.6 TB/s (latency-bound)
+                constexpr int U = 4;
+                const int stride = gridDim.x * 256;
+                int it = blockIdx.x * 256 + threadIdx.x;
+                for (; it + (U - 1) * stride < nfl; it += U * stride) {
+                    Vec8<T> v[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) v[u].load(base + (size_t)(it + u * stride) * 8);
+#pragma unroll
+                    for (int u = 0; u < U; ++u) acc8(v[u], it + u * stride);
+                }
+                for (; it < nfl; it += stride) {
+                    Vec8<T> v;
+                    v.load(base + (size_t)it * 8);
+                    acc8(v, it);
                 }
                 lo += src.C;
                 continue;
             }
-            for (int it = blockIdx.x * 256 + threadIdx.x; it < nitem; it += gridDim.x * 256) {
+            // (cropped / unaligned sources) U pieces per thread in flight, as the fast path; a piece outside the
+            // frame loads nothing and adds zeros
+            auto fetch = [&](Vec8<T>& v, int it) {
                 const int ck = it % nck;
                 const int vox = it / nck;
                 const int ww = vox % src.W;
                 const int r = vox / src.W;
                 const int hh = r % src.H, dd = r / src.H;
                 const int cd = dd + src.off_d, ch = hh + src.off_h, cw = ww + src.off_w;
-                if (cd < 0 || cd >= a.Dc || ch < 0 || ch >= a.Hc || cw < 0 || cw >= a.Wc) continue;
-                const T* p = base + (size_t)vox * src.C + ck * 8;
-                Vec8<T> v;
                 v.zero();
+                if (cd < 0 || cd >= a.Dc || ch < 0 || ch >= a.Hc || cw < 0 || cw >= a.Wc) return;
+                const T* p = base + (size_t)vox * src.C + ck * 8;
                 if (vec) {
                     v.load(p);
+                } else if ((src.C & 3) == 0) {  // 4-channel runs (e.g. the 4 conditioning channels)
+                    v.load_half(0, p);
+                    if (ck * 8 + 8 <= src.C) v.load_half(1, p + 4);
                 } else {
 #pragma unroll
                     for (int e = 0; e < 8; ++e)
                         if (ck * 8 + e < src.C) v.load_elem(e, p + e);
                 }
-                const int c0 = lo + ck * 8;
-                if (vec && (cpg & 7) == 0 && (lo & 7) == 0) {  // the 8 channels lie in one group
-                    const int g0 = c0 / cpg;
-                    float fs = 0.f, fq = 0.f;
+            };
+            constexpr int U = 4;
+            const int stride = gridDim.x * 256;
+            const int it0 = blockIdx.x * 256 + threadIdx.x;
+            for (int itb = it0; itb < nitem; itb += U * stride) {
+                Vec8<T> vv[U];
 #pragma unroll
-                    for (int e = 0; e < 8; ++e) {
-                        const float x = v.get(e);
-                        fs += x;
-                        fq = fmaf(x, x, fq);
-                    }
+                for (int u = 0; u < U; ++u)
+                    if (itb + u * stride < nitem) fetch(vv[u], itb + u * stride);
 #pragma unroll
-                    for (int g = 0; g < 8; ++g)
-                        if (g == g0) {
-                            s[g] += fs;
-                            q[g] += fq;
+                for (int u = 0; u < U; ++u) {
+                    const int it = itb + u * stride;
+                    if (it >= nitem) break;
+                    const Vec8<T>& v = vv[u];
+                    const int ck = it % nck;
+                    const int c0 = lo + ck * 8;
+                    if (vec && (cpg & 7) == 0 && (lo & 7) == 0) {  // the 8 channels lie in one group
+                        const int g0 = c0 / cpg;
+                        float fs = 0.f, fq = 0.f;
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) {
+                            const float x = v.get(e);
+                            fs += x;
+                            fq = fmaf(x, x, fq);
                         }
-                } else {
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) {
-                        if (ck * 8 + e >= src.C) continue;
-                        const float x = v.get(e);
-                        const int ge = (c0 + e) / cpg;
 #pragma unroll
                         for (int g = 0; g < 8; ++g)
-                            if (g == ge) {
-                                s[g] += x;
-                                q[g] += (double)x * x;
+                            if (g == g0) {
+                                s[g] += fs;
+                                q[g] += fq;
                             }
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) {
+                            if (ck * 8 + e >= src.C) continue;
+                            const float x = v.get(e);
+                            const int ge = (c0 + e) / cpg;
+#pragma unroll
+                            for (int g = 0; g < 8; ++g)
+                                if (g == ge) {
+                                    s[g] += x;
+                                    q[g] += (double)x * x;
+                                }
+                        }
                     }
                 }
             }
@@ -567,13 +638,28 @@ __global__ __launch_bounds__(256) void frame_pack3d_kernel(const nps_conv3d_t a,
     const int npc = Cpad / 8;
     const int nitem = a.Dc * a.Hc * a.Wc * npc;
     T* ob = out + (size_t)b * a.Dc * a.Hc * a.Wc * Cpad;
-    for (int it = blockIdx.x * 256 + threadIdx.x; it < nitem; it += gridDim.x * 256) {
-        const int pc = it % npc;
+    // one source covering the frame exactly, C % 4 == 0: its voxel index is the frame's, no decomposition
+    const nps_src3_t& s0 = a.src[0];
+    const bool flat = a.nsrc == 1 && s0.off_d == 0 && s0.off_h == 0 && s0.off_w == 0 && s0.D == a.Dc &&
+                      s0.H == a.Hc && s0.W == a.Wc && (s0.C & 3) == 0;
+    const T* fb = reinterpret_cast<const T*>(s0.ptr) + (size_t)b * a.Dc * a.Hc * a.Wc * s0.C;
+    auto fetch = [&](Vec8<T>& v, int it) {
         const int vox = it / npc;
+        const int pc = it - vox * npc;
+        if (flat) {
+            v.zero();
+            const T* p = fb + (size_t)vox * s0.C + pc * 8;
+            if (pc * 8 + 4 <= s0.C) v.load_half(0, p);
+            if (pc * 8 + 8 <= s0.C) v.load_half(1, p + 4);
+            return;
+        }
         const int cw = vox % a.Wc, r = vox / a.Wc;
         const int ch = r % a.Hc, cd = r / a.Hc;
-        Vec8<T> v;
         load_piece<T>(v, a, b, cd, ch, cw, pc * 8);
+    };
+    auto put = [&](Vec8<T>& v, int it) {
+        const int vox = it / npc;
+        const int pc = it - vox * npc;
         if (gn || a.pre_act) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
@@ -584,6 +670,22 @@ __global__ __launch_bounds__(256) void frame_pack3d_kernel(const nps_conv3d_t a,
             }
         }
         v.store(ob + (size_t)vox * Cpad + pc * 8);
+    };
+    // U pieces per thread: all loads issued before the first store (vmcnt retires loads and stores in order)
+    constexpr int U = 4;
+    const int stride = gridDim.x * 256;
+    int it = blockIdx.x * 256 + threadIdx.x;
+    for (; it + (U - 1) * stride < nitem; it += U * stride) {
+        Vec8<T> v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) fetch(v[u], it + u * stride);
+#pragma unroll
+        for (int u = 0; u < U; ++u) put(v[u], it + u * stride);
+    }
+    for (; it < nitem; it += stride) {
+        Vec8<T> v;
+        fetch(v, it);
+        put(v, it);
     }
 }
 

@@ -121,6 +121,8 @@ _SIGS = {
     "nps_conv2d_wgrad_x3": (_i, [ctypes.POINTER(WgradArgs), _vp, _vp, _vp, _vp]),
     "nps_channel_sums": (_i, [_vp, _l, _i, _vp, _vp]),
     "nps_frame_pack_bwd": (_i, [ctypes.POINTER(Conv2dArgs), _vp, ctypes.POINTER(ctypes.c_void_p), _vp, _vp, _vp, _vp]),
+    "nps_frame_pack_bwd_tagged": (_i, [ctypes.POINTER(Conv2dArgs), _vp, ctypes.POINTER(ctypes.c_void_p),
+                                       ctypes.POINTER(ctypes.c_void_p), _vp, _vp, _vp, _vp]),
     "nps_gelu": (_i, [_vp, _vp, _l, _vp]),
     "nps_gelu_bwd": (_i, [_vp, _vp, _vp, _l, _vp]),
     "nps_add_at": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp]),

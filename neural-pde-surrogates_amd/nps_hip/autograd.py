@@ -60,13 +60,16 @@ def wgrad(a: torch.Tensor, x: torch.Tensor, KH: int, KW: int, dil=1, pad=(0, 0),
     p.KH, p.KW, p.dil, p.pad_y, p.pad_x, p.circ = KH, KW, dil, pad[0], pad[1], circ
     p.g = ptr(g)
     if ops.CONV_PRECISION == ops.PREC_X3F16 and KH == KW and KH <= 3 and dil == 1 and M % 4 == 0 and N % 4 == 0:
-        ar = a_range if a_range is not None else ops.absmax(a)
-        xr = ops.absmax(x)
+        # operand ranges: the tensors' live range tags (written by the kernels that produced them), an absmax
+        # pass only for a tensor without one (ops.input_tag); a_range: a's tag pointer when the caller has it
+        ops.reserve_tags(a.device, 2)
+        ar = a_range if a_range is not None else _range_ptr(a)
+        xr = _range_ptr(x)
         ws = torch.empty(lib.nps_wgrad_x3_ws_floats(M, N, KH, KW), dtype=torch.float32, device=a.device)
         arith = "x3w"
 
         def launch():
-            check(lib.nps_conv2d_wgrad_x3(ctypes.byref(p), ptr(ar), ptr(xr), ptr(ws), stream_ptr()), "conv2d_wgrad_x3")
+            check(lib.nps_conv2d_wgrad_x3(ctypes.byref(p), ar, xr, ptr(ws), stream_ptr()), "conv2d_wgrad_x3")
     else:
         arith = "f32w"
 
@@ -82,6 +85,24 @@ def wgrad(a: torch.Tensor, x: torch.Tensor, KH: int, KW: int, dil=1, pad=(0, 0),
     else:
         launch()
     return g
+
+
+def _range_ptr(t: torch.Tensor) -> int:
+    """Device pointer of an upper bound of |t| (a range tag, include/nps.h): t's live tag, else a fresh absmax."""
+    if ops.USE_IN_TAGS:
+        return ops.input_tag(t)
+    return ptr(_keep(ops.absmax(t)))
+
+
+_KEEP = []
+
+
+def _keep(t):
+    """Hold a one-off range tensor until the next backward launch has been enqueued (stream-ordered reuse of
+    the caching allocator makes an early free safe; the list only bounds its lifetime to a few launches)."""
+    _KEEP.append(t)
+    del _KEEP[:-8]
+    return t
 
 
 def channel_sums(x: torch.Tensor) -> torch.Tensor:
@@ -144,8 +165,14 @@ class FrameFn(torch.autograd.Function):
         dsrc = [torch.empty_like(t) if need[i] else None for i, t in enumerate(srcs)]
         arr = (ctypes.c_void_p * 3)(*[(d.data_ptr() if d is not None else None) for d in dsrc] +
                                    [None] * (3 - len(dsrc)))
-        check(lib.nps_frame_pack_bwd(ctypes.byref(a), ptr(gout), arr, ptr(dgamma), ptr(dbeta), ptr(work),
-                                     stream_ptr()), "frame_pack_bwd")
+        # each source gradient leaves with a range tag: the conv backward reading it as dy needs no absmax pass
+        tags = [None] * 3
+        if ops.USE_OUT_TAGS:
+            ops.reserve_tags(gout.device, len(dsrc))
+            tags[:len(dsrc)] = [ops.new_tag(d) if d is not None else None for d in dsrc]
+        tarr = (ctypes.c_void_p * 3)(*tags)
+        check(lib.nps_frame_pack_bwd_tagged(ctypes.byref(a), ptr(gout), arr, tarr, ptr(dgamma), ptr(dbeta),
+                                            ptr(work), stream_ptr()), "frame_pack_bwd")
         return (None, dgamma, dbeta, *dsrc)
 
 
@@ -229,8 +256,10 @@ class Conv2dFn(torch.autograd.Function):
         B, Ho, Wo, Cout = gy.shape
         Cin = w.shape[1]
         dx = dw = db = rng = None
+        if ops.CONV_PRECISION == ops.PREC_X3F16 and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2]):
+            ops.reserve_tags(gy.device, 3)
+            rng = _range_ptr(gy)  # gradients: any magnitude (its tag, or one absmax pass shared by dx and dw)
         if ctx.needs_input_grad[1]:
-            rng = ops.absmax(gy) if ops.CONV_PRECISION == ops.PREC_X3F16 else None  # gradients: any magnitude
             if s == 1:
                 if circ:
                     dx = ops.conv2d([Src(gy)], (Ho, Wo), _pack_plain(_dgrad_weight(w), d), None, Cin, KH, KW, dil=d,
@@ -300,9 +329,8 @@ class ConvTranspose2dFn(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[1]:
             w2 = w.detach().view(Cin, Cout, 2, 2, 2, 2).permute(0, 3, 5, 1, 2, 4).reshape(Cin, 4 * Cout, 2, 2)
-            rng = ops.absmax(gout) if ops.CONV_PRECISION == ops.PREC_X3F16 else None
             dxp = ops.conv2d([Src(dq)], (Hp + 1, Wp + 1), _pack_plain(w2.contiguous()), None, Cin, 2, 2,
-                             out_hw=(Hp, Wp), in_scale=rng)
+                             out_hw=(Hp, Wp))  # dq's range: its tag (ops.input_tag), shared from gout
             if c:
                 dx = torch.empty_like(x)
                 check(lib.nps_circular_fold(ptr(dxp), ptr(dx), B, H, W, Cin, c, stream_ptr()), "circular_fold")

@@ -7,7 +7,7 @@ cat / pad / crop is ever materialised.
 """
 import math
 import os
-from typing import List, NamedTuple, Optional, Sequence
+from typing import List, NamedTuple, Optional, Sequence, Union
 
 import torch
 
@@ -362,7 +362,7 @@ def conv2d(srcs: Sequence[Src], frame_hw, wpack: torch.Tensor, bias: Optional[to
            KW: int, stride=1, dil=1, pad=(0, 0), circ=0, out_hw=None, gn: Optional[GN] = None, pre_act=0,
            out: Optional[torch.Tensor] = None, out_nchw=False, out_os=1, out_off=(0, 0), accumulate=False,
            addends: Sequence[torch.Tensor] = (), act=0, add_after_act=False, pad_bottom=None,
-           in_scale: Optional[torch.Tensor] = None, out_stats: Optional[torch.Tensor] = None, phases: int = 1,
+           in_scale: Optional[Union[torch.Tensor, int]] = None, out_stats: Optional[torch.Tensor] = None, phases: int = 1,
            s2d_pad: Optional[int] = None):
     """One fused conv launch.  `pad` = top/left zero padding (in the circularly
     extended frame), `pad_bottom` defaults to `pad`.  `out_stats`: a new_stats() buffer the launch adds
@@ -439,8 +439,8 @@ def conv2d(srcs: Sequence[Src], frame_hw, wpack: torch.Tensor, bias: Optional[to
         a.nphase, a.phase_wstride = 4, wpack.nps_phase_stride
     reserve_tags(out.device, len(srcs) + 1)  # every tag this launch reads or writes, before any pointer
     if a.precision == PREC_X3F16:
-        if in_scale is not None:  # explicit range (gradients): overrides the sources' tags
-            a.in_scale = ptr(in_scale)
+        if in_scale is not None:  # explicit range (a tag tensor or its device pointer): overrides the sources' tags
+            a.in_scale = in_scale if isinstance(in_scale, int) else ptr(in_scale)
         elif USE_IN_TAGS and not (fused and gn is not None):
             # the sources' tags (a fused GroupNorm prologue normalises the frame: its output range is not
             # the sources'; the kernel bounds it from gamma, beta and the group size, gn_prologue_scale)

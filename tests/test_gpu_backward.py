@@ -151,6 +151,48 @@ def test_conv_transpose_backward_vs_torch(circ):
     assert rel_l2(m.bias.grad, sd["bias"].grad) < TOL
 
 
+@pytest.mark.parametrize("quad", [True, False])
+def test_frame_backward_source_gradient_range_tags(quad):
+    """nps_frame_pack_bwd_tagged: each source gradient's range tag equals max |dsrc| (the quad kernel publishes it
+    per wave, the element-wise path runs one absmax per source), so the conv backward that reads it as dy scales
+    by it instead of an absmax pass; gradients as the untagged entry point's."""
+    import ctypes
+    from nps_hip import ops, lib, ptr, stream_ptr, check, Conv2dArgs
+    torch.manual_seed(11)
+    c1 = 12 if quad else 6  # 6 channels (and 5 per group): off the quad kernels
+    B, H, W = 2, 13, 17
+    s1, s2 = torch.randn(B, H, W, c1, device=DEV), torch.randn(B, H + 2, W + 2, 4, device=DEV) * 3
+    srcs = [ops.Src(s1), ops.Src(s2, -1, -1)]
+    st = ops.group_norm_stats(srcs, (H, W), 2)
+    C = c1 + 4
+    gamma, beta = 1 + 0.1 * torch.randn(C, device=DEV), 0.1 * torch.randn(C, device=DEV)
+    gy = torch.randn(B, H, W, C, device=DEV)
+    outs = []
+    for tagged in (False, True):
+        a = Conv2dArgs()
+        a.nsrc, a.src = 2, ops._c_src(srcs)
+        a.B, a.Hin, a.Win, a.Cin = B, H, W, C
+        a.gn_stats, a.gn_gamma, a.gn_beta, a.gn_groups, a.gn_eps = ptr(st), ptr(gamma), ptr(beta), 2, 1e-5
+        a.pre_act = 1
+        d = [torch.empty_like(s1), torch.empty_like(s2)]
+        dg, db = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+        work = torch.empty((B, 2, C), dtype=torch.float64, device=DEV)
+        arr = (ctypes.c_void_p * 3)(d[0].data_ptr(), d[1].data_ptr(), None)
+        if tagged:
+            ops.reserve_tags(gy.device, 2)
+            tags = (ctypes.c_void_p * 3)(ops.new_tag(d[0]), ops.new_tag(d[1]), None)
+            check(lib.nps_frame_pack_bwd_tagged(ctypes.byref(a), ptr(gy), arr, tags, ptr(dg), ptr(db), ptr(work),
+                                                stream_ptr()), "frame_pack_bwd_tagged")
+            for t in d:
+                assert ops.tag_value(t) == float(t.abs().max())
+        else:
+            check(lib.nps_frame_pack_bwd(ctypes.byref(a), ptr(gy), arr, ptr(dg), ptr(db), ptr(work), stream_ptr()),
+                  "frame_pack_bwd")
+        outs.append(d)
+    for u, t in zip(*outs):  # (the GroupNorm reduction's float atomics make two runs differ in the last bits)
+        torch.testing.assert_close(u, t, rtol=1e-5, atol=1e-6)
+
+
 def test_residual_block_backward_concat_crop_groupnorm():
     """cat(h, crop(s), crop(vb)) -> GN(1)+GELU -> conv1 -> GN+GELU -> conv2, + crop-padded 1x1 shortcut."""
     from models.enc_proc_dec_components.proc_unet_modern import ResidualBlock

@@ -161,3 +161,28 @@ def test_conv3d_upsample_transposed(dt, shape):
     y = ops.conv3d([ops.Src3(_ndhwc(x, dt))], (D, H, W), wp, b.to(DEV), 40, 2, transposed=True, circ=1, zpad=1)
     assert y.shape[1:4] == ref.shape[2:]
     assert rel_l2(_ncdhw(y), ref) < TOL[dt]
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("groups", [1, 2, 4])
+def test_gn_stats3d_and_frame_pack3d_channels_mod4(dt, groups):
+    """C5's 64 + 4 = 68-channel frames (C % 8 == 4): the moments sweep the source as a flat element array
+    (16-B loads, a group per 4-element half) when the channels per group are a multiple of 4 (GroupNorm 1, 2)
+    and fall back to per-element pieces otherwise (4 groups of 17); the frame pack reads 4-channel halves.
+    Against the fp64 GroupNorm + GELU of the same frame."""
+    from nps_hip import ops
+    torch.manual_seed(7)
+    B, dhw = 2, (5, 6, 11)
+    x = torch.randn(B, 68, *dhw) * 1.5 + 0.3
+    fr = _rt(x, dt)
+    st = ops.gn_stats3d([ops.Src3(_ndhwc(x, dt))], dhw, groups).cpu()
+    g = fr.view(B, groups, 68 // groups, *dhw)
+    torch.testing.assert_close(st[:, :, 0], g.sum((2, 3, 4, 5)), rtol=1e-6, atol=1e-3)
+    torch.testing.assert_close(st[:, :, 1], (g ** 2).sum((2, 3, 4, 5)), rtol=1e-6, atol=1e-3)
+    gamma, beta = 1 + 0.2 * torch.randn(68), 0.1 * torch.randn(68)
+    gn = ops.GN(st.to(DEV), gamma.to(DEV), beta.to(DEV), groups, 1e-5)
+    packed = ops.frame_pack3d([ops.Src3(_ndhwc(x, dt))], dhw, gn, pre_act=1)
+    assert packed.shape[-1] == 80 and float(packed[..., 68:].abs().max()) == 0.0
+    want = F.gelu(F.group_norm(fr, groups, gamma.double(), beta.double(), eps=1e-5))
+    got = packed[..., :68].float().cpu().permute(0, 4, 1, 2, 3).double()
+    assert rel_l2(got, _rt(want, dt) if dt == torch.bfloat16 else want) < (1e-2 if dt == torch.bfloat16 else 1e-6)

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 GPU pass (gpurun): parity suite, C3 bench + rocprof, B=2 line, training lines (B=2, B=16) + rocprof of
 # the B=16 step, C5 (ufno3d bf16) line + rocprof, N=2 training rehearsal.  Outputs: gpurun_out/${TAG}_*.
-# usage: tools/r4_full.sh TAG [steps...]   steps: tests sel($TESTSEL) bench prof b2 train trainprof c5 c5prof reh (default: all)
+# usage: tools/r4_full.sh TAG [steps...]   steps: tests sel($TESTSEL) bench prof b2 b2prof train trainprof c5 c5prof reh (default: all)
 set -o pipefail
 TAG=${1:-r4full}; shift
 STEPS="${@:-tests bench prof b2 train trainprof c5 c5prof reh}"
@@ -18,6 +18,8 @@ for s in $STEPS; do
     prof)  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d ${O}_prof -o run -- python3 bench.py --steps 3 --warmup 1 --cpu-calls 0 \
              > ${O}_prof.log 2>&1 || { echo "prof failed"; tail -20 ${O}_prof.log; exit 1; } ;;
     b2)    timeout -k 10 300 python -u bench.py --global-batch 2 --cpu-calls 0 > ${O}_b2.json 2> ${O}_b2.err || { echo "b2 failed"; tail -20 ${O}_b2.err; exit 1; }; tail -c 300 ${O}_b2.json ;;
+    b2prof) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d ${O}_b2prof -o run -- python3 bench.py --global-batch 2 --steps 10 --warmup 2 --cpu-calls 0 \
+             > ${O}_b2prof.log 2>&1 || { echo "b2 prof failed"; tail -20 ${O}_b2prof.log; exit 1; } ;;
     train) for gb in 2 16; do timeout -k 10 400 python -u bench.py --mode train --steps 5 --warmup 2 --global-batch $gb > ${O}_train_b$gb.json 2> ${O}_train_b$gb.err \
              || { echo "train $gb failed"; tail -20 ${O}_train_b$gb.err; exit 1; }; tail -c 300 ${O}_train_b$gb.json; done ;;
     trainprof) timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d ${O}_tprof -o run -- python3 bench.py --mode train --steps 3 --warmup 1 --global-batch 16 --cpu-calls 0 \
