@@ -15,6 +15,7 @@
 // accumulator (~2^-21 relative per product, the fp32 class of the reference's FMA chain).
 #include "conv2d_common.hpp"
 
+#include <cstdlib>
 #include <type_traits>
 
 namespace {
@@ -69,10 +70,15 @@ __device__ __attribute__((aligned(16))) float wx_zero4[4];
 // MFMAs of tile i splits tile i + 1 into the other LDS buffer (VALU beside the partner wave's MFMAs); one
 // barrier per tile.  Lanes 0-15 of a wave-quarter take 16 consecutive pixel pairs, so the packed 2-pixel
 // b32 writes of one instruction hit distinct banks.
+// Grid: base = n_mt * n_nt (m, n) tiles x splits pixel ranges, 1-D.  With splits % 8 == 0 the (tile, split) of
+// work-group l is XCD-aware: work-groups are dealt to the 8 XCDs round-robin (l % 8), and the `base` tiles of
+// one split — which read the same A and X pixels (each tile its own 64-channel slices) — are consecutive
+// work-groups of ONE XCD, so the pixels come from HBM once and from that XCD's L2 for the other tiles (for a
+// 1x1 conv the kernel is bound by those reads: 3 m-tiles x 3 n-tiles read every byte 3 times).
 template <int KH, int KW>
 __global__ __launch_bounds__(512) void wgrad_x3_kernel(const nps_wgrad_t p, const float* a_range,
                                                        const float* x_range, float* __restrict__ ws, int ntiles,
-                                                       int tiles_per_split, int n_nt) {
+                                                       int tiles_per_split, int n_nt, int base, int xcd_remap) {
     constexpr int NT = KH * KW;
     constexpr bool ROWSPLIT = NT == 1;
     constexpr int NT0 = ROWSPLIT ? 1 : (NT + 1) / 2;       // taps of waves 0-3
@@ -89,10 +95,19 @@ __global__ __launch_bounds__(512) void wgrad_x3_kernel(const nps_wgrad_t p, cons
     constexpr int BUF = 2 * (64 * WX_APITCH + 64 * BP);      // halves per LDS buffer
     extern __shared__ __attribute__((aligned(16))) _Float16 wsm[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int nt = blockIdx.x % n_nt, mt = blockIdx.x / n_nt;
+    int tile, split;
+    if (xcd_remap) {
+        const int j = blockIdx.x >> 3;  // this work-group's rank on its XCD
+        tile = j % base;
+        split = (j / base) * 8 + (blockIdx.x & 7);
+    } else {
+        tile = blockIdx.x % base;
+        split = blockIdx.x / base;
+    }
+    const int nt = tile % n_nt, mt = tile / n_nt;
     const int m0 = mt * 64, n0 = nt * 64;
     const int tiles_x = (p.Wa + WX_TW - 1) / WX_TW, tiles_y = (p.Ha + WX_TH - 1) / WX_TH;
-    const int t_begin = blockIdx.y * tiles_per_split;
+    const int t_begin = split * tiles_per_split;
     const int t_end = min(ntiles, t_begin + tiles_per_split);
     if (t_begin >= t_end) return;
     const int nloc = t_end - t_begin;
@@ -316,6 +331,12 @@ __global__ void wgrad_fold_kernel(const float* __restrict__ w, float* __restrict
     }
 }
 
+// dev knob NPS_WX_REMAP=0: the plain (tile-fastest) work-group order
+const int g_wx_remap = [] {
+    const char* e = std::getenv("NPS_WX_REMAP");
+    return (e != nullptr && e[0] == '0') ? 0 : 1;
+}();
+
 template <int KH, int KW>
 int launch_wgrad_x3(const nps_wgrad_t& p, const float* ar, const float* xr, float* ws, hipStream_t s) {
     const long tiles_x = (p.Wa + WX_TW - 1) / WX_TW, tiles_y = (p.Ha + WX_TH - 1) / WX_TH;
@@ -328,10 +349,13 @@ int launch_wgrad_x3(const nps_wgrad_t& p, const float* ar, const float* xr, floa
     long splits = 512 / base;
     const long max_splits = (ntiles + 7) / 8;
     if (splits > max_splits) splits = max_splits;
+    if (splits >= 16) splits &= ~7L;  // a multiple of 8: the XCD-aware tile order (kernel comment)
     if (splits < 1) splits = 1;
     const int per = (int)((ntiles + splits - 1) / splits);
-    splits = (ntiles + per - 1) / per;
-    NPS_CHECK_ARG(base < (1L << 31) && splits < 65536, "conv2d_wgrad_x3: grid too large");
+    const long used = (ntiles + per - 1) / per;  // splits that own tiles (the rest exit at once)
+    const int remap = (splits % 8 == 0 && g_wx_remap) ? 1 : 0;
+    if (!remap) splits = used;
+    NPS_CHECK_ARG(base * splits < (1L << 31), "conv2d_wgrad_x3: grid too large");
     const size_t lds = wx_lds_bytes(KH);
     static bool attr_set = false;
     if (!attr_set) {
@@ -344,8 +368,8 @@ int launch_wgrad_x3(const nps_wgrad_t& p, const float* ar, const float* xr, floa
         nps::set_error("conv2d_wgrad_x3: workspace memset failed");
         return -2;
     }
-    wgrad_x3_kernel<KH, KW><<<dim3((unsigned)base, (unsigned)splits), 512, lds, s>>>(p, ar, xr, ws, (int)ntiles, per,
-                                                                                    n_nt);
+    wgrad_x3_kernel<KH, KW><<<(unsigned)(base * splits), 512, lds, s>>>(p, ar, xr, ws, (int)ntiles, per, n_nt,
+                                                                         (int)base, remap);
     NPS_CHECK_LAUNCH("conv2d_wgrad_x3");
     const long total = (long)MN * KH * KW;
     const long nb = (total + 255) / 256;
