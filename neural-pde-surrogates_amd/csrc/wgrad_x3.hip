@@ -321,6 +321,156 @@ __global__ __launch_bounds__(512) void wgrad_x3_kernel(const nps_wgrad_t p, cons
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// 1x1 weight gradient with 192 x 192 work-group tiles: G[m][n] += sum_p A[p][m] X[p][n] over the flat pixel
+// range (a 1x1 conv's dy and input share their pixels).  The 64 x 64 tiles of wgrad_x3_kernel stage every
+// pixel for only 64 x 64 MACs and re-stage it once per (m, n) tile (3 x 3 tiles at M = N = 192), which left the
+// 1x1 class at 0.09 of 833 TF/s; here one work-group covers up to 192 m x 192 n, so each staged pixel feeds
+// 192 x 192 MACs and A, X are read once per m-tile / n-tile pair.
+//   * 512 threads: threads 0-255 stage A, 256-511 stage X — 32-pixel tiles, each thread 3 items of (pixel pair,
+//     channel quad): two 16-B loads, split hi + lo, four packed 2-pixel b32 writes per half into [channel][pixel]
+//     LDS rows (80-B pitch: the MFMA operand reads are conflict-free ds_read_b128), two LDS buffers;
+//   * wave w computes m [96 (w & 1), +96) x n [96 ((w >> 1) & 1), +96) (3 x 3 accumulators of 32 x 32) over
+//     pixels [16 (w >> 2), +16) of each tile: one K-step of v_mfma_f32_32x32x16_f16, 27 MFMAs (3 passes) per
+//     tile; the two pixel halves add into the same G entries;
+//   * split K over pixel tiles (XCD-aware order as wgrad_x3_kernel), fp32 atomics into W[m][n], fold into G.
+constexpr int W1_TP = 32;              // pixels per tile
+constexpr int W1_PITCH = W1_TP + 8;    // halves per LDS channel row
+constexpr int W1_ROWS = 192;           // channel rows per operand (the work-group's m or n range)
+constexpr int W1_BUF = 2 * 2 * W1_ROWS * W1_PITCH;  // halves per buffer: [A | X] x [hi | lo]
+constexpr size_t W1_LDS = (size_t)2 * W1_BUF * 2;   // two buffers, bytes
+
+__global__ __launch_bounds__(512) void wgrad1_wide_kernel(const nps_wgrad_t p, const float* a_range,
+                                                          const float* x_range, float* __restrict__ ws,
+                                                          long npix, int ntiles, int tiles_per_split, int n_nt,
+                                                          int base, int xcd_remap) {
+    extern __shared__ __attribute__((aligned(16))) _Float16 w1sm[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    int tile, split;
+    if (xcd_remap) {
+        const int j = blockIdx.x >> 3;
+        tile = j % base;
+        split = (j / base) * 8 + (blockIdx.x & 7);
+    } else {
+        tile = blockIdx.x % base;
+        split = blockIdx.x / base;
+    }
+    const int mt = tile / n_nt, nt = tile % n_nt;
+    const int m0 = mt * W1_ROWS, n0 = nt * W1_ROWS;
+    const int t_begin = split * tiles_per_split;
+    const int t_end = min(ntiles, t_begin + tiles_per_split);
+    if (t_begin >= t_end) return;
+    const float sa = pow2_scale_for(nps::tag_read(a_range));
+    const float sx = pow2_scale_for(nps::tag_read(x_range));
+
+    // ---- staging role: threads 0-255 A (channels m0..), 256-511 X (channels n0..)
+    const bool isx = tid >= 256;
+    const int st = tid & 255;
+    const float* src = isx ? p.x : p.a;
+    const int C = isx ? p.N : p.M;
+    const int c0 = isx ? n0 : m0;
+    const float scale = isx ? sx : sa;
+    int it_pp[3], it_c[3];
+    bool it_ok[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {  // item = (pixel pair pp of 16, channel quad cq of 48)
+        const int i = st + 256 * k;
+        it_pp[k] = i & 15;
+        it_c[k] = (i >> 4) * 4;  // channel offset in the 192-row block
+        it_ok[k] = c0 + it_c[k] < C;
+    }
+    auto issue = [&](int t, f32x4 (&r)[3][2]) {
+        const long pbase = (long)t * W1_TP;
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const long px = pbase + 2 * it_pp[k] + j;
+                const float* q = (it_ok[k] && px < npix) ? src + px * C + c0 + it_c[k] : wx_zero4;
+                r[k][j] = *reinterpret_cast<const f32x4*>(q);
+            }
+    };
+    auto commit = [&](int i, const f32x4 (&r)[3][2]) {
+        _Float16* H = w1sm + (i & 1) * W1_BUF + (isx ? 2 * W1_ROWS * W1_PITCH : 0);
+        _Float16* L = H + W1_ROWS * W1_PITCH;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            f16x4 h0, l0, h1, l1;
+            split4(r[k][0] * scale, h0, l0);
+            split4(r[k][1] * scale, h1, l1);
+            const int base_o = it_c[k] * W1_PITCH + 2 * it_pp[k];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                *reinterpret_cast<h2f*>(H + base_o + e * W1_PITCH) = h2f{h0[e], h1[e]};
+                *reinterpret_cast<h2f*>(L + base_o + e * W1_PITCH) = h2f{l0[e], l1[e]};
+            }
+        }
+    };
+
+    // ---- MFMA role
+    const int wm = wave & 1, wn = (wave >> 1) & 1, half = wave >> 2, h = lane >> 5;
+    f32x16 acc[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    const int koff = 16 * half + 8 * h;  // this lane's 8 pixels of the tile
+    auto compute = [&](int i) {
+        const _Float16* Ah = w1sm + (i & 1) * W1_BUF;
+        const _Float16* Al = Ah + W1_ROWS * W1_PITCH;
+        const _Float16* Xh = Al + W1_ROWS * W1_PITCH;
+        const _Float16* Xl = Xh + W1_ROWS * W1_PITCH;
+        f16x8 ah[3], al[3], bh[3], bl[3];
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+            const int ra = (wm * 96 + b * 32 + (lane & 31)) * W1_PITCH + koff;
+            const int rb = (wn * 96 + b * 32 + (lane & 31)) * W1_PITCH + koff;
+            ah[b] = *reinterpret_cast<const f16x8*>(Ah + ra);
+            al[b] = *reinterpret_cast<const f16x8*>(Al + ra);
+            bh[b] = *reinterpret_cast<const f16x8*>(Xh + rb);
+            bl[b] = *reinterpret_cast<const f16x8*>(Xl + rb);
+        }
+#pragma unroll
+        for (int bm = 0; bm < 3; ++bm)
+#pragma unroll
+            for (int bn = 0; bn < 3; ++bn) {
+                f32x16& c = acc[bm][bn];
+                c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[bm], bh[bn], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[bm], bl[bn], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[bm], bh[bn], c, 0, 0, 0);
+            }
+    };
+
+    // ---- pipeline: tile i + 1 fetched into registers while tile i is computed, then split into the other buffer
+    const int nloc = t_end - t_begin;
+    f32x4 r[3][2];
+    issue(t_begin, r);
+    commit(0, r);
+    __syncthreads();
+    for (int i = 0; i < nloc; ++i) {
+        if (i + 1 < nloc) issue(t_begin + i + 1, r);
+        compute(i);
+        if (i + 1 < nloc) commit(i + 1, r);
+        __syncthreads();
+    }
+
+    // ---- partial into W[m][n]: lane holds rows (rr/4)*8 + h*4 + rr%4 of each block, column lane%32
+    const float inv = 1.f / (sa * sx);
+#pragma unroll
+    for (int bm = 0; bm < 3; ++bm)
+#pragma unroll
+        for (int bn = 0; bn < 3; ++bn) {
+            const int n = n0 + wn * 96 + bn * 32 + (lane & 31);
+#pragma unroll
+            for (int rr = 0; rr < 16; ++rr) {
+                const int m = m0 + wm * 96 + bm * 32 + (rr >> 2) * 8 + h * 4 + (rr & 3);
+                if (m < p.M && n < p.N) atomicAdd(ws + (size_t)m * p.N + n, acc[bm][bn][rr] * inv);
+            }
+        }
+}
+
 // G[m][n][tap] += W[tap][m][n]
 __global__ void wgrad_fold_kernel(const float* __restrict__ w, float* __restrict__ g, int MN, int nt) {
     const long total = (long)MN * nt;
@@ -378,6 +528,49 @@ int launch_wgrad_x3(const nps_wgrad_t& p, const float* ar, const float* xr, floa
     return 0;
 }
 
+// 1x1 weight gradient on wgrad1_wide_kernel (dy and x on the same pixels: no padding / circular extension)
+int launch_wgrad1_wide(const nps_wgrad_t& p, const float* ar, const float* xr, float* ws, hipStream_t s) {
+    const long npix = (long)p.B * p.Ha * p.Wa;
+    const long ntiles = (npix + W1_TP - 1) / W1_TP;
+    NPS_CHECK_ARG(ntiles < (1L << 30), "conv2d_wgrad_x3 (1x1): too many tiles");
+    const int n_mt = (p.M + W1_ROWS - 1) / W1_ROWS, n_nt = (p.N + W1_ROWS - 1) / W1_ROWS;
+    const long base = (long)n_mt * n_nt;
+    long splits = 512 / base;  // two work-groups per CU in turn (LDS: 120 KiB each, one resident)
+    const long max_splits = (ntiles + 7) / 8;
+    if (splits > max_splits) splits = max_splits;
+    if (splits >= 16) splits &= ~7L;
+    if (splits < 1) splits = 1;
+    const int per = (int)((ntiles + splits - 1) / splits);
+    const long used = (ntiles + per - 1) / per;
+    const int remap = (splits % 8 == 0 && g_wx_remap) ? 1 : 0;
+    if (!remap) splits = used;
+    NPS_CHECK_ARG(base * splits < (1L << 31), "conv2d_wgrad_x3 (1x1): grid too large");
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)wgrad1_wide_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)W1_LDS);
+        attr_set = true;
+    }
+    const size_t MN = (size_t)p.M * p.N;
+    if (hipMemsetAsync(ws, 0, sizeof(float) * MN, s) != hipSuccess) {
+        nps::set_error("conv2d_wgrad_x3: workspace memset failed");
+        return -2;
+    }
+    wgrad1_wide_kernel<<<(unsigned)(base * splits), 512, W1_LDS, s>>>(p, ar, xr, ws, npix, (int)ntiles, per, n_nt,
+                                                                       (int)base, remap);
+    NPS_CHECK_LAUNCH("conv2d_wgrad_x3 (1x1 wide)");
+    const long nb = ((long)MN + 255) / 256;
+    wgrad_fold_kernel<<<(unsigned)(nb < 2048 ? nb : 2048), 256, 0, s>>>(ws, p.g, (int)MN, 1);
+    NPS_CHECK_LAUNCH("conv2d_wgrad_x3 (fold)");
+    return 0;
+}
+
+// dev knob NPS_WX_WIDE1=0: 1x1 weight gradients on the 64 x 64 tiles of wgrad_x3_kernel
+const int g_wx_wide1 = [] {
+    const char* e = std::getenv("NPS_WX_WIDE1");
+    return (e != nullptr && e[0] == '0') ? 0 : 1;
+}();
+
 }  // namespace
 
 extern "C" size_t nps_wgrad_x3_ws_floats(int M, int N, int KH, int KW) { return (size_t)M * N * KH * KW; }
@@ -395,7 +588,10 @@ extern "C" int nps_conv2d_wgrad_x3(const nps_wgrad_t* pp, const float* a_range, 
                   "conv2d_wgrad_x3: channel counts %d, %d must be multiples of 4 (16-B pixel quads)", p.M, p.N);
     hipStream_t s = (hipStream_t)stream;
     switch (p.KH) {
-        case 1: return launch_wgrad_x3<1, 1>(p, a_range, x_range, ws, s);
+        case 1:
+            if (g_wx_wide1 && p.pad_y == 0 && p.pad_x == 0 && p.circ == 0 && p.Ha == p.Hx && p.Wa == p.Wx)
+                return launch_wgrad1_wide(p, a_range, x_range, ws, s);
+            return launch_wgrad_x3<1, 1>(p, a_range, x_range, ws, s);
         case 2: return launch_wgrad_x3<2, 2>(p, a_range, x_range, ws, s);
         default: return launch_wgrad_x3<3, 3>(p, a_range, x_range, ws, s);
     }

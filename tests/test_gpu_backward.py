@@ -102,6 +102,12 @@ WGRAD_X3_CASES = [
     (3, 128, 128, 3, 0, 1, 96, 96, 1.0, 1.0),       # many pixel tiles per split
     (2, 192, 81, 1, 0, 0, 32, 32, 1.0, 1.0),        # the encoder's 81-channel 1x1: zero-padded to 84
     (2, 30, 22, 3, 1, 0, 20, 20, 1.0, 1.0),         # both channel counts off the 4-channel quads
+    # 1x1 on the 192 x 192 work-group kernel (wgrad1_wide_kernel): M, N past one 192-row tile, ragged last
+    # 32-pixel tile, many tiles per split, range cases
+    (2, 388, 196, 1, 0, 0, 37, 29, 1.0, 1.0),
+    (4, 192, 192, 1, 0, 0, 64, 64, 1.0, 1.0),
+    (1, 196, 388, 1, 0, 0, 13, 11, 1e-4, 1e3),
+    (2, 84, 192, 1, 0, 0, 40, 40, 1.5e5, 1e-3),
 ]
 
 
