@@ -617,7 +617,7 @@ __global__ __launch_bounds__(256) void gn_stats3d_kernel(const nps_conv3d_t a, i
 // channels of one voxel (16-B loads / stores for bf16).
 template <typename T>
 __global__ __launch_bounds__(256) void frame_pack3d_kernel(const nps_conv3d_t a, T* __restrict__ out, int Cpad) {
-    __shared__ float scl[512], sft[512];
+    __shared__ __attribute__((aligned(16))) float scl[512], sft[512];
     const int b = blockIdx.y;
     const bool gn = a.gn_stats != nullptr;
     for (int c = threadIdx.x; c < Cpad; c += 256) {
@@ -661,13 +661,23 @@ __global__ __launch_bounds__(256) void frame_pack3d_kernel(const nps_conv3d_t a,
         const int vox = it / npc;
         const int pc = it - vox * npc;
         if (gn || a.pre_act) {
+            // the piece's 8 affine pairs as 16-B LDS reads, GELU on packed pairs (gelu_fast2)
+            const f32x4 s0 = *reinterpret_cast<const f32x4*>(scl + pc * 8), s1 = *reinterpret_cast<const f32x4*>(scl + pc * 8 + 4);
+            const f32x4 h0 = *reinterpret_cast<const f32x4*>(sft + pc * 8), h1 = *reinterpret_cast<const f32x4*>(sft + pc * 8 + 4);
+            float y[8];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const int c = pc * 8 + e;
-                float x = fmaf(v.get(e), scl[c], sft[c]);
-                if (a.pre_act == 1) x = nps::gelu_fast(x);
-                v.set(e, c < a.Cin ? x : 0.f);
+            for (int e = 0; e < 8; ++e)
+                y[e] = fmaf(v.get(e), e < 4 ? s0[e] : s1[e - 4], e < 4 ? h0[e] : h1[e - 4]);
+            if (a.pre_act == 1) {
+#pragma unroll
+                for (int e = 0; e < 8; e += 2) {
+                    const nps::f32x2 g = nps::gelu_fast2(nps::f32x2{y[e], y[e + 1]});
+                    y[e] = g[0];
+                    y[e + 1] = g[1];
+                }
             }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v.set(e, pc * 8 + e < a.Cin ? y[e] : 0.f);
         }
         v.store(ob + (size_t)vox * Cpad + pc * 8);
     };

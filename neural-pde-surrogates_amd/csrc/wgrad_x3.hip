@@ -471,6 +471,211 @@ __global__ __launch_bounds__(512) void wgrad1_wide_kernel(const nps_wgrad_t p, c
         }
 }
 
+// ---------------------------------------------------------------------------------------------
+// 2x2 weight gradient with 128 m x 128 n work-group tiles (the space-to-depth Downsample and the transposed
+// conv's phase form: M = 192, N = 4 x 192).  wgrad_x3_kernel's 64 x 64 tiles use each staged pixel for 64 x 64
+// MACs per tap and re-stage it per (m, n) tile; here a 32-pixel tile (2 rows x 16) of A [m][px] and its 3 x 18
+// patch of X [n][row][col] feed 128 x 128 x 4 taps.  Wave w: m [64 (w & 1), +64) x n [64 ((w >> 1) & 1), +64)
+// (2 x 2 accumulators of 32 x 32) for the taps of kernel row ky = w >> 2 (both kx: the patch row is read once,
+// the kx = 1 run built in registers as in wgrad_x3_kernel); one K-step (16 pixels = one row) per MFMA.
+constexpr int W2_TH = 2, W2_TW = 16, W2_TP = W2_TH * W2_TW;
+constexpr int W2_APITCH = W2_TP + 8;              // halves per A row
+constexpr int W2_PROW = 24;                        // halves per patch row (17 used)
+constexpr int W2_PR = W2_TH + 1;                   // patch rows
+constexpr int W2_BPITCH = W2_PR * W2_PROW + 8;     // halves per patch channel
+constexpr int W2_ROWS = 128;
+constexpr int W2_BUF = 2 * W2_ROWS * W2_APITCH + 2 * W2_ROWS * W2_BPITCH;  // halves per buffer
+constexpr size_t W2_LDS = (size_t)2 * W2_BUF * 2;
+
+__global__ __launch_bounds__(512) void wgrad2_wide_kernel(const nps_wgrad_t p, const float* a_range,
+                                                          const float* x_range, float* __restrict__ ws, int ntiles,
+                                                          int tiles_per_split, int n_nt, int base, int xcd_remap) {
+    constexpr int PC = W2_TW + 1, PPR = (PC + 1) / 2;  // useful patch columns, pixel pairs per patch row (9)
+    constexpr int NPB = W2_PR * PPR;                    // patch pixel pairs (27)
+    extern __shared__ __attribute__((aligned(16))) _Float16 w2sm[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    int tile, split;
+    if (xcd_remap) {
+        const int j = blockIdx.x >> 3;
+        tile = j % base;
+        split = (j / base) * 8 + (blockIdx.x & 7);
+    } else {
+        tile = blockIdx.x % base;
+        split = blockIdx.x / base;
+    }
+    const int mt = tile / n_nt, nt = tile % n_nt;
+    const int m0 = mt * W2_ROWS, n0 = nt * W2_ROWS;
+    const int tiles_x = (p.Wa + W2_TW - 1) / W2_TW, tiles_y = (p.Ha + W2_TH - 1) / W2_TH;
+    const int t_begin = split * tiles_per_split;
+    const int t_end = min(ntiles, t_begin + tiles_per_split);
+    if (t_begin >= t_end) return;
+    const float sa = pow2_scale_for(nps::tag_read(a_range));
+    const float sx = pow2_scale_for(nps::tag_read(x_range));
+    const int Hext = p.Hx + 2 * p.circ, Wext = p.Wx + 2 * p.circ;
+
+    // staging slots: A item = (pixel pair pp of 16, channel quad of 32): one per thread; B items = (patch pair of
+    // 27, channel quad of 32): two per thread (864 of 1024 used).  Lanes 0-15 of a wave-quarter take 16
+    // consecutive pairs, so the packed 2-pixel b32 writes of one instruction hit distinct banks.
+    const int a_pp = tid & 15, a_q = tid >> 4;
+    const int a_r = (2 * a_pp) / W2_TW, a_c = (2 * a_pp) % W2_TW, a_m = m0 + 4 * a_q;
+    const bool a_ok = a_m < p.M;
+    const int a_lds = 4 * a_q * W2_APITCH + 2 * a_pp;
+    int b_r[2], b_c[2], b_n[2], b_lds[2];
+    bool b_ok[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int idx = tid + 512 * k, l = idx & 15, g = idx >> 4;  // g: group of 16 pairs
+        const int ngrp = (NPB + 15) / 16;                          // 2 pair-groups per channel quad
+        const int pp = l + 16 * (g % ngrp), nq = g / ngrp;
+        const bool in = nq < W2_ROWS / 4 && pp < NPB;
+        b_r[k] = pp / PPR;
+        b_c[k] = 2 * (pp % PPR);
+        b_n[k] = n0 + 4 * nq;
+        b_ok[k] = in && b_n[k] < p.N;
+        b_lds[k] = in ? 4 * nq * W2_BPITCH + b_r[k] * W2_PROW + b_c[k] : -1;
+    }
+    auto wrap = [&](int e, int H) {
+        int v = e - p.circ;
+        v = v < 0 ? v + H : v;
+        return v >= H ? v - H : v;
+    };
+    auto issue = [&](int t, f32x4 (&ra)[2], f32x4 (&rb)[2][2]) {
+        const int b = t / (tiles_y * tiles_x);
+        const int rr = t - b * tiles_y * tiles_x;
+        const int oy0 = (rr / tiles_x) * W2_TH, ox0 = (rr % tiles_x) * W2_TW;
+        const float* ab = p.a + (size_t)b * p.Ha * p.Wa * p.M;
+        const float* xb = p.x + (size_t)b * p.Hx * p.Wx * p.N;
+        {
+            const int oy = oy0 + a_r, ox = ox0 + a_c;
+            const bool ok = a_ok && oy < p.Ha;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const float* src = (ok && ox + j < p.Wa) ? ab + ((size_t)oy * p.Wa + ox + j) * p.M + a_m : wx_zero4;
+                ra[j] = *reinterpret_cast<const f32x4*>(src);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int ye = oy0 + b_r[k] - p.pad_y;
+            const bool rok = b_ok[k] && ye >= 0 && ye < Hext;
+            const int y = wrap(ye, p.Hx);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int xe = ox0 + b_c[k] + j - p.pad_x;
+                const bool ok = rok && b_c[k] + j < PC && xe >= 0 && xe < Wext;
+                const float* src = ok ? xb + ((size_t)y * p.Wx + wrap(xe, p.Wx)) * p.N + b_n[k] : wx_zero4;
+                rb[k][j] = *reinterpret_cast<const f32x4*>(src);
+            }
+        }
+    };
+    auto put = [&](_Float16* H, _Float16* L, int base_o, int pitch, const f32x4& v0, const f32x4& v1, float sc) {
+        f16x4 h0, l0, h1, l1;
+        split4(v0 * sc, h0, l0);
+        split4(v1 * sc, h1, l1);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            *reinterpret_cast<h2f*>(H + base_o + e * pitch) = h2f{h0[e], h1[e]};
+            *reinterpret_cast<h2f*>(L + base_o + e * pitch) = h2f{l0[e], l1[e]};
+        }
+    };
+    auto commit = [&](int i, const f32x4 (&ra)[2], const f32x4 (&rb)[2][2]) {
+        _Float16* Ah = w2sm + (i & 1) * W2_BUF;
+        _Float16* Al = Ah + W2_ROWS * W2_APITCH;
+        _Float16* Bh = Al + W2_ROWS * W2_APITCH;
+        _Float16* Bl = Bh + W2_ROWS * W2_BPITCH;
+        put(Ah, Al, a_lds, W2_APITCH, ra[0], ra[1], sa);
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+            if (b_lds[k] >= 0) put(Bh, Bl, b_lds[k], W2_BPITCH, rb[k][0], rb[k][1], sx);
+    };
+
+    // MFMA role
+    const int wm = wave & 1, wn = (wave >> 1) & 1, ky = wave >> 2, h = lane >> 5;
+    f32x16 acc[2][2][2];  // [kx][m block][n block]
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[x][i][j][r] = 0.f;
+    auto compute = [&](int i) {
+        const _Float16* Ah = w2sm + (i & 1) * W2_BUF;
+        const _Float16* Al = Ah + W2_ROWS * W2_APITCH;
+        const _Float16* Bh = Al + W2_ROWS * W2_APITCH;
+        const _Float16* Bl = Bh + W2_ROWS * W2_BPITCH;
+#pragma unroll
+        for (int r = 0; r < W2_TH; ++r) {
+            f16x8 ah[2], al[2];
+#pragma unroll
+            for (int bm = 0; bm < 2; ++bm) {
+                const int ra = (wm * 64 + bm * 32 + (lane & 31)) * W2_APITCH + r * W2_TW + 8 * h;
+                ah[bm] = *reinterpret_cast<const f16x8*>(Ah + ra);
+                al[bm] = *reinterpret_cast<const f16x8*>(Al + ra);
+            }
+#pragma unroll
+            for (int bn = 0; bn < 2; ++bn) {
+                const int rb = (wn * 64 + bn * 32 + (lane & 31)) * W2_BPITCH + (r + ky) * W2_PROW + 8 * h;
+                unsigned dh[6], dl[6];
+                const u32x4 h4 = *reinterpret_cast<const u32x4*>(Bh + rb);
+                const u32x4 l4 = *reinterpret_cast<const u32x4*>(Bl + rb);
+                const u32x2 h2 = *reinterpret_cast<const u32x2*>(Bh + rb + 8);
+                const u32x2 l2 = *reinterpret_cast<const u32x2*>(Bl + rb + 8);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    dh[e] = h4[e];
+                    dl[e] = l4[e];
+                }
+                dh[4] = h2[0];
+                dh[5] = h2[1];
+                dl[4] = l2[0];
+                dl[5] = l2[1];
+                static_for<2>([&](auto kxc) {
+                    constexpr int kx = decltype(kxc)::value;
+                    const f16x8 bh = shifted_run<kx>(dh), bl = shifted_run<kx>(dl);
+#pragma unroll
+                    for (int bm = 0; bm < 2; ++bm) {
+                        f32x16& c = acc[kx][bm][bn];
+                        c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[bm], bh, c, 0, 0, 0);
+                        c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[bm], bl, c, 0, 0, 0);
+                        c = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[bm], bh, c, 0, 0, 0);
+                    }
+                });
+            }
+        }
+    };
+
+    const int nloc = t_end - t_begin;
+    f32x4 ra[2], rb[2][2];
+    issue(t_begin, ra, rb);
+    commit(0, ra, rb);
+    __syncthreads();
+    for (int i = 0; i < nloc; ++i) {
+        if (i + 1 < nloc) issue(t_begin + i + 1, ra, rb);
+        compute(i);
+        if (i + 1 < nloc) commit(i + 1, ra, rb);
+        __syncthreads();
+    }
+
+    const float inv = 1.f / (sa * sx);
+#pragma unroll
+    for (int kx = 0; kx < 2; ++kx) {
+        float* wt = ws + (size_t)(ky * 2 + kx) * p.M * p.N;
+#pragma unroll
+        for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+            for (int bn = 0; bn < 2; ++bn) {
+                const int n = n0 + wn * 64 + bn * 32 + (lane & 31);
+#pragma unroll
+                for (int rr = 0; rr < 16; ++rr) {
+                    const int m = m0 + wm * 64 + bm * 32 + (rr >> 2) * 8 + h * 4 + (rr & 3);
+                    if (m < p.M && n < p.N) atomicAdd(wt + (size_t)m * p.N + n, acc[kx][bm][bn][rr] * inv);
+                }
+            }
+    }
+}
+
 // G[m][n][tap] += W[tap][m][n]
 __global__ void wgrad_fold_kernel(const float* __restrict__ w, float* __restrict__ g, int MN, int nt) {
     const long total = (long)MN * nt;
@@ -565,9 +770,51 @@ int launch_wgrad1_wide(const nps_wgrad_t& p, const float* ar, const float* xr, f
     return 0;
 }
 
+// 2x2 weight gradient on wgrad2_wide_kernel (128 x 128 work-group tiles)
+int launch_wgrad2_wide(const nps_wgrad_t& p, const float* ar, const float* xr, float* ws, hipStream_t s) {
+    const long tiles_x = (p.Wa + W2_TW - 1) / W2_TW, tiles_y = (p.Ha + W2_TH - 1) / W2_TH;
+    const long ntiles = (long)p.B * tiles_y * tiles_x;
+    NPS_CHECK_ARG(ntiles < (1L << 30), "conv2d_wgrad_x3 (2x2): too many tiles");
+    const int n_mt = (p.M + W2_ROWS - 1) / W2_ROWS, n_nt = (p.N + W2_ROWS - 1) / W2_ROWS;
+    const long base = (long)n_mt * n_nt;
+    long splits = 512 / base;
+    const long max_splits = (ntiles + 7) / 8;
+    if (splits > max_splits) splits = max_splits;
+    if (splits >= 16) splits &= ~7L;
+    if (splits < 1) splits = 1;
+    const int per = (int)((ntiles + splits - 1) / splits);
+    const long used = (ntiles + per - 1) / per;
+    const int remap = (splits % 8 == 0 && g_wx_remap) ? 1 : 0;
+    if (!remap) splits = used;
+    NPS_CHECK_ARG(base * splits < (1L << 31), "conv2d_wgrad_x3 (2x2): grid too large");
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)wgrad2_wide_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)W2_LDS);
+        attr_set = true;
+    }
+    const size_t MN = (size_t)p.M * p.N;
+    if (hipMemsetAsync(ws, 0, sizeof(float) * MN * 4, s) != hipSuccess) {
+        nps::set_error("conv2d_wgrad_x3: workspace memset failed");
+        return -2;
+    }
+    wgrad2_wide_kernel<<<(unsigned)(base * splits), 512, W2_LDS, s>>>(p, ar, xr, ws, (int)ntiles, per, n_nt, (int)base,
+                                                                       remap);
+    NPS_CHECK_LAUNCH("conv2d_wgrad_x3 (2x2 wide)");
+    const long nb = ((long)MN * 4 + 255) / 256;
+    wgrad_fold_kernel<<<(unsigned)(nb < 2048 ? nb : 2048), 256, 0, s>>>(ws, p.g, (int)MN, 4);
+    NPS_CHECK_LAUNCH("conv2d_wgrad_x3 (fold)");
+    return 0;
+}
+
 // dev knob NPS_WX_WIDE1=0: 1x1 weight gradients on the 64 x 64 tiles of wgrad_x3_kernel
 const int g_wx_wide1 = [] {
     const char* e = std::getenv("NPS_WX_WIDE1");
+    return (e != nullptr && e[0] == '0') ? 0 : 1;
+}();
+// dev knob NPS_WX_WIDE2=0: 2x2 weight gradients on the 64 x 64 tiles of wgrad_x3_kernel
+const int g_wx_wide2 = [] {
+    const char* e = std::getenv("NPS_WX_WIDE2");
     return (e != nullptr && e[0] == '0') ? 0 : 1;
 }();
 
@@ -592,7 +839,10 @@ extern "C" int nps_conv2d_wgrad_x3(const nps_wgrad_t* pp, const float* a_range, 
             if (g_wx_wide1 && p.pad_y == 0 && p.pad_x == 0 && p.circ == 0 && p.Ha == p.Hx && p.Wa == p.Wx)
                 return launch_wgrad1_wide(p, a_range, x_range, ws, s);
             return launch_wgrad_x3<1, 1>(p, a_range, x_range, ws, s);
-        case 2: return launch_wgrad_x3<2, 2>(p, a_range, x_range, ws, s);
+        case 2:
+            // (the wide kernel needs M, N > 64 to beat the 64 x 64 tiles)
+            if (g_wx_wide2 && p.M > 64 && p.N > 64) return launch_wgrad2_wide(p, a_range, x_range, ws, s);
+            return launch_wgrad_x3<2, 2>(p, a_range, x_range, ws, s);
         default: return launch_wgrad_x3<3, 3>(p, a_range, x_range, ws, s);
     }
 }

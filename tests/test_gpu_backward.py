@@ -108,6 +108,11 @@ WGRAD_X3_CASES = [
     (4, 192, 192, 1, 0, 0, 64, 64, 1.0, 1.0),
     (1, 196, 388, 1, 0, 0, 13, 11, 1e-4, 1e3),
     (2, 84, 192, 1, 0, 0, 40, 40, 1.5e5, 1e-3),
+    # 2x2 on the 128 x 128 work-group kernel (wgrad2_wide_kernel): the space-to-depth Downsample / transposed-conv
+    # phase shape (M = 192, N = 4 x 192), padding, circular extension, tails past one 128-row tile, range
+    (2, 192, 768, 2, 0, 0, 33, 31, 1.0, 1.0),
+    (1, 100, 136, 2, 1, 0, 19, 21, 1e-4, 1e3),
+    (2, 132, 80, 2, 0, 1, 20, 24, 1.0, 1.0),
 ]
 
 
