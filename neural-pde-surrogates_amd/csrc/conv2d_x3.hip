@@ -400,8 +400,19 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
                     }
                     split4(v * xs, hi, lo);
                     char* base = Pt + x3_slot_px(idx) * X3_PIXB + (idx & 3) * 8;
+#if NPS_X3_ABL == 7  // dev ablation: the commit's arithmetic without its LDS writes (values kept live)
+                    {
+                        typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+                        const u32x2_t hb = __builtin_bit_cast(u32x2_t, hi), lb = __builtin_bit_cast(u32x2_t, lo);
+                        asm volatile("" ::"v"(hb[0] ^ lb[0]), "v"(hb[1] ^ lb[1]));
+                    }
+#elif NPS_X3_ABL == 8  // dev ablation: the LDS writes of constant data (no fetch wait, no arithmetic)
+                    *reinterpret_cast<f16x4*>(base) = f16x4{0, 0, 0, 0};
+                    *reinterpret_cast<f16x4*>(base + 32) = f16x4{0, 0, 0, 0};
+#else
                     *reinterpret_cast<f16x4*>(base) = hi;
                     *reinterpret_cast<f16x4*>(base + 32) = lo;
+#endif
                 }
             }
         };
@@ -465,6 +476,14 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
             barrier();
             for (int st = 0; st < nstages; ++st) {
 #if NPS_X3_ABL == 4  // dev ablation: the producers only keep the barriers (stale patch)
+                barrier();
+                continue;
+#elif NPS_X3_ABL == 5  // dev ablation: fetch only (no GroupNorm/GELU/split/LDS commit)
+                m = issue(min(st + 3, last), r0);
+                barrier();
+                continue;
+#elif NPS_X3_ABL == 6 || NPS_X3_ABL == 7 || NPS_X3_ABL == 8  // dev ablations: commit only (stale registers, no
+                if (st + 2 < nstages) commit(st + 2, r0, m);                      // fetch); 7, 8: see commit
                 barrier();
                 continue;
 #endif

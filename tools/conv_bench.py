@@ -29,12 +29,20 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--check", action="store_true")
     ap.add_argument("--prec", default="x3f16", choices=["x3f16", "f32"])
+    ap.add_argument("--data", default="randn", choices=["randn", "zero", "const", "wzero"],
+                    help="input / weight content (data-dependence of the kernel's clock: zero / constant operands)")
     a = ap.parse_args()
     ops.CONV_PRECISION = ops.PREC_F32 if a.prec == "f32" else ops.PREC_X3F16
     dev = "cuda"
     torch.manual_seed(0)
     x = torch.randn(a.b, a.hw, a.hw, a.cin, device=dev)
     w = torch.randn(a.cout, a.cin, a.k, a.k, device=dev) * (1.0 / (a.cin * a.k * a.k) ** 0.5)
+    if a.data == "zero":
+        x.zero_()
+    elif a.data == "const":
+        x.fill_(0.75)
+    elif a.data == "wzero":
+        w.zero_()
     bias = torch.randn(a.cout, device=dev)
     wp = ops.pack_conv_weight(w, a.stride, a.dil)
     gn = None
