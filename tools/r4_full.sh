@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 GPU pass (gpurun): parity suite, C3 bench + rocprof, B=2 line, training lines (B=2, B=16) + rocprof of
 # the B=16 step, C5 (ufno3d bf16) line + rocprof, N=2 training rehearsal.  Outputs: gpurun_out/${TAG}_*.
-# usage: tools/r4_full.sh TAG [steps...]   steps: tests sel($TESTSEL) bench prof b2 b2prof train trainprof c5 c5prof reh (default: all)
+# usage: tools/r4_full.sh TAG [steps...]   steps: tests sel($TESTSEL) pmc bench prof b2 b2prof train trainprof c5 c5prof reh (default: all)
 set -o pipefail
 TAG=${1:-r4full}; shift
 STEPS="${@:-tests bench prof b2 train trainprof c5 c5prof reh}"
@@ -14,6 +14,7 @@ for s in $STEPS; do
              || { echo "tests failed"; tail -30 ${O}_tests.log; exit 1; }; tail -2 ${O}_tests.log ;;
     sel)   timeout -k 10 400 python -u -m pytest $TESTSEL -m gpu -q -x --timeout 200 --timeout-method thread > ${O}_sel.log 2>&1 \
              || { echo "selected tests failed"; tail -30 ${O}_sel.log; exit 1; }; tail -2 ${O}_sel.log ;;
+    pmc)   timeout -k 10 900 bash tools/pmc_traffic.sh > ${O}_pmc.log 2>&1 || { echo "pmc failed"; tail -20 ${O}_pmc.log; exit 1; }; cp gpurun_out/pmc_traffic.json ${O}_pmc_traffic.json && cp gpurun_out/pmc_traffic.json profiles/pmc_traffic.json ;;
     bench) timeout -k 10 400 python -u bench.py > ${O}_bench.json 2> ${O}_bench.err || { echo "bench failed"; tail -20 ${O}_bench.err; exit 1; }; tail -c 600 ${O}_bench.json ;;
     prof)  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d ${O}_prof -o run -- python3 bench.py --steps 3 --warmup 1 --cpu-calls 0 \
              > ${O}_prof.log 2>&1 || { echo "prof failed"; tail -20 ${O}_prof.log; exit 1; } ;;
