@@ -424,6 +424,10 @@ typedef struct {
     const void* addend;         /* indexed like out, or NULL (proc_ufno.py:118 h_fno + h_unet) */
     int act;                    /* 0 none, 1 GELU, after bias + addend */
     int bf16;                   /* 1: bf16 storage / bf16 MFMA; 0: fp32 storage / exact fp32 MFMA */
+    /* [B][NPS_STATS_SUB][2] fp64 or NULL: the launch ADDS the (sum, sum of squares) of the values it stores
+     * (as stored: bf16-rounded for bf16 storage) — the GroupNorm(1) moments of its output, carried to the next
+     * frame instead of an nps_gn_stats3d pass.  Plain epilogue only (no accumulate / addend / act / phases). */
+    double* out_stats;
 } nps_conv3d_t;
 
 /* Conv3d weight (Cout, Cin, K, K, K) or, transposed != 0, ConvTranspose3d weight (Cin, Cout, 4, 4, 4) ->

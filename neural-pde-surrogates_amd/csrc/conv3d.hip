@@ -352,7 +352,15 @@ __global__ __launch_bounds__(256) void conv3d_kernel(const nps_conv3d_t a, int n
     const int pd = a.transposed ? (z >> 2) : 0, ph = a.transposed ? ((z >> 1) & 1) : 0,
               pw = a.transposed ? (z & 1) : 0;
     const int od = md * a.out_os + a.out_off_d + pd;
-    if (od < 0 || od >= a.out_D) return;
+    // out_stats: moments of the stored values (fp32 per 4-channel quad, fp64 across), published per wave at the
+    // end — so no early return: every lane reaches the wave-collective publish
+    const bool st = a.out_stats != nullptr;
+    float f1 = 0.f, f2 = 0.f;  // this lane's (at most 2 x RW x 16) stored values: fp32, then fp64 per wave
+    auto mom = [&](float x0, float x1, float x2, float x3) {
+        f1 += (x0 + x1) + (x2 + x3);
+        f2 += (x0 * x0 + x1 * x1) + (x2 * x2 + x3 * x3);
+    };
+    if (od >= 0 && od < a.out_D) {
     T* out = reinterpret_cast<T*>(a.out);
     const T* add = reinterpret_cast<const T*>(a.addend);
     const int w = w0 + col;
@@ -386,6 +394,7 @@ __global__ __launch_bounds__(256) void conv3d_kernel(const nps_conv3d_t a, int n
                         for (int e = 0; e < 4; ++e) o[e] = nps::gelu_erf(o[e]);
                     if (a.accumulate) o += *reinterpret_cast<const f32x4*>(op);
                     *reinterpret_cast<f32x4*>(op) = o;
+                    if (st) mom(o[0], o[1], o[2], o[3]);
                 } else if (vec4) {  // bf16: 4 channels = one 8-B access
                     float o[4] = {v[0], v[1], v[2], v[3]};
                     if (ap) {
@@ -403,6 +412,7 @@ __global__ __launch_bounds__(256) void conv3d_kernel(const nps_conv3d_t a, int n
                     }
                     const u32x2 r = {f2bf(o[0]) | (f2bf(o[1]) << 16), f2bf(o[2]) | (f2bf(o[3]) << 16)};
                     *reinterpret_cast<u32x2*>(op) = r;
+                    if (st) mom(bf2f(r[0] & 0xffffu), bf2f(r[0] >> 16), bf2f(r[1] & 0xffffu), bf2f(r[1] >> 16));
                 } else {
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
@@ -412,9 +422,24 @@ __global__ __launch_bounds__(256) void conv3d_kernel(const nps_conv3d_t a, int n
                         if (a.act == 1) o = nps::gelu_erf(o);
                         if (a.accumulate) o += ld1<T>(op + e);
                         st1<T>(op + e, o);
+                        if (st) {
+                            const float q = ld1<T>(op + e);  // (as stored)
+                            f1 += q;
+                            f2 += q * q;
+                        }
                     }
                 }
             }
+        }
+    }
+    }
+    if (st) {
+        const double s1 = nps::wave_sum((double)f1);
+        const double s2 = nps::wave_sum((double)f2);
+        if ((threadIdx.x & 63) == 0) {
+            double* q = a.out_stats + ((size_t)b * NPS_STATS_SUB + nps::wave_salt() % NPS_STATS_SUB) * 2;
+            atomicAdd(q, s1);
+            atomicAdd(q + 1, s2);
         }
     }
 }
@@ -794,6 +819,8 @@ extern "C" int nps_conv3d_fwd(const nps_conv3d_t* ap, void* stream) {
                                             a.Cin % a.gn_groups == 0),
                   "conv3d: bad GroupNorm prologue");
     NPS_CHECK_ARG(a.pre_act == 0 || a.pre_act == 1, "conv3d: pre_act 0 or 1");
+    NPS_CHECK_ARG(a.out_stats == nullptr || (!a.accumulate && a.addend == nullptr && a.act == 0 && !a.transposed),
+                  "conv3d: out_stats needs a plain epilogue (no accumulate / addend / act / phases)");
     const int nchunk = (a.Cin + 15) / 16, ntile = (a.Cout + 63) / 64;
     hipStream_t s = (hipStream_t)stream;
     return a.bf16 ? dispatch<bf16_t>(a, nchunk, ntile, s) : dispatch<float>(a, nchunk, ntile, s);

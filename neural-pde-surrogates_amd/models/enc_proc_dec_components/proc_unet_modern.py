@@ -302,7 +302,12 @@ class ResidualBlock(nn.Module):
         gn1 = gn2 = None
         if isinstance(self.norm1, nn.GroupNorm):
             gn1 = _gn_args(self.norm1, ops.gn_stats3d(srcs, frame_dhw, self.norm1.num_groups))
-        h1 = self.conv1.run3d(srcs, frame_dhw, gn=gn1, pre_act=act)
+        # conv1 adds the moments of what it stores (nps_conv3d_t.out_stats): norm2's GroupNorm(1) statistics
+        # without a pass over h1
+        B = srcs[0].t.shape[0]
+        carry = isinstance(self.norm2, nn.GroupNorm) and self.norm2.num_groups == 1
+        st1 = ops.new_stats(B, srcs[0].t) if carry else None
+        h1 = self.conv1.run3d(srcs, frame_dhw, gn=gn1, pre_act=act, out_stats=st1)
         if isinstance(self.shortcut, nn.Identity):
             s0 = srcs[0]
             if len(srcs) != 1 or s0.off_d or s0.off_h or s0.off_w or tuple(s0.t.shape[1:4]) != tuple(frame_dhw):
@@ -312,7 +317,9 @@ class ResidualBlock(nn.Module):
             out = self.shortcut.run3d(srcs, frame_dhw)
         d1 = tuple(h1.shape[1:4])
         if isinstance(self.norm2, nn.GroupNorm):
-            gn2 = _gn_args(self.norm2, ops.gn_stats3d([ops.Src3(h1)], d1, self.norm2.num_groups))
+            st2 = (ops._stats_sum([st1], B, ops.new_stats(B, h1, 1)) if carry
+                   else ops.gn_stats3d([ops.Src3(h1)], d1, self.norm2.num_groups))
+            gn2 = _gn_args(self.norm2, st2)
         K, s, circ, zpad = self.conv2.geometry3d()
         d2 = tuple((n + 2 * (circ + zpad) - K) // s + 1 for n in d1)
         self.conv2.run3d([ops.Src3(h1)], d1, gn=gn2, pre_act=act, out=out,

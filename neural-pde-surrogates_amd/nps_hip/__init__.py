@@ -79,7 +79,7 @@ class Conv3dArgs(ctypes.Structure):
         ("out", ctypes.c_void_p), ("out_C", ctypes.c_int), ("out_D", ctypes.c_int), ("out_H", ctypes.c_int),
         ("out_W", ctypes.c_int), ("out_os", ctypes.c_int), ("out_off_d", ctypes.c_int), ("out_off_h", ctypes.c_int),
         ("out_off_w", ctypes.c_int), ("accumulate", ctypes.c_int), ("addend", ctypes.c_void_p), ("act", ctypes.c_int),
-        ("bf16", ctypes.c_int),
+        ("bf16", ctypes.c_int), ("out_stats", ctypes.c_void_p),
     ]
 
 

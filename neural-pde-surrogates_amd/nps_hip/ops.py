@@ -787,7 +787,7 @@ def frame_pack3d(srcs: Sequence[Src3], frame_dhw, gn: Optional[GN] = None, pre_a
 def conv3d(srcs: Sequence[Src3], frame_dhw, wpack: torch.Tensor, bias: Optional[torch.Tensor], Cout: int, K: int,
            stride=1, transposed=False, circ=0, zpad=0, gn: Optional[GN] = None, pre_act=0,
            out: Optional[torch.Tensor] = None, out_os=1, out_off=(0, 0, 0), accumulate=False,
-           addend: Optional[torch.Tensor] = None, act=0) -> torch.Tensor:
+           addend: Optional[torch.Tensor] = None, act=0, out_stats: Optional[torch.Tensor] = None) -> torch.Tensor:
     """One nps_conv3d launch over a virtual NDHWC frame (sources at crop offsets), extended per side by
     `circ` circular then `zpad` zero voxels; valid K^3 conv (stride), or with `transposed` the 8 phase convs
     (K = 2) of a k4/s2 transposed conv written with out_os = 2.  Without `out` a tensor of the conv's
@@ -821,6 +821,7 @@ def conv3d(srcs: Sequence[Src3], frame_dhw, wpack: torch.Tensor, bias: Optional[
     a.pre_act = pre_act
     a.K, a.stride, a.transposed = K, stride, 1 if transposed else 0
     a.Dout, a.Hout, a.Wout = Dout, Hout, Wout
+    a.out_stats = ptr(out_stats)  # (new_stats(B, ..) buffer: the stored values' GroupNorm(1) moments)
     a.wpack, a.bias, a.Cout = ptr(wpack), ptr(bias), Cout
     a.out, a.out_C, a.out_D, a.out_H, a.out_W = ptr(out), out.shape[4], out.shape[1], out.shape[2], out.shape[3]
     a.out_os, (a.out_off_d, a.out_off_h, a.out_off_w) = out_os, out_off

@@ -186,3 +186,27 @@ def test_gn_stats3d_and_frame_pack3d_channels_mod4(dt, groups):
     want = F.gelu(F.group_norm(fr, groups, gamma.double(), beta.double(), eps=1e-5))
     got = packed[..., :68].float().cpu().permute(0, 4, 1, 2, 3).double()
     assert rel_l2(got, _rt(want, dt) if dt == torch.bfloat16 else want) < (1e-2 if dt == torch.bfloat16 else 1e-6)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+def test_conv3d_out_stats_carry_moments(dt):
+    """nps_conv3d_t.out_stats: a plain-epilogue conv adds the GroupNorm(1) moments of the values it stores (as
+    stored: bf16-rounded for bf16) — the ResidualBlock's norm2 statistics of h1 without a gn_stats3d pass;
+    equal to gn_stats3d over the output, and to the fp64 sums of it."""
+    from nps_hip import ops
+    torch.manual_seed(9)
+    B, dhw = 2, (6, 10, 21)
+    x = torch.randn(B, 36, *dhw)
+    w, b = torch.randn(24, 36, 3, 3, 3) * 0.05, torch.randn(24) * 0.1
+    gamma, beta = 1 + 0.2 * torch.randn(36), 0.1 * torch.randn(36)
+    src = [ops.Src3(_ndhwc(x, dt))]
+    gn = ops.GN(ops.gn_stats3d(src, dhw, 1), gamma.to(DEV), beta.to(DEV), 1, 1e-5)
+    st = ops.new_stats(B, src[0].t)
+    y = ops.conv3d(src, dhw, ops.pack_conv3d_weight(w.to(DEV), bf16=dt == torch.bfloat16), b.to(DEV), 24, 3, gn=gn,
+                   pre_act=1, out_stats=st)
+    got = ops._stats_sum([st], B, ops.new_stats(B, y, 1)).cpu()[:, 0]
+    ref = ops.gn_stats3d([ops.Src3(y)], y.shape[1:4], 1).cpu()[:, 0]
+    yd = y.float().cpu().double().reshape(B, -1)
+    torch.testing.assert_close(got, ref, rtol=1e-6, atol=1e-3)
+    torch.testing.assert_close(got[:, 0], yd.sum(1), rtol=1e-6, atol=1e-3)
+    torch.testing.assert_close(got[:, 1], (yd ** 2).sum(1), rtol=1e-6, atol=1e-3)
