@@ -148,7 +148,10 @@ size_t nps_conv2d_packed_size(int Cout, int Cin, int ntaps);
  * stride-2 4x4 transposed-conv weight w[Cin][Cout][4][4]
  * (nn.ConvTranspose2d layout) as the 2x2 conv of output phase
  * (py, px) = (phase>>1, phase&1); KH = KW = 2 then.  transposed_phase == -2 packs a 3x3 stride-2
- * weight w[Cout][Cin/4][3][3] for the space-to-depth 2x2 form (KH = KW = 2, Cin = 4C). */
+ * weight w[Cout][Cin/4][3][3] for the space-to-depth 2x2 form (KH = KW = 2, Cin = 4C).
+ * transposed_phase == -3 packs the input-gradient conv of a stride-1 conv whose weight is
+ * w[Cin][Cout][KH][KW] (Cout / Cin: the packed conv's): w transposed and flipped, element (co, ci, ky, kx) =
+ * w[ci][co][KH-1-ky][KW-1-kx]. */
 int nps_conv2d_pack_weights(const float* w, float* wpack, int Cout, int Cin, int KH, int KW,
                             int transposed_phase, void* stream);
 /* Same transforms, packed as [hi | lo] fp16 MFMA fragments of s*w for precision = NPS_PREC_X3F16, with s

@@ -459,6 +459,8 @@ __device__ __forceinline__ float weight_elem(const float* __restrict__ w, int Co
         const int kyy = 2 * ky + (par >> 1), kxx = 2 * kx + (par & 1);
         return (kyy < 3 && kxx < 3) ? w[(((size_t)co * C + c) * 3 + kyy) * 3 + kxx] : 0.f;
     }
+    if (tphase == -3)  // input-gradient conv of w[Cin][Cout][KH][KW] (the forward conv's): transposed, flipped
+        return w[(((size_t)ci * Cout + co) * KH + (KH - 1 - ky)) * KW + (KW - 1 - kx)];
     if (tphase < 0) return w[(((size_t)co * Cin + ci) * KH + ky) * KW + kx];
     // 4x4 / stride-2 transposed conv, output phase (py, px): tap (ty, tx) uses
     // kernel element (py + 2(1-ty), px + 2(1-tx)) of w[Cin][Cout][4][4]
@@ -488,9 +490,11 @@ __global__ void pack_weights_kernel(const float* __restrict__ w, float* __restri
 
 // Packed layout (3-pass split fp16, same bytes): [chunk][tap][cb][hl (2)][lane (64)][8 halves]
 // element j of lane = (hi | lo) of s * w[co = cb*32 + (lane&31)][ci = chunk*16 + (lane>>5)*8 + j][tap],
-// s = pow2_scale_for(max|w|) (max|w| is in the buffer's trailer, written by nps_absmax_scalar beforehand)
+// s = pow2_scale_for(max|w|): max|w| from the per-work-group partials nps_absmax_parts left in trailer[1 ..],
+// written back to trailer[0] (where the conv kernels read it)
 __global__ void pack_weights_x3_kernel(const float* __restrict__ w, _Float16* __restrict__ wp, int Cout, int Cin,
-                                       int KH, int KW, int tphase, size_t total_pairs, const float* __restrict__ wmax) {
+                                       int KH, int KW, int tphase, size_t total_pairs, float* __restrict__ wmax,
+                                       int nparts) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // (hi, lo) pair index
     if (i >= total_pairs) return;
     const int ntaps = KH * KW;
@@ -504,9 +508,12 @@ __global__ void pack_weights_x3_kernel(const float* __restrict__ w, _Float16* __
     // 1x1: chunk pair (2s, 2s + 1) covers channels [32s, 32s + 32) with lane half h holding the contiguous
     // run [32s + 16h, 32s + 16h + 16): chunk 2s its first 8, chunk 2s + 1 its last 8 (conv1x1_x3_kernel
     // fetches 64 contiguous bytes per lane); other tap counts: chunk c = channels [16c, 16c + 16)
-    const int ci = ntaps == 1 && tphase == -1 ? (chunk >> 1) * 32 + (lane >> 5) * 16 + (chunk & 1) * 8 + j
+    const int ci = ntaps == 1 && (tphase == -1 || tphase == -3) ? (chunk >> 1) * 32 + (lane >> 5) * 16 + (chunk & 1) * 8 + j
                                               : chunk * CK + (lane >> 5) * 8 + j;
-    const float v = pow2_scale_for(*wmax) * weight_elem(w, Cout, Cin, KH, KW, tphase, cb * 32 + (lane & 31), ci, tap);
+    float m = 0.f;  // max|w| from the absmax partials in trailer[1 .. nparts]; thread 0 publishes it as trailer[0]
+    for (int k = 0; k < nparts; ++k) m = fmaxf(m, wmax[1 + k]);
+    if (i == 0) wmax[0] = m;
+    const float v = pow2_scale_for(m) * weight_elem(w, Cout, Cin, KH, KW, tphase, cb * 32 + (lane & 31), ci, tap);
     const size_t frag = i >> 9;  // (chunk, tap, cb) fragment of 64 lanes x 8
     const size_t o = frag * 1024 + (size_t)lane * 8 + j;
     const h2f hv = pkrtz(v, 0.f);
@@ -566,8 +573,9 @@ extern "C" size_t nps_conv2d_packed_size(int Cout, int Cin, int ntaps) { return 
 extern "C" int nps_conv2d_pack_weights(const float* w, float* wpack, int Cout, int Cin, int KH, int KW,
                                        int transposed_phase, void* stream) {
     NPS_CHECK_ARG(w && wpack && Cout > 0 && Cin > 0 && KH > 0 && KW > 0, "conv2d_pack_weights: bad args");
-    NPS_CHECK_ARG(transposed_phase == -1 || ((transposed_phase == -2 || (transposed_phase >= 0 && transposed_phase < 4)) &&
-                                             KH == 2 && KW == 2 && (transposed_phase != -2 || Cin % 4 == 0)),
+    NPS_CHECK_ARG(transposed_phase == -1 || transposed_phase == -3 ||
+                      ((transposed_phase == -2 || (transposed_phase >= 0 && transposed_phase < 4)) && KH == 2 &&
+                       KW == 2 && (transposed_phase != -2 || Cin % 4 == 0)),
                   "conv2d_pack_weights: phase / space-to-depth packing needs KH=KW=2");
     const size_t total = packed_body(Cout, Cin, KH * KW);
     const int bs = 256;
@@ -580,17 +588,19 @@ extern "C" int nps_conv2d_pack_weights(const float* w, float* wpack, int Cout, i
 extern "C" int nps_conv2d_pack_weights_x3(const float* w, float* wpack, int Cout, int Cin, int KH, int KW,
                                           int transposed_phase, void* stream) {
     NPS_CHECK_ARG(w && wpack && Cout > 0 && Cin > 0 && KH > 0 && KW > 0, "conv2d_pack_weights_x3: bad args");
-    NPS_CHECK_ARG(transposed_phase == -1 || ((transposed_phase == -2 || (transposed_phase >= 0 && transposed_phase < 4)) &&
-                                             KH == 2 && KW == 2 && (transposed_phase != -2 || Cin % 4 == 0)),
+    NPS_CHECK_ARG(transposed_phase == -1 || transposed_phase == -3 ||
+                      ((transposed_phase == -2 || (transposed_phase >= 0 && transposed_phase < 4)) && KH == 2 &&
+                       KW == 2 && (transposed_phase != -2 || Cin % 4 == 0)),
                   "conv2d_pack_weights_x3: phase / space-to-depth packing needs KH=KW=2");
     const size_t pairs = packed_body(Cout, Cin, KH * KW);  // one (hi, lo) pair per fp32 slot
     float* wmax = wpack + pairs;                             // trailer[0]
-    const long nw = transposed_phase == -1 ? (long)Cout * Cin * KH * KW
+    const long nw = transposed_phase == -1 || transposed_phase == -3 ? (long)Cout * Cin * KH * KW
                                            : (transposed_phase == -2 ? (long)Cout * (Cin / 4) * 9 : (long)Cout * Cin * 16);
-    if (nps_absmax_scalar(w, nw, wmax, (hipStream_t)stream) != 0) return -2;
+    const int nparts = nps_absmax_parts(w, nw, wmax + 1, PACK_TRAILER - 1, (hipStream_t)stream);
+    if (nparts <= 0) return -2;
     const int bs = 256;
     pack_weights_x3_kernel<<<(unsigned)((pairs + bs - 1) / bs), bs, 0, (hipStream_t)stream>>>(
-        w, reinterpret_cast<_Float16*>(wpack), Cout, Cin, KH, KW, transposed_phase, pairs, wmax);
+        w, reinterpret_cast<_Float16*>(wpack), Cout, Cin, KH, KW, transposed_phase, pairs, wmax, nparts);
     NPS_CHECK_LAUNCH("conv2d_pack_weights_x3");
     return 0;
 }
@@ -1139,25 +1149,26 @@ __global__ void absmax_kernel(const float* __restrict__ x, long n, float* __rest
 
 // plain scalar max|x| into *out (one float; the packed-weight trailer): single-address atomics, used once
 // per parameter version
-__global__ void absmax_scalar_kernel(const float* __restrict__ x, long n, unsigned int* __restrict__ out) {
+// one partial max|x| per work-group (no atomics, no zero-fill): parts[blockIdx.x]
+__global__ __launch_bounds__(256) void absmax_parts_kernel(const float* __restrict__ x, long n,
+                                                           float* __restrict__ parts) {
+    __shared__ float wm[4];
     float m = 0.f;
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
         m = fmaxf(m, fabsf(x[i]));
     m = nps::wave_max(m);
-    if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
+    if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) parts[blockIdx.x] = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
 }
 }  // namespace
 
-int nps_absmax_scalar(const float* x, long n, float* out, hipStream_t s) {
-    if (hipMemsetAsync(out, 0, sizeof(float), s) != hipSuccess) {
-        nps::set_error("absmax: memset failed");
-        return -2;
-    }
-    long nb = (n + 256 * 16 - 1) / (256 * 16);
-    nb = nb < 1 ? 1 : (nb > 1024 ? 1024 : nb);
-    absmax_scalar_kernel<<<(unsigned)nb, 256, 0, s>>>(x, n, reinterpret_cast<unsigned int*>(out));
-    NPS_CHECK_LAUNCH("absmax (scalar)");
-    return 0;
+int nps_absmax_parts(const float* x, long n, float* parts, int max_parts, hipStream_t s) {
+    long nb = (n + 256 * 8 - 1) / (256 * 8);
+    nb = nb < 1 ? 1 : (nb > max_parts ? max_parts : nb);
+    absmax_parts_kernel<<<(unsigned)nb, 256, 0, s>>>(x, n, parts);
+    NPS_CHECK_LAUNCH("absmax (partials)");
+    return (int)nb;
 }
 namespace {
 }  // namespace

@@ -308,5 +308,6 @@ inline int x3_lds_bytes(const nps_conv2d_t& a) { return 128 + x3_region_bytes(a)
 
 // conv2d_x3.hip: launch of the split-fp16 kernel for a planned nps_conv2d_t
 int nps_launch_conv2d_x3(const nps_conv2d_t& a, int lds, hipStream_t s);
-// conv2d.hip: *out = max |x[i]| as one float (the packed-weight trailer; nps_absmax writes a range tag)
-int nps_absmax_scalar(const float* x, long n, float* out, hipStream_t s);
+// conv2d.hip: partial maxima of |x| (one per work-group, at most max_parts) to parts[]; returns their count
+// (the packed-weight trailer; nps_absmax writes a range tag)
+int nps_absmax_parts(const float* x, long n, float* parts, int max_parts, hipStream_t s);

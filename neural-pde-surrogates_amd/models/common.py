@@ -65,13 +65,8 @@ def crop_Nd(num_spatial_dims, enc_ftrs, shape):
 class _PackedMixin:
     """Caches the MFMA-packed copy of `weight`, re-packed when the parameter changes."""
 
-    def _packed(self, fn):
-        w = self.weight
-        key = (w.data_ptr(), w._version, str(w.device), ops.CONV_PRECISION)
-        if getattr(self, "_pk_key", None) != key:
-            self._pk = fn(w)
-            self._pk_key = key
-        return self._pk
+    def _packed(self, fn, kind="conv"):
+        return ops.cached_pack(self.weight, kind, fn)
 
 
 class Conv2d(_PackedMixin, nn.Conv2d):
@@ -106,24 +101,20 @@ class Conv2d(_PackedMixin, nn.Conv2d):
                 and len(srcs) == 1 and srcs[0].off_y == 0 and srcs[0].off_x == 0
                 and tuple(x.shape[1:3]) == tuple(frame_hw) and x.shape[3] % 4 == 0
                 and "gn" not in kw and not kw.get("pre_act")):
-            # U-Net Downsample: 3x3/s2 as a 2x2 stride-1 conv over a space-to-depth copy
+            # U-Net Downsample: 3x3/s2 as a 2x2 stride-1 conv over the space-to-depth input
             p = lo[0]
             Ho = (frame_hw[0] + 2 * p - 3) // 2 + 1
             Wo = (frame_hw[1] + 2 * p - 3) // 2 + 1
-            wk = self.weight
-            key = ("s2d", wk.data_ptr(), wk._version, str(wk.device), ops.CONV_PRECISION)
-            if getattr(self, "_pk2_key", None) != key:
-                self._pk2 = ops.pack_conv_weight_s2d(wk)
-                self._pk2_key = key
-            if ops.S2D_VIEW and x.shape[3] % 16 == 0 and self._pk2.nps_precision == ops.PREC_X3F16:
+            pk2 = self._packed(ops.pack_conv_weight_s2d, "s2d")
+            if ops.S2D_VIEW and x.shape[3] % 16 == 0 and pk2.nps_precision == ops.PREC_X3F16:
                 # the split-fp16 producers read the space-to-depth view straight from x (nps_conv2d_t.s2d)
-                return ops.conv2d([ops.Src(x)], (Ho + 1, Wo + 1), self._pk2, self.bias, self.out_channels, 2, 2,
+                return ops.conv2d([ops.Src(x)], (Ho + 1, Wo + 1), pk2, self.bias, self.out_channels, 2, 2,
                                   out_hw=(Ho, Wo), s2d_pad=p, **kw)
             xq = ops.space_to_depth(x, p, Ho + 1, Wo + 1)
-            return ops.conv2d([ops.Src(xq)], (Ho + 1, Wo + 1), self._pk2, self.bias, self.out_channels, 2, 2,
+            return ops.conv2d([ops.Src(xq)], (Ho + 1, Wo + 1), pk2, self.bias, self.out_channels, 2, 2,
                               out_hw=(Ho, Wo), **kw)
-        return ops.conv2d(srcs, frame_hw, self._packed(lambda w: ops.pack_conv_weight(w, s, d)), self.bias,
-                          self.out_channels, KH, KW,
+        pk = self._packed(lambda w: ops.pack_conv_weight(w, s, d), ("conv", s, d))
+        return ops.conv2d(srcs, frame_hw, pk, self.bias, self.out_channels, KH, KW,
                           stride=s, dil=d, pad=lo, pad_bottom=hi, circ=circ, **kw)
 
     def forward(self, x):
@@ -153,7 +144,7 @@ class ConvTranspose2d(_PackedMixin, nn.ConvTranspose2d):
         Hp, Wp = H + 2 * c, W + 2 * c
         Ho, Wo = 2 * Hp + 2 - 2 * p, 2 * Wp + 2 - 2 * p
         out = ops.empty_nhwc(B, Ho, Wo, self.out_channels, x)
-        phases = self._packed(ops.pack_convT_phases)
+        phases = self._packed(ops.pack_convT_phases, "convT")
         st = ops.new_stats(B, x)  # the 4 phases store every output element once: GroupNorm(1) moments of out
         if getattr(phases[0], "nps_precision", None) == ops.PREC_X3F16 and ops.MERGE_CONVT_PHASES:
             # one launch: the phases' work-groups share each input patch (nps_conv2d_t.nphase)
@@ -264,7 +255,7 @@ class Conv3d(_Packed3Mixin, _PackedMixin, nn.Conv3d):
     def run(self, srcs, frame_hw, **kw):
         """srcs: NDHWC sources viewed as (B, D*H, W, C); frame_hw = (D*H, W)."""
         self._check()
-        pk = self._packed(lambda w: ops.pack_conv_weight(w.reshape(w.shape[0], w.shape[1], 1, 1)))
+        pk = self._packed(lambda w: ops.pack_conv_weight(w.reshape(w.shape[0], w.shape[1], 1, 1)), "conv1d")
         return ops.conv2d(srcs, frame_hw, pk, self.bias, self.out_channels, 1, 1, **kw)
 
     def run_bf16(self, srcs, act=0, addend=None):

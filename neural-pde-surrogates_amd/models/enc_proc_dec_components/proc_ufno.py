@@ -64,8 +64,12 @@ class UFNO(nn.Module):
         act = activation_code(self.activation)
         for fno, unet in zip(self.fno_layers, self.unet_layers):
             srcs = [ops.Src(h)] + ([ops.Src(vb)] if vb is not None else [])
-            h_fno = fno.run(srcs)
-            h = unet.run(h, vb, addend=h_fno, act_after=act)
+            # the FNO layer and the U-Net read the same h: the FNO layer runs on a side stream (ops.Fork,
+            # lane 1) beside the U-Net, whose final conv joins it and adds its output
+            fork = ops.Fork(h, lane=1, on=ops.SIDE_FNO)
+            with fork:
+                h_fno = fno.run(srcs)
+            h = unet.run(h, vb, addend=h_fno, act_after=act, addend_fork=fork)
         return h
 
     def run3d(self, h, vb):

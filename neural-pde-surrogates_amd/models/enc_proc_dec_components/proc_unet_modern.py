@@ -86,9 +86,10 @@ class UNetModern(nn.Module):
             self.final = get_conv_with_right_spatial_dim(num_spatial_dims, in_channels=hidden_features,
                                                          out_channels=hidden_features, kernel_size=3, **padding_kwargs)
 
-    def run(self, h, vb, addend=None, act_after=0):
+    def run(self, h, vb, addend=None, act_after=0, addend_fork=None):
         """NHWC forward (proc_unet_modern.py:169-196).  Optional fused epilogue on the final conv:
-        out = act_after(final(...) + addend) — the U-FNO block combination."""
+        out = act_after(final(...) + addend) — the U-FNO block combination.  addend_fork: the ops.Fork whose
+        side stream computes addend (joined just before the final conv)."""
         if self.num_spatial_dims != 2:
             raise NotImplementedError("UNetModern: 2-D only on the MI355X path")
         if self.n_cond > 0 and vb is None:
@@ -125,6 +126,8 @@ class UNetModern(nn.Module):
             gn = _gn_args(self.norm, ops.group_norm_stats([ops.Src(h)], (H, W), self.norm.num_groups))
         oy, ox = crop_offsets(self.final_out_hw(H, W), h_shape[1:3])
         B, Ht, Wt = h_shape[0], h_shape[1], h_shape[2]
+        if addend_fork is not None:
+            addend_fork.join(addend)
         out = ops.empty_nhwc(B, Ht, Wt, self.final.out_channels, h)
         if oy > 0 or ox > 0:
             out.zero_()  # crop_Nd zero-pads when the output is smaller than the input
@@ -257,6 +260,18 @@ class ResidualBlock(nn.Module):
             self.norm2 = nn.Identity()
         self.num_spatial_dims = num_spatial_dims
 
+    def _shortcut_fork(self, x0, H, W):
+        """An ops.Fork for the shortcut when conv1's launch leaves >= SIDE_MIN_IDLE of the CUs idle in its
+        last round (the 258^2 convs: 1122 tiles on 256 CUs at B = 2), else None (no fork: cross-stream waits
+        cost more than an exact-round launch leaves idle)."""
+        if not (x0.is_cuda and ops.SIDE_STREAM):
+            return None
+        KH, KW, s, d, lo, hi, circ = self.conv1.geometry()
+        Ho = (H + 2 * circ + lo[0] + hi[0] - d * (KH - 1) - 1) // s + 1
+        Wo = (W + 2 * circ + lo[1] + hi[1] - d * (KW - 1) - 1) // s + 1
+        idle = ops.last_round_idle(Ho, Wo, x0.shape[0], self.conv1.out_channels, x0.device)
+        return ops.Fork(x0) if idle >= ops.SIDE_MIN_IDLE else None
+
     def run(self, srcs, frame_hw):
         """srcs: the virtual NHWC input x (concat of slices).  Returns crop_Nd(h, sc) + sc."""
         act = activation_code(self.activation)
@@ -264,15 +279,11 @@ class ResidualBlock(nn.Module):
         gn1 = gn2 = None
         if isinstance(self.norm1, nn.GroupNorm):
             gn1 = _gn_args(self.norm1, ops.group_norm_stats(srcs, (H, W), self.norm1.num_groups))
-        # conv1 adds norm2's moments of h1 as it stores it (ops.conv2d out_stats): no statistics pass
-        st1 = ops.new_stats(srcs[0].t.shape[0], srcs[0].t) if isinstance(self.norm2, nn.GroupNorm) else None
-        h1 = self.conv1.run(srcs, (H, W), gn=gn1, pre_act=act, out_stats=st1)
-        if st1 is not None:
-            ops.attach_stats(h1, st1)
         # The block output's moments (the next block's norm1): those of the shortcut output — x's own for
         # the identity, else added by the 1x1 conv — then conv2, accumulating at its crop offset, adds
         # the change it makes (nps_conv2d_t.out_stats)
-        st2 = None
+        st2 = out = None
+        fork = None
         if isinstance(self.shortcut, nn.Identity):
             if len(srcs) != 1 or srcs[0].off_y or srcs[0].off_x or tuple(srcs[0].t.shape[1:3]) != (H, W):
                 raise RuntimeError("identity shortcut on a concatenated input")
@@ -280,11 +291,26 @@ class ResidualBlock(nn.Module):
             if isinstance(self.norm1, nn.GroupNorm):
                 st2 = ops.copy_stats(ops.source_stats(srcs[0].t))
         else:
+            # the 1x1 shortcut reads only x: it runs on a side stream beside conv1 (ops.Fork) when conv1's
+            # persistent grid leaves many CUs idle in its last round (the 258^2 convs), its work-groups
+            # taking them; its moments buffer is taken before the fork point (no fill on the side stream)
             st2 = ops.new_stats(srcs[0].t.shape[0], srcs[0].t) if isinstance(self.norm1, nn.GroupNorm) else None
-            out = self.shortcut.run(srcs, (H, W), out_stats=st2)
+            fork = self._shortcut_fork(srcs[0].t, H, W)
+            if fork is None:
+                out = self.shortcut.run(srcs, (H, W), out_stats=st2)
+        # conv1 adds norm2's moments of h1 as it stores it (ops.conv2d out_stats): no statistics pass
+        st1 = ops.new_stats(srcs[0].t.shape[0], srcs[0].t) if isinstance(self.norm2, nn.GroupNorm) else None
+        h1 = self.conv1.run(srcs, (H, W), gn=gn1, pre_act=act, out_stats=st1)
+        if st1 is not None:
+            ops.attach_stats(h1, st1)
+        if fork is not None:
+            with fork:
+                out = self.shortcut.run(srcs, (H, W), out_stats=st2)
         H1, W1 = h1.shape[1:3]
         if isinstance(self.norm2, nn.GroupNorm):
             gn2 = _gn_args(self.norm2, ops.group_norm_stats([ops.Src(h1)], (H1, W1), self.norm2.num_groups))
+        if fork is not None:
+            fork.join(out)  # conv2 accumulates into the shortcut output
         KH, KW, s, d, lo, hi, circ = self.conv2.geometry()
         H2 = (H1 + 2 * circ + lo[0] + hi[0] - d * (KH - 1) - 1) // s + 1
         W2 = (W1 + 2 * circ + lo[1] + hi[1] - d * (KW - 1) - 1) // s + 1

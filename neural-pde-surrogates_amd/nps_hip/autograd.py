@@ -196,11 +196,6 @@ def crop(x: torch.Tensor, out_hw, off) -> torch.Tensor:
 
 
 # ------------------------------------------------------------------------- conv
-def _dgrad_weight(w):
-    """conv weight [Cout][Cin][KH][KW] -> the weight of the input-gradient conv [Cin][Cout][KH][KW] (flipped)."""
-    return w.detach().flip(2, 3).transpose(0, 1).contiguous()
-
-
 def _s2_phase_weight(w, ry, rx, p):
     """Input-gradient phase (ry, rx) of a stride-2 3x3 conv with top/left padding p in {0, 1}: dx[2q + r]
     sums dy[o] w[k] over 2o + k - p = 2q + r, i.e. o in {q - 1 + p, q + p}.  As a 2x2 conv of dy with top
@@ -235,11 +230,13 @@ class Conv2dFn(torch.autograd.Function):
             p = lo[0]
             Ho, Wo = (H + 2 * p - 3) // 2 + 1, (W + 2 * p - 3) // 2 + 1
             xq = ops.space_to_depth(x, p, Ho + 1, Wo + 1)
-            y = ops.conv2d([Src(xq)], (Ho + 1, Wo + 1), ops.pack_conv_weight_s2d(weight), bias, Cout, 2, 2,
+            y = ops.conv2d([Src(xq)], (Ho + 1, Wo + 1), ops.cached_pack(weight, "s2d", ops.pack_conv_weight_s2d),
+                           bias, Cout, 2, 2,
                            out_hw=(Ho, Wo))
             ctx.save_for_backward(xq, weight)
         elif s == 1:
-            y = ops.conv2d([Src(x)], (H, W), ops.pack_conv_weight(weight, 1, d), bias, Cout, KH, KW, dil=d, pad=lo,
+            wp = ops.cached_pack(weight, ("conv", 1, d), lambda w: ops.pack_conv_weight(w, 1, d))
+            y = ops.conv2d([Src(x)], (H, W), wp, bias, Cout, KH, KW, dil=d, pad=lo,
                            pad_bottom=hi, circ=circ)
             ctx.save_for_backward(x, weight)
         else:
@@ -262,11 +259,11 @@ class Conv2dFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             if s == 1:
                 if circ:
-                    dx = ops.conv2d([Src(gy)], (Ho, Wo), _pack_plain(_dgrad_weight(w), d), None, Cin, KH, KW, dil=d,
+                    dx = ops.conv2d([Src(gy)], (Ho, Wo), ops.pack_conv_weight_dgrad(w, d), None, Cin, KH, KW, dil=d,
                                     circ=circ, out_hw=(H, W), in_scale=rng)
                 else:
                     pt = (d * (KH - 1) - lo[0], d * (KW - 1) - lo[1])
-                    dx = ops.conv2d([Src(gy)], (Ho, Wo), _pack_plain(_dgrad_weight(w), d), None, Cin, KH, KW, dil=d,
+                    dx = ops.conv2d([Src(gy)], (Ho, Wo), ops.pack_conv_weight_dgrad(w, d), None, Cin, KH, KW, dil=d,
                                     pad=pt, out_hw=(H, W), in_scale=rng)
             else:
                 p = lo[0]
@@ -307,7 +304,7 @@ class ConvTranspose2dFn(torch.autograd.Function):
         Hp, Wp = H + 2 * c, W + 2 * c
         Ho, Wo = 2 * Hp + 2 - 2 * p, 2 * Wp + 2 - 2 * p
         out = ops.empty_nhwc(B, Ho, Wo, Cout, x)
-        phases = ops.pack_convT_phases(weight)
+        phases = ops.cached_pack(weight, "convT", ops.pack_convT_phases)
         for ph in range(4):
             py, px = ph >> 1, ph & 1
             ops.conv2d([Src(x)], (H, W), phases[ph], bias, Cout, 2, 2, pad=(1, 1), circ=c, out_hw=(Hp + 1, Wp + 1),

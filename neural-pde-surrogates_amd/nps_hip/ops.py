@@ -75,7 +75,15 @@ class _TagArena:
         tags reserves them all before it reads any tag pointer, so no wrap (which zeroes the buffer)
         can happen between reading an input tag and launching the kernel that reads it."""
         if self.next + k > _ARENA_TAGS:
-            self.buf.zero_()        # stream-ordered after every kernel that used the old generation
+            # stream-ordered after every kernel that used the old generation; once side streams (Fork) have
+            # carried launches, the device drains before and after the zero so no stream's kernel can read
+            # or raise a tag across it (a wrap comes every few model calls)
+            fenced = _forked and self.buf.is_cuda
+            if fenced:
+                torch.cuda.synchronize(self.buf.device)
+            self.buf.zero_()
+            if fenced:
+                torch.cuda.synchronize(self.buf.device)
             self.gen += 1
             self.next = 0
 
@@ -97,6 +105,87 @@ class _Tag(NamedTuple):
 
 
 _arenas = {}
+_forked = False  # set by the first Fork that runs launches on a side stream
+
+
+# ----------------------------------------------------------------- side streams ----
+# Launches that do not depend on the one just issued (the ResidualBlock's 1x1 shortcut beside conv1, the U-FNO
+# block's FNO layer beside its U-Net) go to a second HIP stream, so their work-groups take the CUs a
+# persistent 3x3 launch leaves idle in its last round (B = 2: the 258^2 convs are 1122 tiles on 256 CUs,
+# 4.4 rounds).  Each lane is one stream per device (one hardware queue).  dev knob NPS_SIDE_STREAM=0: off.
+SIDE_STREAM = os.environ.get("NPS_SIDE_STREAM", "1") == "1"
+SIDE_FNO = os.environ.get("NPS_SIDE_FNO", "1") == "1"      # dev knob: the U-FNO block's FNO layer fork
+# dev knob: the shortcut fork needs conv1's last round to leave at least this fraction of the CUs idle
+SIDE_MIN_IDLE = float(os.environ.get("NPS_SIDE_MIN_IDLE", "0.25"))
+_side_streams = {}
+_side_depth = 0   # > 0 while launches go to a side stream
+
+
+_ncu = {}
+
+
+def last_round_idle(Ho: int, Wo: int, B: int, Cout: int, device) -> float:
+    """Fraction of the CUs left idle in the last round of a wide split-fp16 3x3 launch (the persistent grid
+    of nps_launch_conv2d_x3: one work-group per CU, 16 x 8-pixel x 192-channel tiles as nps_conv2d_plan
+    picks them for these shapes).  A fork beside such a launch pays only when this is large: every
+    cross-stream wait costs ~15 us (profiles/r4/experiments/side_stream_forks_ab.txt)."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    n = _ncu.get(idx)
+    if n is None:
+        n = _ncu[idx] = torch.cuda.get_device_properties(idx).multi_processor_count & ~7
+    tiles = -(-Ho // 16) * -(-Wo // 8) * B * -(-Cout // 192)
+    last = tiles % n
+    return 0.0 if last == 0 else 1.0 - last / n
+
+
+class Fork:
+    """`f = Fork(t)` marks the fork point on the current stream (t: any tensor of the device);
+    `with f:` issues the enclosed launches on side stream `lane`, which starts at the fork point;
+    `f.join(*outs)` makes the current stream wait for them and hands it the tensors they allocated.
+    Moments buffers made inside (new_stats) are private zeros of the side stream; the tag arena fences a
+    wrap across all streams.  A no-op on the CPU or with NPS_SIDE_STREAM=0."""
+
+    def __init__(self, like: torch.Tensor, lane: int = 0, on: bool = True):
+        d = like.device
+        self.on = on and SIDE_STREAM and d.type == "cuda"
+        self.done = None
+        if not self.on:
+            return
+        idx = d.index if d.index is not None else torch.cuda.current_device()
+        key = (idx, lane)
+        self.side = _side_streams.get(key)
+        if self.side is None:
+            self.side = _side_streams[key] = torch.cuda.Stream(device=idx)
+        self.main = torch.cuda.current_stream(idx)
+        self.start = torch.cuda.Event()
+        self.start.record(self.main)
+
+    def __enter__(self):
+        global _side_depth, _forked
+        if self.on:
+            _forked = True
+            self.side.wait_event(self.start)
+            self._ctx = torch.cuda.stream(self.side)
+            self._ctx.__enter__()
+            _side_depth += 1
+        return self
+
+    def __exit__(self, *exc):
+        global _side_depth
+        if self.on:
+            _side_depth -= 1
+            self._ctx.__exit__(*exc)
+            self.done = torch.cuda.Event()
+            self.done.record(self.side)
+        return False
+
+    def join(self, *outs):
+        if self.done is not None:
+            self.main.wait_event(self.done)
+            for t in outs:
+                if isinstance(t, torch.Tensor):
+                    t.record_stream(self.main)
+            self.done = None
 
 
 def _arena(device) -> _TagArena:
@@ -189,7 +278,7 @@ def new_stats(B: int, like: torch.Tensor, sub: int = STATS_SUB) -> torch.Tensor:
     d = like.device
     key = (d.type, d.index if d.index is not None else torch.cuda.current_device())
     ch = _stats_chunks.get(key)
-    if n > _STATS_CHUNK // 4:
+    if n > _STATS_CHUNK // 4 or _side_depth > 0:  # (a side stream's buffers are zeroed on that stream)
         return torch.zeros((B, sub, 2), dtype=torch.float64, device=d)
     if ch is None or ch[1] + n > _STATS_CHUNK:
         ch = [torch.zeros(_STATS_CHUNK, dtype=torch.float64, device=d), 0]
@@ -278,12 +367,35 @@ def _pack(w, Cout, Cin, KH, KW, mode, precision):
     return out
 
 
+def cached_pack(w: torch.Tensor, kind, fn):
+    """fn(w) — a packed copy of the parameter w — cached on w per `kind` until w changes (data pointer,
+    w._version: the optimizer's in-place step bumps it) or the conv precision does.  The inference run()
+    paths and the autograd functions share the cache, so a training step packs each weight once for the
+    no-grad pushforward unroll and the differentiable forward together."""
+    key = (w.data_ptr(), w._version, str(w.device), CONV_PRECISION)
+    cache = getattr(w, "_nps_packs", None)
+    if cache is None:
+        cache = w._nps_packs = {}
+    ent = cache.get(kind)
+    if ent is None or ent[0] != key:
+        ent = cache[kind] = (key, fn(w))
+    return ent[1]
+
+
 def pack_conv_weight(w: torch.Tensor, stride=1, dil=1) -> torch.Tensor:
     """nn.Conv2d weight (Cout, Cin, KH, KW) -> MFMA-fragment-packed buffer (fp32 or split-fp16 fragments,
     whichever the conv of this geometry runs in)."""
     w = w.detach().contiguous()
     Cout, Cin, KH, KW = w.shape
     return _pack(w, Cout, Cin, KH, KW, -1, conv_precision(KH, KW, stride, dil))
+
+
+def pack_conv_weight_dgrad(w: torch.Tensor, dil=1) -> torch.Tensor:
+    """Weight (Cout, Cin, KH, KW) of a stride-1 conv -> the packed weight of its input-gradient conv
+    (Cin outputs, Cout inputs, taps flipped): the transpose + flip happen inside the pack kernel (mode -3)."""
+    w = w.detach().contiguous()
+    Cout, Cin, KH, KW = w.shape
+    return _pack(w, Cin, Cout, KH, KW, -3, conv_precision(KH, KW, 1, dil))
 
 
 def pack_conv_weight_s2d(w: torch.Tensor) -> torch.Tensor:

@@ -440,3 +440,18 @@ def test_pushforward_train_one_epoch():
     for _ in range(3):
         l2 = float(tr2.train_one_epoch([(u2[:, :, :1], u2, pos, cond, torch.empty(u2.shape[0], 0, device=DEV), sc)], epoch=3))
         assert l2 == l2
+
+
+@pytest.mark.parametrize("cout,cin,k,dil", [(192, 388, 3, 1), (192, 196, 1, 1), (4, 16, 2, 1), (40, 84, 1, 1),
+                                            (64, 64, 5, 3), (8, 12, 3, 1)])
+def test_dgrad_packing_equals_flipped_transpose(cout, cin, k, dil):
+    """pack_weights mode -3 (the input-gradient conv's weight, transposed + flipped inside the pack kernel)
+    is bit-identical to packing the torch flip/transpose of w (both arithmetics: 5x5 dilated packs fp32)."""
+    from nps_hip import ops
+    torch.manual_seed(cout + cin + k)
+    w = (torch.randn(cout, cin, k, k) * 0.1).to(DEV)
+    got = ops.pack_conv_weight_dgrad(w, dil)
+    ref = ops.pack_conv_weight(w.flip(2, 3).transpose(0, 1).contiguous(), 1, dil)
+    assert got.nps_precision == ref.nps_precision
+    body = got.numel() - 64 + 1  # fragment body + trailer[0] (max|w|); the rest of the trailer is unwritten
+    assert torch.equal(got[:body], ref[:body])

@@ -280,6 +280,27 @@ def test_processor_golden(name):
     assert rel_l2(y, g["y"]) < TOL
 
 
+@pytest.mark.parametrize("min_idle", [0.0, 0.25])
+def test_side_stream_forks_match_serial(monkeypatch, min_idle):
+    """ops.Fork (the U-FNO block's FNO layer and the ResidualBlock shortcuts on side streams): the U-FNO
+    processor golden, forks on (every shortcut forked at min_idle 0) vs all launches on one stream — the same
+    kernels on the same inputs, so equal up to the order of the moments' float atomics (rel-L2 < 1e-6)."""
+    from nps_hip import ops
+    m, g = _proc("ufno")
+    h, vb = g["h"].to(DEV), g["vb"].to(DEV)
+    monkeypatch.setattr(ops, "SIDE_STREAM", False)
+    with torch.no_grad():
+        y0 = m(h=h, variables_broadcast=vb)
+    monkeypatch.setattr(ops, "SIDE_STREAM", True)
+    monkeypatch.setattr(ops, "SIDE_MIN_IDLE", min_idle)
+    with torch.no_grad():
+        y1 = m(h=h, variables_broadcast=vb)
+        y2 = m(h=h, variables_broadcast=vb)
+    torch.cuda.synchronize()
+    assert rel_l2(y1, y0) < 1e-6 and rel_l2(y2, y0) < 1e-6
+    assert rel_l2(y1.cpu(), g["y"]) < TOL
+
+
 # ------------------------------------------------------------------ full models + rollout
 def _build_model(g):
     import models

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 GPU pass (gpurun): parity suite, C3 bench + rocprof, B=2 line, training lines (B=2, B=16) + rocprof of
 # the B=16 step, C5 (ufno3d bf16) line + rocprof, N=2 training rehearsal.  Outputs: gpurun_out/${TAG}_*.
-# usage: tools/r4_full.sh TAG [steps...]   steps: tests sel($TESTSEL) pmc bench prof b2 b2prof train trainprof c5 c5prof reh (default: all)
+# usage: tools/r4_full.sh TAG [steps...]   steps: tests sel($TESTSEL) pmc bench prof b2 b2prof train trainprof tb2prof c5 c5prof reh (default: all)
 set -o pipefail
 TAG=${1:-r4full}; shift
 STEPS="${@:-tests bench prof b2 train trainprof c5 c5prof reh}"
@@ -25,6 +25,8 @@ for s in $STEPS; do
              || { echo "train $gb failed"; tail -20 ${O}_train_b$gb.err; exit 1; }; tail -c 300 ${O}_train_b$gb.json; done ;;
     trainprof) timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d ${O}_tprof -o run -- python3 bench.py --mode train --steps 3 --warmup 1 --global-batch 16 --cpu-calls 0 \
              > ${O}_tprof.log 2>&1 || { echo "train prof failed"; tail -20 ${O}_tprof.log; exit 1; } ;;
+    tb2prof) timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d ${O}_tb2prof -o run -- python3 bench.py --mode train --steps 5 --warmup 2 --global-batch 2 --cpu-calls 0 \
+             > ${O}_tb2prof.log 2>&1 || { echo "train b2 prof failed"; tail -20 ${O}_tb2prof.log; exit 1; } ;;
     c5)    timeout -k 10 400 python -u bench.py --model ufno3d --dtype bf16 > ${O}_c5.json 2> ${O}_c5.err || { echo "c5 failed"; tail -20 ${O}_c5.err; exit 1; }; tail -c 300 ${O}_c5.json ;;
     c5prof) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d ${O}_c5prof -o run -- python3 bench.py --model ufno3d --dtype bf16 --steps 3 --warmup 1 --cpu-calls 0 \
              > ${O}_c5prof.log 2>&1 || { echo "c5 prof failed"; tail -20 ${O}_c5prof.log; exit 1; } ;;
