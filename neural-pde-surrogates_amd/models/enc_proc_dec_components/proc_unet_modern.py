@@ -170,7 +170,7 @@ class UNetModern(nn.Module):
         y = ad.conv2d(self.final, ad.frame([ops.Src(h)], (H, W), norm, activation_code(self.activation)))
         return ad.crop(y, h_shape[1:3], crop_offsets(y.shape[1:3], h_shape[1:3]))
 
-    def run3d(self, h, vb, addend=None, act_after=0):
+    def run3d(self, h, vb, addend=None, act_after=0, addend_fork=None):
         """NDHWC forward of the 3-D U-Net (proc_unet_modern.py:169-196 with num_spatial_dims=3; the 3-D
         Upsample is this build's ConvTranspose3d_padded), fp32 or bf16 storage.  Optional fused epilogue on
         the final conv: out = act_after(final(...) + addend) — the U-FNO block combination."""
@@ -209,6 +209,8 @@ class UNetModern(nn.Module):
         K, s, circ, zpad = self.final.geometry3d()
         fo = tuple((n + 2 * (circ + zpad) - K) // s + 1 for n in dhw)
         off = crop_offsets3(fo, h_shape[1:4])
+        if addend_fork is not None:
+            addend_fork.join(addend)
         out = torch.empty(tuple(h_shape[:4]) + (self.final.out_channels,), dtype=h.dtype, device=h.device)
         if any(o > 0 for o in off):
             out.zero_()  # crop_Nd zero-pads when the output is smaller than the input

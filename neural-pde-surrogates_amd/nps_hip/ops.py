@@ -115,6 +115,14 @@ _forked = False  # set by the first Fork that runs launches on a side stream
 # 4.4 rounds).  Each lane is one stream per device (one hardware queue).  dev knob NPS_SIDE_STREAM=0: off.
 SIDE_STREAM = os.environ.get("NPS_SIDE_STREAM", "1") == "1"
 SIDE_FNO = os.environ.get("NPS_SIDE_FNO", "1") == "1"      # dev knob: the U-FNO block's FNO layer fork
+# ... for activations of at most this many elements (B=2 C3: 25 M; at B=16, 201 M, the U-Net's launches keep
+# the CUs busy and the FNO layer's kernels only stretch them: +0.4 %, profiles/r4/experiments/side_stream_*)
+SIDE_FNO_MAX_ELEMS = int(float(os.environ.get("NPS_SIDE_FNO_MAX_ELEMS", "6.4e7")))
+
+
+def fno_fork(h: torch.Tensor) -> "Fork":
+    """The U-FNO block's fork for its FNO layer (lane 1): on for small activations (see SIDE_FNO_MAX_ELEMS)."""
+    return Fork(h, lane=1, on=SIDE_FNO and h.numel() <= SIDE_FNO_MAX_ELEMS)
 # dev knob: the shortcut fork needs conv1's last round to leave at least this fraction of the CUs idle
 SIDE_MIN_IDLE = float(os.environ.get("NPS_SIDE_MIN_IDLE", "0.25"))
 _side_streams = {}

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Same-box A/B of the side-stream forks (ops.Fork): model parity tests with forks on, then the C3 rollout at
 # B = 2 and B = 16 with the forks off / shipped (shortcut fork gated on conv1's last-round idle CUs) / every shortcut forked /
-# FNO-layer fork only, two rounds each, plus a kernel trace
+# FNO-layer fork at every size, two rounds each, plus a kernel trace
 # of the B = 2 rollout with forks on.  usage: tools/side_ab.sh TAG     outputs: gpurun_out/TAG_*
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
@@ -9,7 +9,7 @@ TAG=${1:-side}
 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread \
     > gpurun_out/${TAG}_tests.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/${TAG}_tests.log; exit 1; }
 tail -2 gpurun_out/${TAG}_tests.log
-VARIANTS=("NPS_SIDE_STREAM=0" "NPS_SIDE_STREAM=1" "NPS_SIDE_MIN_IDLE=0" "NPS_SIDE_MIN_IDLE=2")
+VARIANTS=("NPS_SIDE_STREAM=0" "NPS_SIDE_STREAM=1" "NPS_SIDE_MIN_IDLE=0" "NPS_SIDE_FNO_MAX_ELEMS=1e12")
 for r in 1 2; do
   for gb in 2 16; do
     for V in "${VARIANTS[@]}"; do
