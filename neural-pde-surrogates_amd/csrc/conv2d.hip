@@ -495,8 +495,19 @@ __global__ void pack_weights_kernel(const float* __restrict__ w, float* __restri
 __global__ void pack_weights_x3_kernel(const float* __restrict__ w, _Float16* __restrict__ wp, int Cout, int Cin,
                                        int KH, int KW, int tphase, size_t total_pairs, float* __restrict__ wmax,
                                        int nparts) {
+    // max|w| from the absmax partials in trailer[1 .. nparts] (wave 0 reduces them, LDS broadcast); the first
+    // thread of the launch publishes it as trailer[0]
+    __shared__ float s_max;
+    if (threadIdx.x < 64) {
+        const float p = (int)threadIdx.x < nparts ? wmax[1 + threadIdx.x] : 0.f;
+        const float mw = nps::wave_max(p);
+        if (threadIdx.x == 0) s_max = mw;
+    }
+    __syncthreads();
+    const float m = s_max;
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // (hi, lo) pair index
     if (i >= total_pairs) return;
+    if (i == 0) wmax[0] = m;
     const int ntaps = KH * KW;
     const int ncb = packed_ncb(Cout);
     const int j = i & 7;
@@ -510,9 +521,6 @@ __global__ void pack_weights_x3_kernel(const float* __restrict__ w, _Float16* __
     // fetches 64 contiguous bytes per lane); other tap counts: chunk c = channels [16c, 16c + 16)
     const int ci = ntaps == 1 && (tphase == -1 || tphase == -3) ? (chunk >> 1) * 32 + (lane >> 5) * 16 + (chunk & 1) * 8 + j
                                               : chunk * CK + (lane >> 5) * 8 + j;
-    float m = 0.f;  // max|w| from the absmax partials in trailer[1 .. nparts]; thread 0 publishes it as trailer[0]
-    for (int k = 0; k < nparts; ++k) m = fmaxf(m, wmax[1 + k]);
-    if (i == 0) wmax[0] = m;
     const float v = pow2_scale_for(m) * weight_elem(w, Cout, Cin, KH, KW, tphase, cb * 32 + (lane & 31), ci, tap);
     const size_t frag = i >> 9;  // (chunk, tap, cb) fragment of 64 lanes x 8
     const size_t o = frag * 1024 + (size_t)lane * 8 + j;
@@ -1150,23 +1158,38 @@ __global__ void absmax_kernel(const float* __restrict__ x, long n, float* __rest
 // plain scalar max|x| into *out (one float; the packed-weight trailer): single-address atomics, used once
 // per parameter version
 // one partial max|x| per work-group (no atomics, no zero-fill): parts[blockIdx.x]
-__global__ __launch_bounds__(256) void absmax_parts_kernel(const float* __restrict__ x, long n,
-                                                           float* __restrict__ parts) {
-    __shared__ float wm[4];
+// (1024 threads, 16-B loads when x is 16-B aligned: at most 63 work-groups must cover a whole weight)
+__global__ __launch_bounds__(1024) void absmax_parts_kernel(const float* __restrict__ x, long n,
+                                                            float* __restrict__ parts) {
+    __shared__ float wm[16];
     float m = 0.f;
-    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
-        m = fmaxf(m, fabsf(x[i]));
+    const long t0 = (long)blockIdx.x * blockDim.x + threadIdx.x, step = (long)gridDim.x * blockDim.x;
+    long tail = 0;
+    if ((reinterpret_cast<size_t>(x) & 15) == 0) {
+        const long n4 = n >> 2;
+        const float4* x4 = reinterpret_cast<const float4*>(x);
+        for (long i = t0; i < n4; i += step) {
+            const float4 v = x4[i];
+            m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+        }
+        tail = n4 << 2;
+    }
+    for (long i = tail + t0; i < n; i += step) m = fmaxf(m, fabsf(x[i]));
     m = nps::wave_max(m);
     if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
     __syncthreads();
-    if (threadIdx.x == 0) parts[blockIdx.x] = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
+    if (threadIdx.x < 64) {
+        float v = (int)threadIdx.x < (int)(blockDim.x >> 6) ? wm[threadIdx.x] : 0.f;
+        v = nps::wave_max(v);
+        if (threadIdx.x == 0) parts[blockIdx.x] = v;
+    }
 }
 }  // namespace
 
 int nps_absmax_parts(const float* x, long n, float* parts, int max_parts, hipStream_t s) {
-    long nb = (n + 256 * 8 - 1) / (256 * 8);
+    long nb = (n + 1024 * 16 - 1) / (1024 * 16);
     nb = nb < 1 ? 1 : (nb > max_parts ? max_parts : nb);
-    absmax_parts_kernel<<<(unsigned)nb, 256, 0, s>>>(x, n, parts);
+    absmax_parts_kernel<<<(unsigned)nb, 1024, 0, s>>>(x, n, parts);
     NPS_CHECK_LAUNCH("absmax (partials)");
     return (int)nb;
 }
