@@ -98,14 +98,18 @@ def conv_roofline(model, x, cond, pos, sc):
 
 def probe_roofline(fn):
     """Run fn() with every conv / weight-gradient launch bracketed by HIP events on its stream
-    (ops.conv_probe); roofline of the class with the largest total time."""
+    (ops.conv_probe); roofline of the class with the largest total time.  The probe call runs on one stream
+    (ops.SIDE_STREAM off): a launch on a side stream would be timed from its dispatch, including the wait for
+    CUs a concurrent launch holds, not its own duration (the timed steps keep the side streams)."""
     from nps_hip import ops
     ops.conv_probe = []
+    side, ops.SIDE_STREAM = ops.SIDE_STREAM, False
     try:
         fn()
         torch.cuda.synchronize()
     finally:
         probe, ops.conv_probe = ops.conv_probe, None
+        ops.SIDE_STREAM = side
     groups = {}
     for e0, e1, f, (prec, ntaps, waves), nb in probe:
         g = groups.setdefault((prec, ntaps), [0.0, 0.0, 0, 0.0])
