@@ -141,9 +141,13 @@ def last_round_idle(Ho: int, Wo: int, B: int, Cout: int, device) -> float:
     n = _ncu.get(idx)
     if n is None:
         n = _ncu[idx] = torch.cuda.get_device_properties(idx).multi_processor_count & ~7
-    tiles = -(-Ho // 16) * -(-Wo // 8) * B * -(-Cout // 192)
-    last = tiles % n
-    return 0.0 if last == 0 else 1.0 - last / n
+    return idle_fraction(-(-Ho // 16) * -(-Wo // 8) * B * -(-Cout // 192), n)
+
+
+def idle_fraction(tiles: int, workgroups: int) -> float:
+    """Idle share of a persistent grid of `workgroups` in the last round of `tiles` tiles."""
+    last = tiles % workgroups
+    return 0.0 if last == 0 else 1.0 - last / workgroups
 
 
 class Fork:

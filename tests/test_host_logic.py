@@ -141,3 +141,41 @@ def test_3d_ufno_multires_defines_the_upsample():
     with pytest.raises(NotImplementedError, match="spatial dim 3"):
         UFNO(pde=None, num_spatial_dims=3, n_cond=4, hidden_features=16, hidden_blocks=1, fno_modes=(4, 4, 4),
              ch_mults=(1, 1), is_attn=(False, False), norm=True, padding_mode="ones")
+
+
+def test_side_stream_fork_host_logic():
+    """ops.Fork is a no-op for CPU tensors (enter / exit / join touch no device); the shortcut-fork gate's
+    last-round idle share of the persistent 3x3 grid (ops.last_round_idle: 16 x 8-pixel tiles, 256 CUs)."""
+    from nps_hip import ops
+    x = torch.zeros(2, 4, 4, 8)
+    f = ops.Fork(x)
+    assert not f.on
+    with f:
+        y = x + 1
+    f.join(y)
+    assert ops._side_depth == 0
+    tiles = lambda H, W, B: -(-H // 16) * -(-W // 8) * B  # noqa: E731
+    assert tiles(258, 258, 2) == 1122 and abs(ops.idle_fraction(1122, 256) - (1 - 98 / 256)) < 1e-12
+    assert ops.idle_fraction(tiles(256, 256, 2), 256) == 0.0      # exact rounds: no fork
+    assert ops.idle_fraction(tiles(125, 125, 2), 256) == 0.0
+    assert ops.idle_fraction(tiles(258, 258, 16), 256) == 1 - 16 / 256
+
+
+def test_cached_pack_follows_parameter_version():
+    """ops.cached_pack re-packs when the parameter changes in place (optimizer step: _version bump) and keeps
+    one entry per kind."""
+    from nps_hip import ops
+    w = nn.Parameter(torch.randn(4, 4))
+    calls = []
+
+    def fn(t):
+        calls.append(t._version)
+        return t.detach().clone()
+    a = ops.cached_pack(w, "conv", fn)
+    assert ops.cached_pack(w, "conv", fn) is a and len(calls) == 1
+    ops.cached_pack(w, "dgrad", fn)
+    assert len(calls) == 2
+    with torch.no_grad():
+        w.add_(1.0)
+    b = ops.cached_pack(w, "conv", fn)
+    assert len(calls) == 3 and torch.equal(b, w.detach())
