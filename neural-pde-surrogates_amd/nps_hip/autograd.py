@@ -256,6 +256,9 @@ class Conv2dFn(torch.autograd.Function):
         if ops.CONV_PRECISION == ops.PREC_X3F16 and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2]):
             ops.reserve_tags(gy.device, 3)
             rng = _range_ptr(gy)  # gradients: any magnitude (its tag, or one absmax pass shared by dx and dw)
+        # the weight gradient reads only gy and x: it runs on a side stream beside the input-gradient conv(s)
+        # (ops.Fork), each filling the CUs the other's last round leaves idle; joined before returning
+        fork = ops.Fork(gy, on=ops.SIDE_WGRAD and ctx.needs_input_grad[1] and ctx.needs_input_grad[2])
         if ctx.needs_input_grad[1]:
             if s == 1:
                 if circ:
@@ -277,15 +280,17 @@ class Conv2dFn(torch.autograd.Function):
                                    pad=(1 - p, 1 - p), out_hw=(hq, wq), out=dx, out_os=2, out_off=(ry, rx),
                                    in_scale=rng)
         if ctx.needs_input_grad[2]:
-            if s == 1:
-                dw = wgrad(gy, xs, KH, KW, dil=d, pad=lo, circ=circ, a_range=rng)
-                if dw.shape[1] != Cin:      # input carried zero padding channels (packed encoder input)
-                    dw = dw[:, :Cin].contiguous()
-            else:
-                C = Cin
-                G = wgrad(gy, xs, 2, 2, a_range=rng)                       # [Cout][4C][2][2]
-                G = G.view(Cout, 2, 2, C, 2, 2).permute(0, 3, 4, 1, 5, 2).reshape(Cout, C, 4, 4)
-                dw = G[:, :, :3, :3].contiguous()
+            with fork:
+                if s == 1:
+                    dw = wgrad(gy, xs, KH, KW, dil=d, pad=lo, circ=circ, a_range=rng)
+                    if dw.shape[1] != Cin:      # input carried zero padding channels (packed encoder input)
+                        dw = dw[:, :Cin].contiguous()
+                else:
+                    C = Cin
+                    G = wgrad(gy, xs, 2, 2, a_range=rng)                       # [Cout][4C][2][2]
+                    G = G.view(Cout, 2, 2, C, 2, 2).permute(0, 3, 4, 1, 5, 2).reshape(Cout, C, 4, 4)
+                    dw = G[:, :, :3, :3].contiguous()
+            fork.join(dw)
         if ctx.has_bias and ctx.needs_input_grad[3]:
             db = channel_sums(gy)
         return None, dx, dw, db
@@ -324,6 +329,7 @@ class ConvTranspose2dFn(torch.autograd.Function):
         # the transposed conv's adjoint is a 4x4 stride-2 conv of gout: space-to-depth + 2x2 conv
         dq = ops.space_to_depth(gout, p, Hp + 1, Wp + 1)                    # [B][Hp+1][Wp+1][4 Cout]
         dx = dw = db = None
+        fork = ops.Fork(gout, on=ops.SIDE_WGRAD and ctx.needs_input_grad[1] and ctx.needs_input_grad[2])
         if ctx.needs_input_grad[1]:
             w2 = w.detach().view(Cin, Cout, 2, 2, 2, 2).permute(0, 3, 5, 1, 2, 4).reshape(Cin, 4 * Cout, 2, 2)
             dxp = ops.conv2d([Src(dq)], (Hp + 1, Wp + 1), _pack_plain(w2.contiguous()), None, Cin, 2, 2,
@@ -334,13 +340,15 @@ class ConvTranspose2dFn(torch.autograd.Function):
             else:
                 dx = dxp
         if ctx.needs_input_grad[2]:
-            if c:
-                xp = torch.empty((B, Hp, Wp, Cin), dtype=torch.float32, device=x.device)
-                check(lib.nps_circular_pad(ptr(x), ptr(xp), B, H, W, Cin, c, stream_ptr()), "circular_pad")
-            else:
-                xp = x
-            G = wgrad(xp, dq, 2, 2)                                            # [Cin][4 Cout][2][2]
-            dw = G.view(Cin, 2, 2, Cout, 2, 2).permute(0, 3, 4, 1, 5, 2).reshape(Cin, Cout, 4, 4).contiguous()
+            with fork:  # beside the input-gradient conv, as in Conv2dFn.backward
+                if c:
+                    xp = torch.empty((B, Hp, Wp, Cin), dtype=torch.float32, device=x.device)
+                    check(lib.nps_circular_pad(ptr(x), ptr(xp), B, H, W, Cin, c, stream_ptr()), "circular_pad")
+                else:
+                    xp = x
+                G = wgrad(xp, dq, 2, 2)                                            # [Cin][4 Cout][2][2]
+                dw = G.view(Cin, 2, 2, Cout, 2, 2).permute(0, 3, 4, 1, 5, 2).reshape(Cin, Cout, 4, 4).contiguous()
+            fork.join(dw)
         if ctx.has_bias and ctx.needs_input_grad[3]:
             db = channel_sums(gout)
         return None, dx, dw, db

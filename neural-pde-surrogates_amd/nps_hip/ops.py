@@ -120,6 +120,11 @@ SIDE_FNO = os.environ.get("NPS_SIDE_FNO", "1") == "1"      # dev knob: the U-FNO
 SIDE_FNO_MAX_ELEMS = int(float(os.environ.get("NPS_SIDE_FNO_MAX_ELEMS", "6.4e7")))
 
 
+# dev knob NPS_SIDE_WGRAD=1: the training backward's weight gradients on a side stream (see
+# nps_hip.autograd.Conv2dFn.backward)
+SIDE_WGRAD = os.environ.get("NPS_SIDE_WGRAD", "0") == "1"
+
+
 def fno_fork(h: torch.Tensor) -> "Fork":
     """The U-FNO block's fork for its FNO layer (lane 1): on for small activations (see SIDE_FNO_MAX_ELEMS)."""
     return Fork(h, lane=1, on=SIDE_FNO and h.numel() <= SIDE_FNO_MAX_ELEMS)
