@@ -29,12 +29,13 @@ def _c(t):
 
 # ------------------------------------------------------------------------- weight gradient
 def wgrad(a: torch.Tensor, x: torch.Tensor, KH: int, KW: int, dil=1, pad=(0, 0), circ=0,
-          g: Optional[torch.Tensor] = None, a_range: Optional[torch.Tensor] = None) -> torch.Tensor:
+          g: Optional[torch.Tensor] = None, a_range: Optional[int] = None, x_range: Optional[int] = None
+          ) -> torch.Tensor:
     """G[m][n][KH*KW] (+)= sum_pix a[pix][m] * Xext[pix + tap*dil - pad][n].
 
     Split-fp16 MFMA (nps_conv2d_wgrad_x3) under ops.CONV_PRECISION == PREC_X3F16 for undilated square
     kernels up to 3x3 over channel counts that are multiples of 4 — a and x range-scaled from their
-    max |.| (a_range: a's range tag when the caller already has it) — else exact fp32 MFMA
+    max |.| (a_range / x_range: a's / x's range-tag pointers when the caller already has them) — else exact fp32 MFMA
     (nps_conv2d_wgrad)."""
     a, x = _c(a), _c(x)
     B, Ha, Wa, M = a.shape
@@ -64,7 +65,7 @@ def wgrad(a: torch.Tensor, x: torch.Tensor, KH: int, KW: int, dil=1, pad=(0, 0),
         # pass only for a tensor without one (ops.input_tag); a_range: a's tag pointer when the caller has it
         ops.reserve_tags(a.device, 2)
         ar = a_range if a_range is not None else _range_ptr(a)
-        xr = _range_ptr(x)
+        xr = x_range if x_range is not None else _range_ptr(x)
         ws = torch.empty(lib.nps_wgrad_x3_ws_floats(M, N, KH, KW), dtype=torch.float32, device=a.device)
         arith = "x3w"
 
@@ -329,7 +330,15 @@ class ConvTranspose2dFn(torch.autograd.Function):
         # the transposed conv's adjoint is a 4x4 stride-2 conv of gout: space-to-depth + 2x2 conv
         dq = ops.space_to_depth(gout, p, Hp + 1, Wp + 1)                    # [B][Hp+1][Wp+1][4 Cout]
         dx = dw = db = None
-        fork = ops.Fork(gout, on=ops.SIDE_WGRAD and ctx.needs_input_grad[1] and ctx.needs_input_grad[2])
+        fork = None
+        forked = ops.SIDE_WGRAD and ctx.needs_input_grad[1] and ctx.needs_input_grad[2]
+        dq_rng = None
+        if forked and ops.CONV_PRECISION == ops.PREC_X3F16:
+            # dq is read by both streams: its range tag is settled here, before the fork point (a tag computed
+            # lazily by one stream would be read by the other before its absmax ran)
+            ops.reserve_tags(gout.device, 3)
+            dq_rng = _range_ptr(dq)
+        fork = ops.Fork(gout, on=forked)
         if ctx.needs_input_grad[1]:
             w2 = w.detach().view(Cin, Cout, 2, 2, 2, 2).permute(0, 3, 5, 1, 2, 4).reshape(Cin, 4 * Cout, 2, 2)
             dxp = ops.conv2d([Src(dq)], (Hp + 1, Wp + 1), _pack_plain(w2.contiguous()), None, Cin, 2, 2,
@@ -346,7 +355,7 @@ class ConvTranspose2dFn(torch.autograd.Function):
                     check(lib.nps_circular_pad(ptr(x), ptr(xp), B, H, W, Cin, c, stream_ptr()), "circular_pad")
                 else:
                     xp = x
-                G = wgrad(xp, dq, 2, 2)                                            # [Cin][4 Cout][2][2]
+                G = wgrad(xp, dq, 2, 2, x_range=dq_rng)                            # [Cin][4 Cout][2][2]
                 dw = G.view(Cin, 2, 2, Cout, 2, 2).permute(0, 3, 4, 1, 5, 2).reshape(Cin, Cout, 4, 4).contiguous()
             fork.join(dw)
         if ctx.has_bias and ctx.needs_input_grad[3]:
