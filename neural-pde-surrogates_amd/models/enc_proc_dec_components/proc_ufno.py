@@ -66,7 +66,7 @@ class UFNO(nn.Module):
             srcs = [ops.Src(h)] + ([ops.Src(vb)] if vb is not None else [])
             # the FNO layer and the U-Net read the same h: the FNO layer runs on a side stream (ops.Fork,
             # lane 1) beside the U-Net, whose final conv joins it and adds its output
-            fork = ops.fno_fork(h)
+            fork = ops.fno_fork(h, settle=[s.t for s in srcs])
             with fork:
                 h_fno = fno.run(srcs)
             h = unet.run(h, vb, addend=h_fno, act_after=act, addend_fork=fork)
@@ -86,7 +86,7 @@ class UFNO(nn.Module):
         flat = lambda t: t.view(t.shape[0], D * H, W, t.shape[4])  # noqa: E731
         for fno, unet in zip(self.fno_layers, self.unet_layers):
             srcs = [ops.Src(flat(h))] + ([ops.Src(flat(vb))] if vb is not None else [])
-            fork = ops.fno_fork(h)  # the FNO layer beside the U-Net (as run())
+            fork = ops.fno_fork(h, settle=[s.t for s in srcs])  # the FNO layer beside the U-Net (as run())
             with fork:
                 h_fno = fno.run_bf16(srcs, D) if bf16 else fno.run(srcs, D=D)
             h = unet.run3d(h, vb, addend=h_fno.view(B, D, H, W, h_fno.shape[3]), act_after=act, addend_fork=fork)

@@ -262,17 +262,18 @@ class ResidualBlock(nn.Module):
             self.norm2 = nn.Identity()
         self.num_spatial_dims = num_spatial_dims
 
-    def _shortcut_fork(self, x0, H, W):
+    def _shortcut_fork(self, srcs, H, W):
         """An ops.Fork for the shortcut when conv1's launch leaves >= SIDE_MIN_IDLE of the CUs idle in its
         last round (the 258^2 convs: 1122 tiles on 256 CUs at B = 2), else None (no fork: cross-stream waits
         cost more than an exact-round launch leaves idle)."""
+        x0 = srcs[0].t
         if not (x0.is_cuda and ops.SIDE_STREAM):
             return None
         KH, KW, s, d, lo, hi, circ = self.conv1.geometry()
         Ho = (H + 2 * circ + lo[0] + hi[0] - d * (KH - 1) - 1) // s + 1
         Wo = (W + 2 * circ + lo[1] + hi[1] - d * (KW - 1) - 1) // s + 1
         idle = ops.last_round_idle(Ho, Wo, x0.shape[0], self.conv1.out_channels, x0.device)
-        return ops.Fork(x0) if idle >= ops.SIDE_MIN_IDLE else None
+        return ops.Fork(x0, settle=[s.t for s in srcs]) if idle >= ops.SIDE_MIN_IDLE else None
 
     def run(self, srcs, frame_hw):
         """srcs: the virtual NHWC input x (concat of slices).  Returns crop_Nd(h, sc) + sc."""
@@ -297,7 +298,7 @@ class ResidualBlock(nn.Module):
             # persistent grid leaves many CUs idle in its last round (the 258^2 convs), its work-groups
             # taking them; its moments buffer is taken before the fork point (no fill on the side stream)
             st2 = ops.new_stats(srcs[0].t.shape[0], srcs[0].t) if isinstance(self.norm1, nn.GroupNorm) else None
-            fork = self._shortcut_fork(srcs[0].t, H, W)
+            fork = self._shortcut_fork(srcs, H, W)
             if fork is None:
                 out = self.shortcut.run(srcs, (H, W), out_stats=st2)
         # conv1 adds norm2's moments of h1 as it stores it (ops.conv2d out_stats): no statistics pass

@@ -330,15 +330,9 @@ class ConvTranspose2dFn(torch.autograd.Function):
         # the transposed conv's adjoint is a 4x4 stride-2 conv of gout: space-to-depth + 2x2 conv
         dq = ops.space_to_depth(gout, p, Hp + 1, Wp + 1)                    # [B][Hp+1][Wp+1][4 Cout]
         dx = dw = db = None
-        fork = None
         forked = ops.SIDE_WGRAD and ctx.needs_input_grad[1] and ctx.needs_input_grad[2]
-        dq_rng = None
-        if forked and ops.CONV_PRECISION == ops.PREC_X3F16:
-            # dq is read by both streams: its range tag is settled here, before the fork point (a tag computed
-            # lazily by one stream would be read by the other before its absmax ran)
-            ops.reserve_tags(gout.device, 3)
-            dq_rng = _range_ptr(dq)
-        fork = ops.Fork(gout, on=forked)
+        # dq is read by both streams: its range tag is settled before the fork point (ops.Fork settle)
+        fork = ops.Fork(gout, on=forked, settle=[dq])
         if ctx.needs_input_grad[1]:
             w2 = w.detach().view(Cin, Cout, 2, 2, 2, 2).permute(0, 3, 5, 1, 2, 4).reshape(Cin, 4 * Cout, 2, 2)
             dxp = ops.conv2d([Src(dq)], (Hp + 1, Wp + 1), _pack_plain(w2.contiguous()), None, Cin, 2, 2,
@@ -355,7 +349,7 @@ class ConvTranspose2dFn(torch.autograd.Function):
                     check(lib.nps_circular_pad(ptr(x), ptr(xp), B, H, W, Cin, c, stream_ptr()), "circular_pad")
                 else:
                     xp = x
-                G = wgrad(xp, dq, 2, 2, x_range=dq_rng)                            # [Cin][4 Cout][2][2]
+                G = wgrad(xp, dq, 2, 2)                                            # [Cin][4 Cout][2][2]
                 dw = G.view(Cin, 2, 2, Cout, 2, 2).permute(0, 3, 4, 1, 5, 2).reshape(Cin, Cout, 4, 4).contiguous()
             fork.join(dw)
         if ctx.has_bias and ctx.needs_input_grad[3]:

@@ -125,9 +125,9 @@ SIDE_FNO_MAX_ELEMS = int(float(os.environ.get("NPS_SIDE_FNO_MAX_ELEMS", "6.4e7")
 SIDE_WGRAD = os.environ.get("NPS_SIDE_WGRAD", "0") == "1"
 
 
-def fno_fork(h: torch.Tensor) -> "Fork":
+def fno_fork(h: torch.Tensor, settle: Sequence[torch.Tensor] = ()) -> "Fork":
     """The U-FNO block's fork for its FNO layer (lane 1): on for small activations (see SIDE_FNO_MAX_ELEMS)."""
-    return Fork(h, lane=1, on=SIDE_FNO and h.numel() <= SIDE_FNO_MAX_ELEMS)
+    return Fork(h, lane=1, on=SIDE_FNO and h.numel() <= SIDE_FNO_MAX_ELEMS, settle=settle)
 # dev knob: the shortcut fork needs conv1's last round to leave at least this fraction of the CUs idle
 SIDE_MIN_IDLE = float(os.environ.get("NPS_SIDE_MIN_IDLE", "0.25"))
 _side_streams = {}
@@ -160,14 +160,21 @@ class Fork:
     `with f:` issues the enclosed launches on side stream `lane`, which starts at the fork point;
     `f.join(*outs)` makes the current stream wait for them and hands it the tensors they allocated.
     Moments buffers made inside (new_stats) are private zeros of the side stream; the tag arena fences a
-    wrap across all streams.  A no-op on the CPU or with NPS_SIDE_STREAM=0."""
+    wrap across all streams.  `settle`: fp32 tensors both streams may read as split-fp16 conv inputs — their
+    range tags are made live here, before the fork point, because a tag one stream computes lazily (absmax)
+    could be read by the other before that absmax ran.  A no-op on the CPU or with NPS_SIDE_STREAM=0."""
 
-    def __init__(self, like: torch.Tensor, lane: int = 0, on: bool = True):
+    def __init__(self, like: torch.Tensor, lane: int = 0, on: bool = True, settle: Sequence[torch.Tensor] = ()):
         d = like.device
         self.on = on and SIDE_STREAM and d.type == "cuda"
         self.done = None
         if not self.on:
             return
+        if USE_IN_TAGS and CONV_PRECISION == PREC_X3F16:
+            ts = [t for t in settle if t is not None and t.dtype == torch.float32]
+            reserve_tags(d, len(ts))
+            for t in ts:
+                input_tag(t)
         idx = d.index if d.index is not None else torch.cuda.current_device()
         key = (idx, lane)
         self.side = _side_streams.get(key)
