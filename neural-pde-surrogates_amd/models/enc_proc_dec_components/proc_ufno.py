@@ -86,7 +86,9 @@ class UFNO(nn.Module):
         flat = lambda t: t.view(t.shape[0], D * H, W, t.shape[4])  # noqa: E731
         for fno, unet in zip(self.fno_layers, self.unet_layers):
             srcs = [ops.Src(flat(h))] + ([ops.Src(flat(vb))] if vb is not None else [])
-            fork = ops.fno_fork(h, settle=[s.t for s in srcs])  # the FNO layer beside the U-Net (as run())
+            # the FNO layer beside the U-Net (as run(); at every size: C5 at B = 8 +1 %,
+            # profiles/r4/experiments/side_stream_forks_ab.txt)
+            fork = ops.Fork(h, lane=1, on=ops.SIDE_FNO, settle=[s.t for s in srcs])
             with fork:
                 h_fno = fno.run_bf16(srcs, D) if bf16 else fno.run(srcs, D=D)
             h = unet.run3d(h, vb, addend=h_fno.view(B, D, H, W, h_fno.shape[3]), act_after=act, addend_fork=fork)

@@ -115,8 +115,8 @@ _forked = False  # set by the first Fork that runs launches on a side stream
 # 4.4 rounds).  Each lane is one stream per device (one hardware queue).  dev knob NPS_SIDE_STREAM=0: off.
 SIDE_STREAM = os.environ.get("NPS_SIDE_STREAM", "1") == "1"
 SIDE_FNO = os.environ.get("NPS_SIDE_FNO", "1") == "1"      # dev knob: the U-FNO block's FNO layer fork
-# ... for activations of at most this many elements (B=2 C3: 25 M; at B=16, 201 M, the U-Net's launches keep
-# the CUs busy and the FNO layer's kernels only stretch them: +0.4 %, profiles/r4/experiments/side_stream_*)
+# ... for 2-D activations of at most this many elements (B=2 C3: 25 M; at B=16, 201 M, the U-Net's launches
+# keep the CUs busy: within noise, profiles/r4/experiments/side_stream_*; the 3-D U-FNO forks at every size)
 SIDE_FNO_MAX_ELEMS = int(float(os.environ.get("NPS_SIDE_FNO_MAX_ELEMS", "6.4e7")))
 
 
