@@ -319,6 +319,9 @@ int nps_conv2d_wgrad(const nps_wgrad_t* p, void* stream);
  * tap-major, then fold into g).  Same geometry and += semantics as nps_conv2d_wgrad. */
 size_t nps_wgrad_x3_ws_floats(int M, int N, int KH, int KW);
 int nps_conv2d_wgrad_x3(const nps_wgrad_t* p, const float* a_range, const float* x_range, float* ws, void* stream);
+/* The same, storing G = the weight gradient (g need not be zeroed beforehand) instead of adding to it. */
+int nps_conv2d_wgrad_x3_set(const nps_wgrad_t* p, const float* a_range, const float* x_range, float* ws,
+                            void* stream);
 /* out[c] += sum over `rows` rows of x[row][c] (conv bias gradients; parameter-partial reductions) */
 int nps_channel_sums(const float* x, long rows, int C, float* out, void* stream);
 

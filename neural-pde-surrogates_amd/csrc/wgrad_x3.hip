@@ -676,13 +676,14 @@ __global__ __launch_bounds__(512) void wgrad2_wide_kernel(const nps_wgrad_t p, c
     }
 }
 
-// G[m][n][tap] += W[tap][m][n]
-__global__ void wgrad_fold_kernel(const float* __restrict__ w, float* __restrict__ g, int MN, int nt) {
+// G[m][n][tap] += W[tap][m][n] (acc), or = (nps_conv2d_wgrad_x3_set: G need not be zeroed first)
+__global__ void wgrad_fold_kernel(const float* __restrict__ w, float* __restrict__ g, int MN, int nt, int acc) {
     const long total = (long)MN * nt;
     for (long o = (long)blockIdx.x * blockDim.x + threadIdx.x; o < total; o += (long)gridDim.x * blockDim.x) {
         const long mn = o / nt;
         const int t = (int)(o - mn * nt);
-        g[o] += w[(size_t)t * MN + mn];
+        const float v = w[(size_t)t * MN + mn];
+        g[o] = acc ? g[o] + v : v;
     }
 }
 
@@ -693,7 +694,8 @@ const int g_wx_remap = [] {
 }();
 
 template <int KH, int KW>
-int launch_wgrad_x3(const nps_wgrad_t& p, const float* ar, const float* xr, float* ws, hipStream_t s) {
+int launch_wgrad_x3(const nps_wgrad_t& p, const float* ar, const float* xr, float* ws, hipStream_t s,
+                       int acc) {
     const long tiles_x = (p.Wa + WX_TW - 1) / WX_TW, tiles_y = (p.Ha + WX_TH - 1) / WX_TH;
     const long ntiles = (long)p.B * tiles_y * tiles_x;
     NPS_CHECK_ARG(ntiles < (1L << 30), "conv2d_wgrad_x3: too many tiles");
@@ -728,13 +730,14 @@ int launch_wgrad_x3(const nps_wgrad_t& p, const float* ar, const float* xr, floa
     NPS_CHECK_LAUNCH("conv2d_wgrad_x3");
     const long total = (long)MN * KH * KW;
     const long nb = (total + 255) / 256;
-    wgrad_fold_kernel<<<(unsigned)(nb < 2048 ? nb : 2048), 256, 0, s>>>(ws, p.g, (int)MN, KH * KW);
+    wgrad_fold_kernel<<<(unsigned)(nb < 2048 ? nb : 2048), 256, 0, s>>>(ws, p.g, (int)MN, KH * KW, acc);
     NPS_CHECK_LAUNCH("conv2d_wgrad_x3 (fold)");
     return 0;
 }
 
 // 1x1 weight gradient on wgrad1_wide_kernel (dy and x on the same pixels: no padding / circular extension)
-int launch_wgrad1_wide(const nps_wgrad_t& p, const float* ar, const float* xr, float* ws, hipStream_t s) {
+int launch_wgrad1_wide(const nps_wgrad_t& p, const float* ar, const float* xr, float* ws, hipStream_t s,
+                       int acc) {
     const long npix = (long)p.B * p.Ha * p.Wa;
     const long ntiles = (npix + W1_TP - 1) / W1_TP;
     NPS_CHECK_ARG(ntiles < (1L << 30), "conv2d_wgrad_x3 (1x1): too many tiles");
@@ -765,13 +768,14 @@ int launch_wgrad1_wide(const nps_wgrad_t& p, const float* ar, const float* xr, f
                                                                        (int)base, remap);
     NPS_CHECK_LAUNCH("conv2d_wgrad_x3 (1x1 wide)");
     const long nb = ((long)MN + 255) / 256;
-    wgrad_fold_kernel<<<(unsigned)(nb < 2048 ? nb : 2048), 256, 0, s>>>(ws, p.g, (int)MN, 1);
+    wgrad_fold_kernel<<<(unsigned)(nb < 2048 ? nb : 2048), 256, 0, s>>>(ws, p.g, (int)MN, 1, acc);
     NPS_CHECK_LAUNCH("conv2d_wgrad_x3 (fold)");
     return 0;
 }
 
 // 2x2 weight gradient on wgrad2_wide_kernel (128 x 128 work-group tiles)
-int launch_wgrad2_wide(const nps_wgrad_t& p, const float* ar, const float* xr, float* ws, hipStream_t s) {
+int launch_wgrad2_wide(const nps_wgrad_t& p, const float* ar, const float* xr, float* ws, hipStream_t s,
+                       int acc) {
     const long tiles_x = (p.Wa + W2_TW - 1) / W2_TW, tiles_y = (p.Ha + W2_TH - 1) / W2_TH;
     const long ntiles = (long)p.B * tiles_y * tiles_x;
     NPS_CHECK_ARG(ntiles < (1L << 30), "conv2d_wgrad_x3 (2x2): too many tiles");
@@ -802,7 +806,7 @@ int launch_wgrad2_wide(const nps_wgrad_t& p, const float* ar, const float* xr, f
                                                                        remap);
     NPS_CHECK_LAUNCH("conv2d_wgrad_x3 (2x2 wide)");
     const long nb = ((long)MN * 4 + 255) / 256;
-    wgrad_fold_kernel<<<(unsigned)(nb < 2048 ? nb : 2048), 256, 0, s>>>(ws, p.g, (int)MN, 4);
+    wgrad_fold_kernel<<<(unsigned)(nb < 2048 ? nb : 2048), 256, 0, s>>>(ws, p.g, (int)MN, 4, acc);
     NPS_CHECK_LAUNCH("conv2d_wgrad_x3 (fold)");
     return 0;
 }
@@ -822,8 +826,9 @@ const int g_wx_wide2 = [] {
 
 extern "C" size_t nps_wgrad_x3_ws_floats(int M, int N, int KH, int KW) { return (size_t)M * N * KH * KW; }
 
-extern "C" int nps_conv2d_wgrad_x3(const nps_wgrad_t* pp, const float* a_range, const float* x_range, float* ws,
-                                   void* stream) {
+namespace {
+int wgrad_x3_dispatch(const nps_wgrad_t* pp, const float* a_range, const float* x_range, float* ws, void* stream,
+                      int acc) {
     NPS_CHECK_ARG(pp != nullptr && a_range != nullptr && x_range != nullptr && ws != nullptr, "conv2d_wgrad_x3: null");
     const nps_wgrad_t& p = *pp;
     NPS_CHECK_ARG(p.a && p.x && p.g && p.B > 0 && p.Ha > 0 && p.Wa > 0 && p.M > 0 && p.Hx > 0 && p.Wx > 0 && p.N > 0,
@@ -837,12 +842,23 @@ extern "C" int nps_conv2d_wgrad_x3(const nps_wgrad_t* pp, const float* a_range, 
     switch (p.KH) {
         case 1:
             if (g_wx_wide1 && p.pad_y == 0 && p.pad_x == 0 && p.circ == 0 && p.Ha == p.Hx && p.Wa == p.Wx)
-                return launch_wgrad1_wide(p, a_range, x_range, ws, s);
-            return launch_wgrad_x3<1, 1>(p, a_range, x_range, ws, s);
+                return launch_wgrad1_wide(p, a_range, x_range, ws, s, acc);
+            return launch_wgrad_x3<1, 1>(p, a_range, x_range, ws, s, acc);
         case 2:
             // (the wide kernel needs M, N > 64 to beat the 64 x 64 tiles)
-            if (g_wx_wide2 && p.M > 64 && p.N > 64) return launch_wgrad2_wide(p, a_range, x_range, ws, s);
-            return launch_wgrad_x3<2, 2>(p, a_range, x_range, ws, s);
-        default: return launch_wgrad_x3<3, 3>(p, a_range, x_range, ws, s);
+            if (g_wx_wide2 && p.M > 64 && p.N > 64) return launch_wgrad2_wide(p, a_range, x_range, ws, s, acc);
+            return launch_wgrad_x3<2, 2>(p, a_range, x_range, ws, s, acc);
+        default: return launch_wgrad_x3<3, 3>(p, a_range, x_range, ws, s, acc);
     }
+}
+}  // namespace
+
+extern "C" int nps_conv2d_wgrad_x3(const nps_wgrad_t* pp, const float* a_range, const float* x_range, float* ws,
+                                   void* stream) {
+    return wgrad_x3_dispatch(pp, a_range, x_range, ws, stream, 1);
+}
+
+extern "C" int nps_conv2d_wgrad_x3_set(const nps_wgrad_t* pp, const float* a_range, const float* x_range, float* ws,
+                                       void* stream) {
+    return wgrad_x3_dispatch(pp, a_range, x_range, ws, stream, 0);
 }

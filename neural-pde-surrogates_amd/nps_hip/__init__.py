@@ -119,6 +119,7 @@ _SIGS = {
     "nps_conv2d_wgrad": (_i, [ctypes.POINTER(WgradArgs), _vp]),
     "nps_wgrad_x3_ws_floats": (_sz, [_i, _i, _i, _i]),
     "nps_conv2d_wgrad_x3": (_i, [ctypes.POINTER(WgradArgs), _vp, _vp, _vp, _vp]),
+    "nps_conv2d_wgrad_x3_set": (_i, [ctypes.POINTER(WgradArgs), _vp, _vp, _vp, _vp]),
     "nps_channel_sums": (_i, [_vp, _l, _i, _vp, _vp]),
     "nps_frame_pack_bwd": (_i, [ctypes.POINTER(Conv2dArgs), _vp, ctypes.POINTER(ctypes.c_void_p), _vp, _vp, _vp, _vp]),
     "nps_frame_pack_bwd_tagged": (_i, [ctypes.POINTER(Conv2dArgs), _vp, ctypes.POINTER(ctypes.c_void_p),

@@ -40,8 +40,10 @@ def wgrad(a: torch.Tensor, x: torch.Tensor, KH: int, KW: int, dil=1, pad=(0, 0),
     a, x = _c(a), _c(x)
     B, Ha, Wa, M = a.shape
     _, Hx, Wx, N = x.shape
+    x3 = ops.CONV_PRECISION == ops.PREC_X3F16 and KH == KW and KH <= 3 and dil == 1
+    store = g is None and x3 and M % 4 == 0 and N % 4 == 0  # the split-fp16 fold stores g: no zero-fill
     if g is None:
-        g = torch.zeros((M, N, KH, KW), dtype=torch.float32, device=a.device)
+        g = (torch.empty if store else torch.zeros)((M, N, KH, KW), dtype=torch.float32, device=a.device)
     if (ops.CONV_PRECISION == ops.PREC_X3F16 and KH == KW and KH <= 3 and dil == 1 and (M % 4 or N % 4)):
         # channel counts off the split-fp16 kernel's 4-channel quads (the encoder's 81-channel input): zero-pad
         # to a multiple of 4, run the split-fp16 weight gradient and add the real channels' block into g
@@ -69,8 +71,10 @@ def wgrad(a: torch.Tensor, x: torch.Tensor, KH: int, KW: int, dil=1, pad=(0, 0),
         ws = torch.empty(lib.nps_wgrad_x3_ws_floats(M, N, KH, KW), dtype=torch.float32, device=a.device)
         arith = "x3w"
 
+        fn = lib.nps_conv2d_wgrad_x3_set if store else lib.nps_conv2d_wgrad_x3
+
         def launch():
-            check(lib.nps_conv2d_wgrad_x3(ctypes.byref(p), ar, xr, ptr(ws), stream_ptr()), "conv2d_wgrad_x3")
+            check(fn(ctypes.byref(p), ar, xr, ptr(ws), stream_ptr()), "conv2d_wgrad_x3")
     else:
         arith = "f32w"
 
