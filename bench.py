@@ -14,7 +14,10 @@ python bench.py [--gpus N --steps K --warmup W]
     launch from the committed profiles/pmc_traffic.json (tools/pmc_traffic.sh; FETCH_SIZE scaled per access
     shape as calibrated by tools/calib/pmc_calib.hip: x1 for the conv producers' 64-B reads);
   * cpu_baseline: the CPU oracle (oracle/, the reference restated in fp32 PyTorch-CPU) on a bounded
-    sample (2 model calls at B=2) on rank 0 only, with the GPU-vs-CPU rel-L2 of that sample.
+    sample (2 model calls at B=2, after one untimed warm-up call) on rank 0 only, with the GPU-vs-CPU
+    rel-L2 of that sample.
+  * --gpus N > 1 without torchrun: this process starts the N ranks itself (torch.distributed.run children,
+    launch_ranks) before any GPU call; under a launcher, WORLD_SIZE must equal --gpus.
 """
 import argparse
 import json
@@ -26,6 +29,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 for _p in (ROOT, os.path.join(ROOT, "neural-pde-surrogates_amd")):
     if _p not in sys.path:
         sys.path.insert(0, _p)
+
+# bench.py opens its own process group (init_ranks); the mirror packages' torchrun bring-up
+# (common/launch.py) must not open one first when run_fno3d imports models before init_ranks
+os.environ.setdefault("NPS_AUTO_DIST", "0")
 
 import torch  # noqa: E402
 from torch import nn  # noqa: E402
@@ -176,14 +183,42 @@ def shard_bounds(global_batch, world, rank):
     return rank * per, (rank + 1) * per
 
 
-def init_ranks():
+def launch_ranks(argv, n):
+    """`bench.py --gpus N` (N > 1) without a launcher: start N ranks, one process per GPU, as
+    `torch.distributed.run --nproc-per-node N` children on a free 127.0.0.1 port, and return their exit
+    status.  This parent never touches the GPU (no HIP call before or after the children run); each child
+    binds its LOCAL_RANK's card and opens the RCCL group in init_ranks."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+    return subprocess.call(cmd)
+
+
+def check_world(gpus):
+    """The launcher's world size must be the --gpus the line will report."""
+    env = os.environ.get("WORLD_SIZE")
+    if env is not None and int(env) != gpus:
+        raise SystemExit(f"bench.py: --gpus {gpus} but the launcher started WORLD_SIZE={env} ranks")
+
+
+def init_ranks(check=False):
     """(world, rank, device) of this process: one process per GPU (torchrun env), RCCL process group.
 
     NPS_BENCH_REHEARSAL=1 (dev only, never a reported number): every rank on cuda:0 over gloo, so the
-    N > 1 code path (sharding, barriers, max-over-ranks) can run on a one-GPU box."""
+    N > 1 code path (sharding, barriers, max-over-ranks) can run on a one-GPU box.  check=True
+    (--launch-check): gloo on the host, no GPU call at all."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if check:
+        if world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+        return world, rank, torch.device("cpu")
     if world > 1:
         import torch.distributed as dist
         if os.environ.get("NPS_BENCH_REHEARSAL") == "1":
@@ -194,6 +229,26 @@ def init_ranks():
             torch.cuda.set_device(local_rank)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     return world, rank, torch.device("cuda", local_rank)
+
+
+def launch_check(args):
+    """--launch-check: bring the ranks up exactly as a measured run would (launcher, world size, rank ->
+    shard), print what the process group is and every rank's shard of the mode's global batch, touch no
+    GPU.  Used by tests/test_bench_launch.py on the CPU."""
+    world, rank, _ = init_ranks(check=True)
+    gb = args.global_batch if not (args.model in ("fno3d", "ufno3d") and args.global_batch == 16) else 8
+    lo, hi = shard_bounds(gb, world, rank)
+    shards = [[lo, hi]]
+    if world > 1:
+        import torch.distributed as dist
+        shards = [None] * world
+        dist.all_gather_object(shards, [lo, hi])
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "mode": args.mode, "model": args.model, "n_gpus": world,
+                          "gpus_arg": args.gpus, "global_batch": gb, "shards": shards,
+                          "dist": dist_info(world)}), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
 
 
 def max_over_ranks(elapsed, device):
@@ -241,6 +296,8 @@ def cpu_baseline(model, ocfg, opde, res, num_c, calls=2, B=2):
     om = oracle.build_oracle_model(ocfg, opde, {k: v.detach().cpu() for k, v in model.state_dict().items()})
     u, cond, pos, sc = twophase_batch(B, num_c, 25 * (calls + 1), res, res, seed=99, obstacle="disc")
     tw = 25
+    with torch.no_grad():  # one untimed call: allocator / thread-pool warm-up, as the GPU legs get
+        om(u[:, :, :tw], cond=cond, pos=pos, spatial_cond=sc)
     t0 = time.perf_counter()
     with torch.no_grad():
         losses, preds = oracle.simulate(om, u, cond, pos, sc, tw, 25 * (calls + 1))
@@ -279,7 +336,17 @@ def main():
     ap.add_argument("--mode", default="rollout", choices=["rollout", "train"],
                     help="rollout = the headline metric; train = pushforward train_step + backward + RCCL "
                          "all-reduce + Adam (samples/s)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="bring the N ranks up (launcher, process group, shards), print them and exit; no GPU")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # one process per GPU: this parent starts the N ranks and only waits for them
+        raise SystemExit(launch_ranks(sys.argv[1:], args.gpus))
+    check_world(args.gpus)
+    if args.launch_check:
+        return launch_check(args)
     if args.mode == "train":
         return run_train(args)
     if args.model in ("fno3d", "ufno3d"):

@@ -103,8 +103,10 @@ _KEEP = []
 
 
 def _keep(t):
-    """Hold a one-off range tensor until the next backward launch has been enqueued (stream-ordered reuse of
-    the caching allocator makes an early free safe; the list only bounds its lifetime to a few launches)."""
+    """Hold a one-off range tensor (NPS_RANGE_TAGS without input tags) for the launches that read its pointer.
+    The invariant that makes this safe: those launches are enqueued on the stream the tensor was allocated on
+    (or on a side stream that is joined before the caller returns, before 8 more _keep calls can drop it), so the
+    caching allocator's stream-ordered reuse cannot hand its memory out before they ran."""
     _KEEP.append(t)
     del _KEEP[:-8]
     return t
@@ -259,7 +261,10 @@ class Conv2dFn(torch.autograd.Function):
         Cin = w.shape[1]
         dx = dw = db = rng = None
         if ops.CONV_PRECISION == ops.PREC_X3F16 and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2]):
-            ops.reserve_tags(gy.device, 3)
+            # rng is a raw pointer into the tag arena, passed to every launch below: reserve the tags of the
+            # WHOLE backward first (gy's tag; 2 per input-gradient conv — one, or four stride-2 phases; 2 for
+            # the weight gradient), so no later reserve can wrap the arena (zeroing gy's tag) while rng is live
+            ops.reserve_tags(gy.device, 1 + (2 if s == 1 else 8) + 2)
             rng = _range_ptr(gy)  # gradients: any magnitude (its tag, or one absmax pass shared by dx and dw)
         # the weight gradient reads only gy and x: it runs on a side stream beside the input-gradient conv(s)
         # (ops.Fork), each filling the CUs the other's last round leaves idle; joined before returning

@@ -269,11 +269,16 @@ def share_tag(dst: torch.Tensor, src: torch.Tensor) -> torch.Tensor:
 
 
 def input_tag(t: torch.Tensor) -> int:
-    """Tag pointer bounding |t| for a split-fp16 conv reading t (nps_absmax when t has no live tag)."""
+    """Tag pointer bounding |t| for a split-fp16 conv reading t (nps_absmax when t has no live tag).
+
+    On a side stream (inside a Fork) the fresh tag is PRIVATE, not attached to t: t may be an input both
+    streams read (its settled tag died in an arena wrap inside the fork), and a tag attached here would be
+    raised by an absmax queued only on the side stream, which a later main-stream launch reading t could
+    see before that absmax ran.  The main stream measures t itself."""
     tag = tag_of(t)
     if tag is not None:
         return tag.ptr
-    p = new_tag(t)
+    p = _arena(t.device).alloc().ptr if _side_depth > 0 else new_tag(t)
     check(lib.nps_absmax(ptr(t), t.numel(), p, stream_ptr()), "absmax (input tag)")
     return p
 

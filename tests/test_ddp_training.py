@@ -134,7 +134,11 @@ def test_ddp_train_step_equals_one_process_global_batch(tmp_path, mode):
         for p in procs:
             p.join(timeout=60)
     assert all(p.exitcode == 0 for p in procs)
-    # 1 process, concatenated global batch, rank 0's initial parameters and Python RNG state
+    _check_against_one_process(res)
+
+
+def _one_process():
+    """1 process, concatenated global batch, rank 0's initial parameters and Python RNG state."""
     _paths()
     torch.manual_seed(100)
     random.seed(1000)
@@ -142,8 +146,11 @@ def test_ddp_train_step_equals_one_process_global_batch(tmp_path, mode):
     tr = _trainer(model, GLOBAL_B)
     assert tr.grad_sync is None
     v = _global_batch(5, seed=3)
-    want = _run(tr, [_global_batch(), _global_batch(seed=2)], [_shard(v, 0, 2), _shard(v, 2, 4), _shard(v, 4, 5)])
-    w_loss, w_grads, w_params, w_val, w_metrics = want
+    return _run(tr, [_global_batch(), _global_batch(seed=2)], [_shard(v, 0, 2), _shard(v, 2, 4), _shard(v, 4, 5)])
+
+
+def _check_against_one_process(res):
+    w_loss, w_grads, w_params, w_val, w_metrics = _one_process()
     for rank, (loss, grads, params, val, metrics) in res:
         assert loss == pytest.approx(w_loss, rel=1e-6)
         for k in w_grads:
@@ -171,3 +178,44 @@ def test_global_sqrt_loss_single_process_is_sqrt():
     m = (x.detach() ** 2).mean()
     torch.testing.assert_close(out.detach(), torch.sqrt(m).float())
     torch.testing.assert_close(x.grad, x.detach() / (7 * torch.sqrt(m)))
+
+
+def test_torchrun_train_py_without_wrapper(tmp_path):
+    """An unchanged train.py under `torch.distributed.run --nproc-per-node 2`: no init_process_group, no
+    sitecustomize — importing the mirror's data / models / trainers opens the group from torchrun's
+    environment (common/launch.py), and the 2-rank run equals the 1-process global-batch run."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "NPS_AUTO_DIST"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port),
+                        os.path.join(ROOT, "tests", "ddp_torchrun_scenario.py"), str(tmp_path)],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    res = []
+    for rank in range(2):
+        d = torch.load(tmp_path / f"rank{rank}.pt", weights_only=False)
+        assert d["rank"] == rank and d["world"] == 2
+        res.append((rank, d["res"]))
+    _check_against_one_process(res)
+
+
+def test_launch_env_parsing(monkeypatch):
+    _paths()
+    from common import launch
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR"):
+        monkeypatch.delenv(k, raising=False)
+    assert launch.torchrun_env() is None
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    assert launch.torchrun_env() is None
+    monkeypatch.setenv("WORLD_SIZE", "4")
+    monkeypatch.setenv("RANK", "3")
+    assert launch.torchrun_env() is None            # no rendezvous address: not a launcher's env
+    monkeypatch.setenv("MASTER_ADDR", "127.0.0.1")
+    monkeypatch.setenv("LOCAL_RANK", "1")
+    assert launch.torchrun_env() == (4, 3, 1)

@@ -204,3 +204,31 @@ def test_tag_invalidated_by_torch_inplace_write():
     y = m.run([ops.Src(xd)], (20, 24))
     ref = _ref_conv(ops.nhwc_to_nchw(xd).cpu(), m.weight.detach().cpu(), m.bias.detach().cpu(), 1, 1, 0, "zeros")
     assert rel_l2(ops.nhwc_to_nchw(y).cpu(), ref) < TOL
+
+
+@pytest.mark.parametrize("stride,cin,cout,pad", [(1, 64, 64, 1), (2, 12, 40, 1)])
+def test_tag_arena_wrap_inside_conv_backward_keeps_gradient_range(stride, cin, cout, pad):
+    """the conv backward passes gy's range-tag pointer to the input-gradient conv(s) and to
+    the weight gradient; a reserve between them used to wrap the arena (zeroing gy's tag), so the split-fp16
+    dgrad / wgrad of a tiny gradient ran unscaled and flushed to zero.  The backward now reserves every tag it
+    needs before taking the pointer.  The wrap point is swept over every position inside one backward."""
+    from models.common import Conv2d
+    from nps_hip import ops
+    torch.manual_seed(3)
+    m = Conv2d(cin, cout, 3, stride=stride, padding=pad)
+    x = torch.randn(2, cin, 20, 22)
+    xr = x.clone().double().requires_grad_(True)
+    w = m.weight.detach().double().requires_grad_(True)
+    ref = F.conv2d(xr, w, m.bias.detach().double(), stride=stride, padding=pad)
+    g = torch.randn_like(ref) * 1e-8             # far below fp16's subnormals unless range-scaled
+    ref.backward(g)
+    md = m.to(DEV)
+    for left in range(1, 14):
+        xd = x.to(DEV).requires_grad_(True)
+        md.weight.grad = None
+        y = md(xd)
+        ar = ops._arena(y.device)
+        ar.next = ops._ARENA_TAGS - left
+        y.backward(g.float().to(DEV))
+        assert rel_l2(xd.grad, xr.grad) < TOL, left
+        assert rel_l2(md.weight.grad, w.grad) < TOL, left
