@@ -53,7 +53,7 @@ __host__ __device__ constexpr int x3_patch_px_max(int ntaps, int tile_px) {
                        // 3 no producer units, 4 = 1 + 2
 #endif
 #ifndef NPS_X3_ABL
-#define NPS_X3_ABL 0  // dev ablations of the 3x3 main loop (tools/x3_abl.sh); 0 in every shipped build
+#define NPS_X3_ABL 0  // dev ablations of the 3x3 main loop; 0 in every shipped build
 #endif
 // Producer slot -> (patch pixel, channel quad).  REMAP: the 16 lanes of one ds_write_b64 group take
 // pixels {0, 2, 4, 6} (lanes 16-31: {1, 3, 5, 7}) of a run of 8, whose 32-B [hi] / [lo] runs at the 80-B
@@ -244,7 +244,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
 
     // static priority for the producer half (MI355X_MICROARCH 'Two waves per SIMD' item 4): they win the
     // VALU arbitration against their SIMD partner's MFMA stream; same-box A/B: 3x3 class -1.7 % per call
-    // (tools/ab_prio.sh; NPS_X3_PRIO=0 / 2: none / the consumers instead)
+    // (NPS_X3_PRIO=0 / 2: none / the consumers instead)
 #if NPS_X3_PRIO == 1
     if (wave >= 4) __builtin_amdgcn_s_setprio(1);
 #elif NPS_X3_PRIO == 2

@@ -1,20 +1,24 @@
 #!/bin/bash
-# Round-4 GPU pass (gpurun): parity suite, C3 bench + rocprof, B=2 line, training lines (B=2, B=16) + rocprof of
-# the B=16 step, C5 (ufno3d bf16) line + rocprof, N=2 training rehearsal.  Outputs: gpurun_out/${TAG}_*.
-# usage: tools/r4_full.sh TAG [steps...]   steps: tests sel($TESTSEL) pmc bench prof b2 b2prof train trainprof tb2prof c5 c5prof reh (default: all)
+# One GPU-box pass (gpurun): parity suite, C3 bench + rocprof, B=2 line, training lines + rocprof, C5 line +
+# rocprof, and the N=2 rehearsals of `bench.py --gpus 2` (the driver's own command form; ranks share cuda:0
+# over gloo: NPS_BENCH_REHEARSAL=1, never a reported number).  Outputs: gpurun_out/${TAG}_*.
+# usage: tools/gpu_pass.sh TAG [steps...]
+#   steps: tests sel($TESTSEL) pmc bench prof b2 b2prof train trainprof tb2prof c5 c5prof reh rehroll smoke
 set -o pipefail
-TAG=${1:-r4full}; shift
-STEPS="${@:-tests bench prof b2 train trainprof c5 c5prof reh}"
+TAG=${1:-r5}; shift
+STEPS="${@:-tests bench prof b2 train c5 reh}"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 O=gpurun_out/$TAG
 for s in $STEPS; do
   case $s in
-    tests) timeout -k 10 600 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread > ${O}_tests.log 2>&1 \
+    tests) timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread > ${O}_tests.log 2>&1 \
              || { echo "tests failed"; tail -30 ${O}_tests.log; exit 1; }; tail -2 ${O}_tests.log ;;
-    sel)   timeout -k 10 400 python -u -m pytest $TESTSEL -m gpu -q -x --timeout 200 --timeout-method thread > ${O}_sel.log 2>&1 \
+    sel)   timeout -k 10 600 python -u -m pytest $TESTSEL -m gpu -q -x --timeout 200 --timeout-method thread > ${O}_sel.log 2>&1 \
              || { echo "selected tests failed"; tail -30 ${O}_sel.log; exit 1; }; tail -2 ${O}_sel.log ;;
-    pmc)   timeout -k 10 900 bash tools/pmc_traffic.sh > ${O}_pmc.log 2>&1 || { echo "pmc failed"; tail -20 ${O}_pmc.log; exit 1; }; cp gpurun_out/pmc_traffic.json ${O}_pmc_traffic.json && cp gpurun_out/pmc_traffic.json profiles/pmc_traffic.json ;;
+    smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > ${O}_smoke.log 2>&1 \
+             || { echo "smoke failed"; tail -20 ${O}_smoke.log; exit 1; }; tail -3 ${O}_smoke.log ;;
+    pmc)   timeout -k 10 900 bash tools/pmc_traffic.sh > ${O}_pmc.log 2>&1 || { echo "pmc failed"; tail -20 ${O}_pmc.log; exit 1; }; cp gpurun_out/pmc_traffic.json ${O}_pmc_traffic.json ;;
     bench) timeout -k 10 400 python -u bench.py > ${O}_bench.json 2> ${O}_bench.err || { echo "bench failed"; tail -20 ${O}_bench.err; exit 1; }; tail -c 600 ${O}_bench.json ;;
     prof)  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d ${O}_prof -o run -- python3 bench.py --steps 3 --warmup 1 --cpu-calls 0 \
              > ${O}_prof.log 2>&1 || { echo "prof failed"; tail -20 ${O}_prof.log; exit 1; } ;;
@@ -30,9 +34,10 @@ for s in $STEPS; do
     c5)    timeout -k 10 400 python -u bench.py --model ufno3d --dtype bf16 > ${O}_c5.json 2> ${O}_c5.err || { echo "c5 failed"; tail -20 ${O}_c5.err; exit 1; }; tail -c 300 ${O}_c5.json ;;
     c5prof) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d ${O}_c5prof -o run -- python3 bench.py --model ufno3d --dtype bf16 --steps 3 --warmup 1 --cpu-calls 0 \
              > ${O}_c5prof.log 2>&1 || { echo "c5 prof failed"; tail -20 ${O}_c5prof.log; exit 1; } ;;
-    reh)   NPS_BENCH_REHEARSAL=1 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 \
-             bench.py --mode train --gpus 2 --steps 3 --warmup 1 --global-batch 4 --cpu-calls 0 > ${O}_reh_train.json 2> ${O}_reh_train.err \
-             || { echo "rehearsal failed"; tail -20 ${O}_reh_train.err; exit 1; }; tail -c 400 ${O}_reh_train.json ;;
+    reh)   NPS_BENCH_REHEARSAL=1 timeout -k 10 400 python3 bench.py --gpus 2 --mode train --steps 3 --warmup 1 --global-batch 4 --cpu-calls 0 \
+             > ${O}_reh_train.json 2> ${O}_reh_train.err || { echo "train rehearsal failed"; tail -20 ${O}_reh_train.err; exit 1; }; tail -c 400 ${O}_reh_train.json ;;
+    rehroll) NPS_BENCH_REHEARSAL=1 timeout -k 10 400 python3 bench.py --gpus 2 --steps 5 --warmup 1 --cpu-calls 0 \
+             > ${O}_reh_roll.json 2> ${O}_reh_roll.err || { echo "rollout rehearsal failed"; tail -20 ${O}_reh_roll.err; exit 1; }; tail -c 400 ${O}_reh_roll.json ;;
   esac
   echo "step $s ok"
 done
