@@ -272,6 +272,7 @@ inline bool x3_sources_aligned(const nps_conv2d_t& a) {
 // no register-direct epilogue, whose register demand spilled them.
 inline bool x3_wide_eligible(const nps_conv2d_t& a) {
     const int nt = a.KH * a.KW;
+    // (the tile's 6 32-channel weight blocks always exist: packed_ncb pads Cout to a multiple of 192)
     return (nt == 4 || nt == 9) && a.Cout > 128 && a.Cout <= 192 && (a.Cout & 31) == 0 && a.dil == 1 &&
            a.stride == 1 && !a.lattice && !a.out_nchw && (a.out_C & 3) == 0;
 }

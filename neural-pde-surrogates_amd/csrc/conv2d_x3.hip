@@ -36,6 +36,11 @@ __host__ __device__ constexpr int x3_patch_px_max(int ntaps, int tile_px) {
 }
 
 #define X3_MFMA __builtin_amdgcn_mfma_f32_32x32x16_f16
+#define X3_MFMA16 __builtin_amdgcn_mfma_f32_16x16x32_f16
+#ifndef NPS_X3_M16
+#define NPS_X3_M16 0  // 1: wide tiles on tap-paired 16x16x32 consumers (x3_consume_m16; dev variant, 3 % slower:
+                      // profiles/r5/experiments/x3_m16_tap_paired_ab.txt); 0 = the 32x32x16 consumers
+#endif
 #ifndef NPS_X3_PRIO
 #define NPS_X3_PRIO 1
 #endif
@@ -190,6 +195,163 @@ __device__ __forceinline__ void x3_store_phase(const nps_conv2d_t& a, int b, int
     stats_publish(a, b, s1, s2);  // the next GroupNorm(1)'s moments of this sample: one pair per wave
 }
 
+// Wide-tile consumers on v_mfma_f32_16x16x32_f16 with TAP-PAIRED K (NPS_X3_M16, default).  Under the DVFS
+// clock the 16x16x32 shape delivers 1.12-1.15x the FLOP/s of 32x32x16 on random operands at equal cycles
+// per FLOP (MI355X_MICROARCH "DVFS give-back" item 7), and this kernel is clock-held (0.55 of 833 TF/s on
+// zero operands, 0.40 on random ones: DESIGN.md § Round 4).  K of one MFMA = 16 channels of tap t (k 0-15)
+// + the same 16 channels of tap t + 1 (k 16-31), so the split-fp16 passes stay three per 16 input channels
+// and tap (hi*lo, hi*hi, lo*hi over a PAIR of taps: 3 MFMAs of 16 cycles per 16x16 block = the 96 cycles per
+// 32x32 block and tap of the 32x32x16 form) and neither operand is duplicated:
+//   * A (weights) reads the existing packing: lane l = (co row l & 15, channel half (l >> 4) & 1, tap half
+//     l >> 5) takes the 16-B piece that lane (co & 31) + 32 * half of the 32x32x16 fragment of its tap holds;
+//     the two tap halves are two K-groups of the packed weight (per-lane addresses, 256-B runs);
+//   * B (patch) reads 16 B per lane from LDS: pixel l & 15 of the block, channel half, tap half — a pair may
+//     straddle two stages (tap 8 of stage s, tap 0 of s + 1): both are in the ring (stage s + 1 is committed
+//     one stage ahead), and the stage barrier follows the group holding the stage's last tap;
+//   * a flattened K-group count G = nstages * NTAPS that is odd ends with a half-empty pair: its second half
+//     reads zero weights (x3_zero_w) against a re-read of the real patch window.
+// A wave owns 96 channels (6 blocks of 16) x 64 pixels (4 blocks of 16): 24 f32x4 accumulators, as before.
+// MFMA order co-block outer: a block's weight fragments are dead after its 12 MFMAs of the pair, and the next
+// pair's fragments of that block load into the same registers (one pair = 72 MFMAs of cover, as the 32x32x16
+// consumers' 3-slot ring), while the patch operands are double-buffered (the next pair's 8 reads issued at the
+// top of this one).  Epilogue: the tile into LDS and x3_store_phase, as the 32x32x16 consumers.
+__device__ __attribute__((aligned(64))) float x3_zero_w[1536];  // 6 KiB of zero weights (the odd tail's empty half)
+
+template <int NTAPS, int NCO, int TILE_PX, bool PRO, typename Decode, typename Barrier>
+__device__ __forceinline__ void x3_consume_m16(const nps_conv2d_t& a, const Geo& g, const char* ring, const float* btab,
+                                               int stage_b, int nstages, int nwg, Decode& decode, Barrier& barrier) {
+    constexpr int KWT = NTAPS == 9 ? 3 : 2;
+    constexpr int CB = 6, PBn = 4;  // 16-channel co blocks x 16-pixel blocks of a wave
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int px0 = (wave >> 1) * 64, cw0 = (wave & 1) * 96;
+    const int l16 = lane & 15, kb = lane >> 4, kh = kb & 1, th = kb >> 1;
+    int boff[PBn];
+#pragma unroll
+    for (int pb = 0; pb < PBn; ++pb) {
+        const int P = px0 + pb * 16 + l16;
+        const int ti = P / a.TW, tj = P - (P / a.TW) * a.TW;
+        boff[pb] = (ti * g.PW + tj) * X3_PIXB + kh * 16;
+    }
+    f32x4 acc[CB][PBn];
+    const int ncb = packed_ncb(a.Cout);         // 6: wide tiles are Cout == 192 (x3_wide_eligible)
+    const size_t gstride = (size_t)ncb * 2048;  // bytes per K-group (chunk, tap) of the packed weight
+    const int G = nstages * NTAPS;
+    const int GP = (G + 1) >> 1;                // tap pairs
+    // this lane's byte offset inside a 32-co block fragment: row l16 (+256 B for the odd 16-co block), channel
+    // half kh (the 32x32x16 fragment's lanes 32-63); 16-co block b of the wave at ((b >> 1) * 2048 + (b & 1) * 256)
+    const int loff = (l16 + 32 * kh) * 16;
+    const char* wbase = nullptr;
+    f16x8 Aw[CB][2];
+    f16x8 Bh[2][PBn], Bl[2][PBn];
+    auto apair = [&](int gp) {  // this lane's weight row of pair gp (the odd tail's empty half: zeros)
+        const int t = 2 * gp + th;
+        return t < G ? wbase + (size_t)t * gstride : reinterpret_cast<const char*>(x3_zero_w) + loff;
+    };
+    auto boffs = [&](int t) {  // byte offset of flattened tap t's patch window in the LDS ring
+        const int st = t / NTAPS, tap = t - (t / NTAPS) * NTAPS;
+        return (st % X3_NST) * stage_b + ((tap / KWT) * g.PW + tap % KWT) * X3_PIXB;
+    };
+    auto bsel = [&](int gp) {  // this lane's tap of pair gp (the odd tail's empty half re-reads the real tap)
+        const int t = 2 * gp + th;
+        return boffs(t < G ? t : 2 * gp);
+    };
+    auto loadB = [&](int gp, f16x8 (&dh)[PBn], f16x8 (&dl)[PBn]) __attribute__((always_inline)) {
+        const char* p = ring + bsel(gp);
+#pragma unroll
+        for (int pb = 0; pb < PBn; ++pb) {
+            dl[pb] = *reinterpret_cast<const f16x8*>(p + boff[pb] + 32);
+            dh[pb] = *reinterpret_cast<const f16x8*>(p + boff[pb]);
+        }
+    };
+    const float xsc = (PRO && a.gn_stats != nullptr) ? gn_prologue_scale(a) : in_scale_of(a);
+    const size_t wbody = packed_body(a.Cout, a.Cin, NTAPS);
+    float amax = 0.f;
+    for (int l = blockIdx.x; l < nwg; l += gridDim.x) {
+        int cob, b, oy0, ox0, ph;
+        decode(l, cob, b, oy0, ox0, ph);
+        const float* wph = a.wpack + (size_t)ph * a.phase_wstride;
+        const float inv = 1.f / (pow2_scale_for(wph[wbody]) * xsc);
+        wbase = reinterpret_cast<const char*>(wph) + (size_t)cob * (NCO / 32) * 2048 + (cw0 >> 5) * 2048 + loff;
+#pragma unroll
+        for (int i = 0; i < CB; ++i)
+#pragma unroll
+            for (int j = 0; j < PBn; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        {
+            const char* p = apair(0);
+#pragma unroll
+            for (int cb = 0; cb < CB; ++cb) {
+                Aw[cb][0] = *reinterpret_cast<const f16x8*>(p + (cb >> 1) * 2048 + (cb & 1) * 256);
+                Aw[cb][1] = *reinterpret_cast<const f16x8*>(p + (cb >> 1) * 2048 + (cb & 1) * 256 + 1024);
+            }
+        }
+        barrier();
+        loadB(0, Bh[0], Bl[0]);
+        // pair gp: patch operands in slot r, the next pair's into r ^ 1; each co block's next weights load
+        // right after that block's last MFMA (hi after the hi*lo and hi*hi passes, lo after lo*hi)
+        auto group = [&](int gp, const int r) __attribute__((always_inline)) {
+            const int gn = gp + 1 < GP ? gp + 1 : gp;
+            loadB(gn, Bh[r ^ 1], Bl[r ^ 1]);
+            const char* pa = apair(gn);
+#pragma unroll
+            for (int cb = 0; cb < CB; ++cb) {
+#pragma unroll
+                for (int pb = 0; pb < PBn; ++pb)
+                    acc[cb][pb] = X3_MFMA16(Aw[cb][0], Bl[r][pb], acc[cb][pb], 0, 0, 0);  // hi * lo
+#pragma unroll
+                for (int pb = 0; pb < PBn; ++pb)
+                    acc[cb][pb] = X3_MFMA16(Aw[cb][0], Bh[r][pb], acc[cb][pb], 0, 0, 0);  // hi * hi
+                Aw[cb][0] = *reinterpret_cast<const f16x8*>(pa + (cb >> 1) * 2048 + (cb & 1) * 256);
+#pragma unroll
+                for (int pb = 0; pb < PBn; ++pb)
+                    acc[cb][pb] = X3_MFMA16(Aw[cb][1], Bh[r][pb], acc[cb][pb], 0, 0, 0);  // lo * hi
+                Aw[cb][1] = *reinterpret_cast<const f16x8*>(pa + (cb >> 1) * 2048 + (cb & 1) * 256 + 1024);
+            }
+#pragma unroll
+            for (int cb = 0; cb < CB; ++cb) {
+                if (cb < 2) {  // the next pair's 8 patch reads, one per MFMA gap in the first two blocks
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    }
+                    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+                } else {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+                }
+                __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // next hi fragment of block cb
+                __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+                __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // next lo fragment of block cb
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            const int t0 = 2 * gp;
+            if (t0 % NTAPS == NTAPS - 1 || (t0 + 1 < G && (t0 + 1) % NTAPS == NTAPS - 1)) barrier();
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        int gp = 0;
+        for (; gp + 2 <= GP; gp += 2) {
+            group(gp, 0);
+            group(gp + 1, 1);
+        }
+        if (gp < GP) group(gp, 0);
+        // the ring is free (every read of it completed before the last stage barrier): the tile goes to LDS
+        // (16x16 accumulator: lane holds pixel l16, channels 4 kb + [0, 4) of its block), then all 8 waves store it
+        float* T = reinterpret_cast<float*>(const_cast<char*>(ring));
+#pragma unroll
+        for (int pb = 0; pb < PBn; ++pb) {
+            const int P = px0 + pb * 16 + l16;
+#pragma unroll
+            for (int cb = 0; cb < CB; ++cb) {
+                const f32x4 v = acc[cb][pb] * inv;
+                *reinterpret_cast<f32x4*>(T + P * (NCO + 4) + cw0 + cb * 16 + 4 * kb) = v;
+            }
+        }
+        barrier();
+        x3_store_phase<TILE_PX, NCO>(a, b, cob, oy0, ox0, g.T, ph, T, btab, tid, amax);
+        barrier();  // the staged tile is fully read: the producers may refill the ring
+    }
+    nps::tag_publish(a.out_tag, amax, nps::wave_salt());
+}
+
 // PRO: the frame prologue (GroupNorm affine and/or GELU, proc_unet_modern.py:62-99) is applied by the
 // producers while staging, instead of a frame_pack pass in front of the conv.
 // WIDE: the work-group covers 192 output channels x 128 pixels instead of 64 x 4*PB*32: consumer wave w
@@ -205,6 +367,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
     constexpr int TILE_PX = WIDE ? 128 : 4 * PB * 32;
     constexpr int MAXP = (x3_patch_px_max(NTAPS, TILE_PX) * 4 + 255) / 256;
     constexpr bool SPREAD = WIDE && NPS_X3_SPREAD;  // wide tiles: spread store (dev knob: the store phase)
+    constexpr bool M16 = WIDE && !SPREAD && NPS_X3_M16;  // wide tiles: tap-paired 16x16x32 consumers
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const Geo g = make_geo(a);
@@ -512,6 +675,10 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
     }
 
     // ---------------------------------------------------------------------- consumers
+    if constexpr (M16) {
+        x3_consume_m16<NTAPS, NCO, TILE_PX, PRO>(a, g, ring, btab, stage_b, nstages, nwg, decode, barrier);
+        return;
+    }
     int boff[PBW];
     const int px0 = WIDE ? (wave >> 1) * 64 : wave * 32 * PB;  // this wave's first tile pixel
     const int cw0 = WIDE ? (wave & 1) * 96 : 0;                // this wave's first channel in the co group

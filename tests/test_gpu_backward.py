@@ -64,6 +64,10 @@ CONV_CASES = [
     (132, 128, 5, 1, 4, "same", "circular", 40, 36),
     (81, 192, 1, 1, 1, 0, "zeros", 19, 23),         # encoder 1x1, Cin % 4 != 0
     (192, 75, 1, 1, 1, 0, "zeros", 16, 16),         # pre-decoder 1x1
+    # packing boundaries: dgrad Cin / wgrad M one past a 192 pack, 4-channel tails
+    (36, 193, 3, 1, 1, 1, "zeros", 14, 15),         # wgrad M = 193 (pad-4 path), dgrad 193 -> 36
+    (196, 388, 1, 1, 1, 0, "zeros", 12, 13),        # 1x1: wgrad 388 x 196, dgrad 388 -> 196
+    (388, 192, 3, 1, 1, 1, "zeros", 11, 12),        # the U-Net up-block 3x3: dgrad 192 -> 388 (Cout tail 4)
 ]
 
 

@@ -42,6 +42,16 @@ CONV_CASES = [
     (36, 600, 1, 1, 1, 0, "circular", 9, 10),       # co-block waves, two 512-channel groups
     (12, 16, 5, 1, 1, 2, "zeros", 19, 21),          # undilated 5x5, zero pad (split-fp16 25-tap kernel)
     (16, 24, 5, 1, 2, 4, "zeros", 23, 18),          # dilated 5x5 on the lattice, zero pad
+    # packing boundaries (a latent over-read must be caught by a shape, not by allocation luck):
+    # packed_ncb pads Cout to a multiple of 192 (6 x 32-channel blocks), the 1x1 co-block grid splits at 512
+    (16, 193, 3, 1, 1, 1, "zeros", 18, 21),         # 3x3, 64-channel tiles, one channel past a 192 pack
+    (36, 385, 3, 1, 1, 1, "circular", 12, 17),      # 3x3, 7 co tiles, packs of 2 x 192 + 1
+    (40, 160, 3, 1, 1, 1, "zeros", 19, 22),         # 3x3 wide tile, Cout = 160: the last blocks are pack padding
+    (20, 577, 1, 1, 1, 0, "zeros", 11, 13),         # 1x1 co-block waves, 512-channel group 2 of 65 channels
+    (20, 193, 1, 1, 1, 0, "zeros", 14, 9),          # 1x1 co-block waves, one channel past the LDS-weight kernel
+    (33, 192, 1, 1, 1, 0, "zeros", 16, 15),         # 1x1 LDS weights, Cin tail of 1 (frame-packed to 36)
+    (388, 192, 3, 1, 1, 1, "zeros", 17, 19),        # 3x3 wide, 25 stages, Cin tail 4 (the odd tap-pair count)
+    (388, 196, 3, 1, 1, 1, "zeros", 13, 12),        # 3x3, Cout 196: 64-channel tiles, last tile 4 channels
 ]
 
 

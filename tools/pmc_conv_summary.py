@@ -2,7 +2,7 @@
 
 Effective clock = GRBM_GUI_ACTIVE / 8 XCDs / kernel duration (MI355X_MICROARCH.md 'DVFS give-back');
 MFMA pipe busy = SQ_VALU_MFMA_BUSY_CYCLES / (clock cycles x 4 SIMDs x CUs).
-usage: python tools/pmc_conv_summary.py gpurun_out [n_cu]
+usage: python tools/pmc_conv_summary.py gpurun_out [n_cu] [prefix (default pmcc)]
 """
 import csv
 import glob
@@ -12,12 +12,13 @@ from collections import defaultdict
 
 root = sys.argv[1]
 ncu = int(sys.argv[2]) if len(sys.argv) > 2 else 256
+pre = sys.argv[3] if len(sys.argv) > 3 else "pmcc"
 vals = defaultdict(lambda: defaultdict(list))
-for f in glob.glob(f"{root}/pmcc_*/**/*counter_collection.csv", recursive=True):
+for f in glob.glob(f"{root}/{pre}_*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         vals[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
 dur = defaultdict(list)
-for f in glob.glob(f"{root}/pmcc_1/**/*kernel_trace.csv", recursive=True):
+for f in glob.glob(f"{root}/{pre}_1/**/*kernel_trace.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         dur[r["Kernel_Name"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
 name = max(dur, key=lambda k: sum(dur[k]))
