@@ -1,6 +1,7 @@
 #!/bin/bash
 # Same-box A/B of two builds of the library: bench.py alternated A B A B (ROUNDS times), one JSON line each.
-# usage: tools/ab_lib.sh TAG libA.so libB.so [bench.py args...]   (libs relative to nps_hip/, "hip" = libnps_hip.so)
+# usage: tools/ab_lib.sh TAG libA.so libB.so [bench.py args...]   (libs relative to nps_hip/, "hip" = libnps_hip.so,
+#        "env:VAR=VAL" = libnps_hip.so with that environment variable set, e.g. a dev knob)
 # env ROUNDS (default 2).  Output: gpurun_out/${TAG}_ab.jsonl, a summary on stdout.
 set -o pipefail
 TAG=$1; A=$2; B=$3; shift 3
@@ -12,9 +13,14 @@ O=gpurun_out/${TAG}_ab.jsonl
 LIBDIR=neural-pde-surrogates_amd/nps_hip
 for r in $(seq 1 $ROUNDS); do
   for L in $A $B; do
-    [ "$L" = hip ] && F=$LIBDIR/libnps_hip.so || F=$LIBDIR/$L
+    EV=""
+    case $L in
+      hip) F=$LIBDIR/libnps_hip.so ;;
+      env:*) F=$LIBDIR/libnps_hip.so; EV=${L#env:} ;;
+      *) F=$LIBDIR/$L ;;
+    esac
     [ -f "$F" ] || { echo "missing $F"; exit 1; }
-    NPS_HIP_LIB=$PWD/$F timeout -k 10 300 python3 bench.py --cpu-calls 0 "$@" > gpurun_out/${TAG}_one.json 2> gpurun_out/${TAG}_one.err \
+    env $EV NPS_HIP_LIB=$PWD/$F timeout -k 10 300 python3 bench.py --cpu-calls 0 "$@" > gpurun_out/${TAG}_one.json 2> gpurun_out/${TAG}_one.err \
       || { echo "bench failed on $L"; tail -20 gpurun_out/${TAG}_one.err; exit 1; }
     python3 - "$L" gpurun_out/${TAG}_one.json >> $O <<'EOF'
 import json, sys

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--num-c", type=int, default=3)
     a = ap.parse_args()
     dev = torch.device("cuda")
+    ops.SIDE_STREAM = False  # one stream: a forked launch would be timed from its dispatch (bench.probe_roofline)
     model, _, _ = bench.build_model(a.model, a.res, a.num_c, dev)
     from trainers.synthetic import twophase_batch
     u, cond, pos, sc = twophase_batch(B=a.b, num_c=a.num_c, T=50, H=a.res, W=a.res, seed=1)
