@@ -146,7 +146,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
     float amax = 0.f;
     double s1 = 0.0, s2 = 0.0;
     int stat_b = -1;  // sample whose moments (s1, s2) hold
-    const bool vec4 = (a.out_C & 3) == 0 && (a.Cout & 3) == 0;
+    const bool vec4 = !a.out_nchw && (a.out_C & 3) == 0 && (a.Cout & 3) == 0;
     const bool add = a.addend0 != nullptr;
     int out_j = wid;  // block of the next epilogue
 
@@ -160,7 +160,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
         const int oy = p / a.Wout, ox = p - (p / a.Wout) * a.Wout;
         const int dy = oy * a.out_os + a.out_off_y, dx = ox * a.out_os + a.out_off_x;
         const bool pout = p < npx && dy >= 0 && dy < a.out_H && dx >= 0 && dx < a.out_W;
-        const size_t base = (((size_t)b * a.out_H + (pout ? dy : 0)) * a.out_W + (pout ? dx : 0)) * a.out_C + co_lo + 4 * h;
+        // NHWC: channel c of the pixel at base + c; NCHW (the decoder's planar pre-output, dec_grid.py:126-130):
+        // at base + c * plane, so for each channel the wave's 32 pixels are one contiguous run
+        const size_t plane = (size_t)a.out_H * a.out_W;
+        const size_t base = a.out_nchw ? ((size_t)b * a.out_C + co_lo + 4 * h) * plane + (size_t)(pout ? dy : 0) * a.out_W +
+                                             (pout ? dx : 0)
+                                       : (((size_t)b * a.out_H + (pout ? dy : 0)) * a.out_W + (pout ? dx : 0)) * a.out_C +
+                                             co_lo + 4 * h;
         const int cmax = pout ? a.Cout - co_lo - 4 * h : 0;  // quad offset o (within the group) is valid iff o < cmax
         if (a.out_stats != nullptr && b != stat_b) {         // uniform: one publish per sample change
             if (stat_b >= 0) stats_publish(a, stat_b, s1, s2);
@@ -214,7 +220,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
             for (int m = 0; m < 4; ++m) {
                 const int o = cb * 32 + 8 * m;
                 const f32x4 r = {acc[cb][4 * m], acc[cb][4 * m + 1], acc[cb][4 * m + 2], acc[cb][4 * m + 3]};
-                if (vec4) {
+                if (a.out_nchw) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (o + e < cmax) ob[(size_t)(o + e) * plane] = r[e];
+                } else if (vec4) {
                     *reinterpret_cast<f32x4*>(o < cmax ? ob + o : x1r_sink + o) = r;
                 } else {
 #pragma unroll
@@ -293,9 +303,14 @@ void launch(const nps_conv2d_t& a, unsigned grid, int ng, int nres, hipStream_t 
 
 }  // namespace
 
-int nps_launch_conv1x1_res(const nps_conv2d_t& a, hipStream_t s) {
-    if (a.KH * a.KW != 1 || a.accumulate || a.addend1 != nullptr || a.out_nchw) return 0;
-    if (a.out_stats != nullptr && (a.Cout > 192 || a.addend0 != nullptr || a.act != 0)) return 0;
+int nps_launch_conv1x1_res(const nps_conv2d_t& a, int all, hipStream_t s) {
+    // all = 0: only the planar (NCHW) 1x1s with 192 < Cout <= 256 — the decoder's pre-output, which the LDS-staged
+    // kernel (Cout <= 192, NHWC) cannot take and the co-block kernel ran at 1.4 TB/s; all = 1 (dev knob
+    // NPS_X1_RES=1): every eligible 1x1
+    if (!all && !(a.out_nchw && a.Cout > 192 && a.Cout <= 256)) return 0;
+    if (a.KH * a.KW != 1 || a.accumulate || a.addend1 != nullptr) return 0;
+    if (a.out_nchw && (a.addend0 != nullptr || a.out_stats != nullptr)) return 0;
+    if (a.out_stats != nullptr && a.Cout > 192) return 0;  // (moments of the stored values: addend / act included)
     if ((long)a.B * ((a.Hout * a.Wout + 31) / 32) >= (1L << 31)) return 0;
     static long gx = 0;
     if (gx == 0) {

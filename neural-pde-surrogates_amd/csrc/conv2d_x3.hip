@@ -2447,16 +2447,17 @@ int nps_launch_conv2d_x3(const nps_conv2d_t& a, int lds, hipStream_t s) {
             const char* e = getenv("NPS_X3_1X1_WL");
             wl = (e != nullptr && e[0] == '0') ? 0 : 1;
         }
-        NPS_CHECK_ARG(a.out_stats == nullptr || (wl && a.Cout <= 192 && !a.accumulate && !a.addend0 && !a.addend1 &&
-                                                 a.act == 0),
-                      "conv2d_fwd (split-fp16 1x1): out_stats needs the LDS-weight kernel (Cout <= 192) and a "
-                      "plain epilogue (bias only)");
-        static int res_on = -1;  // dev knob NPS_X1_RES=1: resident-weight kernel (conv1x1_res.hip; off: at par or
-        if (res_on < 0) {        // slower on the C3 shapes, profiles/r5/experiments/x1_resident_weights_ab.txt)
+        // out_stats: the LDS-weight kernel's fused register epilogue takes the moments of the values it stores
+        // (after the addend and the activation); its store_tile fallback (two addends, accumulate) cannot
+        NPS_CHECK_ARG(a.out_stats == nullptr || (wl && a.Cout <= 192 && !a.accumulate && a.addend1 == nullptr && lds_epi),
+                      "conv2d_fwd (split-fp16 1x1): out_stats needs the LDS-weight kernel (Cout <= 192), an NHWC "
+                      "4-aligned output and at most one addend, no accumulate");
+        static int res_on = -1;  // dev knob NPS_X1_RES=1: resident-weight kernel for every 1x1 (default: only the
+        if (res_on < 0) {        // planar decoder shape; at par or slower on the others, profiles/r5/experiments/x1_resident_weights_ab.txt)
             const char* e = getenv("NPS_X1_RES");
             res_on = (e != nullptr && e[0] == '1') ? 1 : 0;
         }
-        if (res_on && nps_launch_conv1x1_res(a, s)) return 0;  // resident weights (conv1x1_res.hip)
+        if (nps_launch_conv1x1_res(a, res_on, s)) return 0;  // resident weights (conv1x1_res.hip)
         if (wl && a.Cout <= 192) {  // (Cout 193..256 measured slower with 8 blocks per wave: co-block waves)
             const long nb = ((long)a.Hout * a.Wout + 127) / 128;
             NPS_CHECK_ARG(nb < (1L << 31) && a.B < 65536, "conv2d_fwd: grid too large");

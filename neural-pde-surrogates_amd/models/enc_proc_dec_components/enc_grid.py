@@ -47,7 +47,9 @@ class ElementWise(nn.Module):
         # xin carries <= 3 zero channels of padding; the packed weight is zero-padded to
         # 16-channel chunks, so the same packed buffer serves (ceil16(Cp) == ceil16(n_in)).
         h = c1.run([ops.Src(xin)], (H, W), act=act)
-        return c2.run([ops.Src(h)], (H, W), act=act)
+        # the output carries its GroupNorm(1) moments (a U-Net processor's first norm reads it): no statistics pass
+        st = ops.new_stats(h.shape[0], h)
+        return ops.attach_stats(c2.run([ops.Src(h)], (H, W), act=act, out_stats=st), st)
 
     def run_packed_ad(self, xin):
         """Differentiable form of run_packed (the packed input is data: no gradient flows into it)."""

@@ -131,9 +131,12 @@ class UNetModern(nn.Module):
         out = ops.empty_nhwc(B, Ht, Wt, self.final.out_channels, h)
         if oy > 0 or ox > 0:
             out.zero_()  # crop_Nd zero-pads when the output is smaller than the input
+        # the output carries its GroupNorm(1) moments (the next U-FNO block's norm1 frame reads it): no statistics
+        # pass over it (zero crop padding adds nothing to the sums)
+        st = ops.new_stats(B, out)
         self.final.run([ops.Src(h)], (H, W), gn=gn, pre_act=activation_code(self.activation), out=out,
-                       out_off=(oy, ox), addends=[addend] if addend is not None else [], act=act_after)
-        return out
+                       out_off=(oy, ox), addends=[addend] if addend is not None else [], act=act_after, out_stats=st)
+        return ops.attach_stats(out, st)
 
     def run_ad(self, h, vb):
         """Differentiable NHWC forward (training): proc_unet_modern.py:169-196 as unfused HIP ops."""

@@ -338,6 +338,9 @@ def drop_stats(t: torch.Tensor):
         t._nps_stats = None
 
 
+_DEBUG_STATS = os.environ.get("NPS_DEBUG_STATS") == "1"  # dev: print every GroupNorm statistics pass and its caller
+
+
 def stats_of(t: torch.Tensor) -> Optional[torch.Tensor]:
     """t's live GroupNorm(1) moments, or None."""
     rec = getattr(t, "_nps_stats", None)
@@ -352,6 +355,9 @@ def source_stats(t: torch.Tensor) -> torch.Tensor:
     seed a buffer of your own with copy_stats() to accumulate into."""
     st = stats_of(t)
     if st is None:
+        if _DEBUG_STATS:
+            import traceback
+            print("nps stats pass (source)", tuple(t.shape), "".join(traceback.format_stack(limit=5)[:-1]), flush=True)
         st = new_stats(t.shape[0], t, 1)
         check(lib.nps_group_norm_stats(_c_src([Src(t)]), 1, t.shape[0], t.shape[1], t.shape[2], t.shape[3], 1,
                                        ptr(st), 0, stream_ptr()), "group_norm_stats (source)")
@@ -493,6 +499,10 @@ def group_norm_stats(srcs: Sequence[Src], frame_hw, groups: int) -> torch.Tensor
             return parts[0]
         return _stats_sum(parts, B, new_stats(B, t0, 1))
     Cin = sum(s.t.shape[3] for s in srcs)
+    if _DEBUG_STATS:
+        import traceback
+        print("nps stats pass (frame)", [tuple(s.t.shape) for s in srcs], frame_hw, groups,
+              "".join(traceback.format_stack(limit=5)[:-1]), flush=True)
     stats = torch.empty((B, groups, 2), dtype=torch.float64, device=t0.device)
     check(lib.nps_group_norm_stats(_c_src(srcs), len(srcs), B, frame_hw[0], frame_hw[1], Cin, groups, ptr(stats), 1,
                                    stream_ptr()), "group_norm_stats")
@@ -590,7 +600,9 @@ def conv2d(srcs: Sequence[Src], frame_hw, wpack: torch.Tensor, bias: Optional[to
     if USE_OUT_TAGS:
         a.out_tag = out_tag(out, accumulate) if out_given else new_tag(out)
     if out_stats is not None:
-        plain = not accumulate and not ads and act == 0
+        # 1x1: the LDS-weight kernel's fused epilogue (at most one addend, no accumulate) takes the moments of the
+        # stored values, activation and addend included
+        plain = not accumulate and len(ads) <= 1
         x1_ok = lib.nps_conv2d_x1_dma(ctypes_byref(a)) == 1 or (Cout <= 192 and X1_LDS_WEIGHTS and plain)
         if (a.precision == PREC_X3F16 and (KH * KW != 1 or x1_ok)
                 and not out_nchw and oC % 4 == 0 and Cout % 4 == 0):

@@ -451,3 +451,20 @@ def test_ufno_c2_full_size_one_call():
     ref = oracle.build_oracle_model(ocfg, opde, {k: v.cpu() for k, v in m.state_dict().items()})(
         u, cond=cond, pos=pos, spatial_cond=sc)
     assert rel_l2(y, ref) < TOL
+
+
+@pytest.mark.parametrize("cin,cout,hw", [(192, 225, (37, 29)), (36, 200, (16, 21)), (84, 256, (9, 40))])
+def test_conv1x1_planar_output_vs_torch(cin, cout, hw):
+    """The decoder's pre-output 1x1 (dec_grid.py:126-130) writes NCHW planes with 192 < Cout <= 256: the
+    resident-weight kernel (conv1x1_res.hip, two channel groups of 128) with planar stores."""
+    from models.common import Conv2d
+    from nps_hip import ops
+    torch.manual_seed(5)
+    m = Conv2d(cin, cout, 1)
+    x = torch.randn(2, cin, *hw)
+    ref = Fo.conv2d_ref(x, {"weight": m.weight.detach(), "bias": m.bias.detach()}, "", stride=1, padding=0,
+                        dilation=1, padding_mode="zeros")
+    md = m.to(DEV)
+    y = md.run([ops.Src(ops.nchw_to_nhwc(x.to(DEV)))], hw, out_nchw=True)
+    assert tuple(y.shape) == (2, cout) + hw
+    assert rel_l2(y.cpu(), ref) < TOL
