@@ -548,7 +548,8 @@ bool x3_eligible(const nps_conv2d_t& a) {
     const bool geo = a.stride == 1 && a.KH == a.KW &&
                      ((a.dil == 1 && (nt == 1 || nt == 4 || nt == 9)) || (nt == 25 && a.dil >= 1));
     if (a.gn_stats == nullptr && a.pre_act == 0) return geo;
-    return geo && nt == 9 && (a.pre_act == 0 || a.pre_act == 1) &&
+    // fused prologue: the 3x3 producers, and the 1x1 LDS-weight kernel (its launcher checks Cout <= 192)
+    return geo && (nt == 9 || nt == 1) && (a.pre_act == 0 || a.pre_act == 1) &&
            (a.gn_stats == nullptr || (a.gn_groups > 0 && a.Cin % a.gn_groups == 0 && (a.Cin / a.gn_groups) % 4 == 0));
 }
 

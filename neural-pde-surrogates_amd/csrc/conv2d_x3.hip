@@ -1717,7 +1717,11 @@ __global__ __launch_bounds__(512) void conv1x1_x3_kernel(const nps_conv2d_t a) {
 // blocks x 2 KB) into one of two LDS buffers (fetched one stage ahead into registers, compiler-managed
 // loads), one barrier per stage; B as in conv1x1_x3_kernel (per-lane 64-B runs in a D-deep register
 // ring, zero page outside the frame).  Epilogue: store_tile per 32-channel block.
-template <int NCB, int D>
+// PRO: the frame prologue act(GroupNorm(frame)) (the U-Net's final GN(8) + GELU before its 1x1 conv,
+// proc_unet_modern.py:191-196) applied to each loaded input element before the split, instead of a frame_pack
+// pass: per-channel affine (scale, shift) of this work-group's sample in an LDS table built at kernel start from the
+// fp64 moments, then GELU; frame pixels no source covers get act(GN(0)), the conv's own zero padding stays 0.
+template <int NCB, int D, bool PRO = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void conv1x1_wl_kernel(const nps_conv2d_t a) {
     constexpr int WSTAGE = 2 * NCB * 2048;       // bytes of one stage's weight fragments
     constexpr int WPT = WSTAGE / (256 * 16);     // 16-B pieces per thread per stage
@@ -1734,8 +1738,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     const int h = lane >> 5;
     const int npx = a.Hout * a.Wout;
     const int P = blockIdx.x * 128 + wv * 32 + (lane & 31);
-    const float xs = in_scale_of(a);
-    const bool scaled = has_in_scale(a);
+    const float xs = PRO ? gn_prologue_scale(a) : in_scale_of(a);
+    const bool scaled = PRO || has_in_scale(a);
     int fy, fx;
     bool pin;
     {
@@ -1807,6 +1811,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     if ((int)threadIdx.x < NCB * 32)  // the epilogue's bias table (zero past Cout), behind the first barrier
         reinterpret_cast<float*>(wl + 2 * WSTAGE)[threadIdx.x] =
             (a.bias != nullptr && (int)threadIdx.x < a.Cout) ? a.bias[threadIdx.x] : 0.f;
+    // PRO: per-channel GroupNorm affine of sample b, y = x * gs[c] + gb[c] (gs = rstd * gamma, gb = beta - mean * gs, the
+    // producers' form in conv2d_x3_kernel), zero past Cin (GELU(0) = 0 against zero weights)
+    float* gtab = reinterpret_cast<float*>(wl + 2 * WSTAGE + NCB * 32 * 4);  // [2][nstages * 32]
+    if constexpr (PRO) {
+        const int ncp = ((a.Cin + 2 * CK - 1) / (2 * CK)) * 2 * CK;
+        const bool gn = a.gn_stats != nullptr;
+        const double icnt = gn ? 1.0 / ((double)(a.Cin / a.gn_groups) * a.Hin * a.Win) : 0.0;
+        for (int c = threadIdx.x; c < ncp; c += 256) {
+            float gs = 1.f, gb = 0.f;
+            if (c >= a.Cin) {
+                gs = 0.f;
+            } else if (gn) {
+                const double* st = a.gn_stats + ((size_t)b * a.gn_groups + c / (a.Cin / a.gn_groups)) * 2;
+                const double mu = st[0] * icnt;
+                double var = fma(st[1], icnt, -mu * mu);
+                var = var < 0.0 ? 0.0 : var;
+                const float rstd = __builtin_amdgcn_rsqf((float)(var + (double)a.gn_eps));
+                gs = rstd * a.gn_gamma[c];
+                gb = fmaf(-(float)mu, gs, a.gn_beta[c]);
+            }
+            gtab[c] = gs;
+            gtab[ncp + c] = gb;
+        }
+    }
     f32x16 acc[NCB];
 #pragma unroll
     for (int i = 0; i < NCB; ++i)
@@ -1840,6 +1868,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
             for (int k = 0; k < 2; ++k) {
                 f16x4 h0, l0, h1, l1;
                 f32x4 v0 = raw[j][2 * k], v1 = raw[j][2 * k + 1];
+                if constexpr (PRO) {  // channels st * 32 + h * 16 + 8 k + [0, 8) of this lane's pixel
+                    // (the padded iterations of the ring, st > last, read no table: their input must stay 0)
+                    const int ncp = ((a.Cin + 2 * CK - 1) / (2 * CK)) * 2 * CK;
+                    const bool live = pin && st <= last;
+                    const int c = min(st, last) * 2 * CK + h * CK + 8 * k;
+                    const f32x4 s0 = *reinterpret_cast<const f32x4*>(gtab + c);
+                    const f32x4 s1 = *reinterpret_cast<const f32x4*>(gtab + c + 4);
+                    const f32x4 b0 = *reinterpret_cast<const f32x4*>(gtab + ncp + c);
+                    const f32x4 b1 = *reinterpret_cast<const f32x4*>(gtab + ncp + c + 4);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        float y0 = fmaf(v0[e], s0[e], b0[e]), y1 = fmaf(v1[e], s1[e], b1[e]);
+                        if (a.pre_act == 1) {
+                            y0 = nps::gelu_fast(y0);
+                            y1 = nps::gelu_fast(y1);
+                        }
+                        v0[e] = live ? y0 : 0.f;  // (outside the frame: the conv's zero padding)
+                        v1[e] = live ? y1 : 0.f;
+                    }
+                }
                 if (scaled) {
                     v0 *= xs;
                     v1 *= xs;
@@ -2419,7 +2467,8 @@ int nps_launch_conv2d_x3(const nps_conv2d_t& a, int lds, hipStream_t s) {
     // 1x1 convs (never with a prologue: x3_eligible) run on the ring-free kernel, whose 32-channel
     // stages match the 1x1 weight packing; work-group = min(ncob, 8) waves, blockIdx.z = 512-channel group
     if (a.KH * a.KW == 1) {
-        NPS_CHECK_ARG(!pro, "conv2d_fwd (split-fp16): 1x1 prologue");
+        NPS_CHECK_ARG(!pro || a.Cout <= 192, "conv2d_fwd (split-fp16): a 1x1 prologue needs the LDS-weight kernel "
+                      "(Cout <= 192)");
 #ifdef NPS_X1_DMA_KERNEL
         if (x1_dma_ok(a)) {
             const int ncb = (a.Cout + 31) / 32;
@@ -2456,6 +2505,14 @@ int nps_launch_conv2d_x3(const nps_conv2d_t& a, int lds, hipStream_t s) {
         if (res_on < 0) {        // planar decoder shape; at par or slower on the others, profiles/r5/experiments/x1_resident_weights_ab.txt)
             const char* e = getenv("NPS_X1_RES");
             res_on = (e != nullptr && e[0] == '1') ? 1 : 0;
+        }
+        if (pro) {  // fused GroupNorm + GELU prologue: the LDS-weight kernel with the per-channel affine table
+            const long nb = ((long)a.Hout * a.Wout + 127) / 128;
+            NPS_CHECK_ARG(nb < (1L << 31) && a.B < 65536, "conv2d_fwd: grid too large");
+            const int ncp = ((a.Cin + 31) / 32) * 32;
+            conv1x1_wl_kernel<6, 2, true><<<dim3((unsigned)nb, a.B), 256, 2 * 2 * 6 * 2048 + 6 * 32 * 4 + 2 * ncp * 4, s>>>(a);
+            NPS_CHECK_LAUNCH("conv2d_fwd (split-fp16 1x1, LDS weights, GroupNorm prologue)");
+            return 0;
         }
         if (nps_launch_conv1x1_res(a, res_on, s)) return 0;  // resident weights (conv1x1_res.hip)
         if (wl && a.Cout <= 192) {  // (Cout 193..256 measured slower with 8 blocks per wave: co-block waves)

@@ -22,6 +22,9 @@ PREC_F32, PREC_X3F16 = 0, 1
 # instead of a frame_pack pass in front of the conv (dev knob NPS_FUSE_PROLOGUE=0: off).  Pays off on the
 # wide 192-channel tiles, whose producers stage each patch once for all output channels.
 FUSE_PROLOGUE = os.environ.get("NPS_FUSE_PROLOGUE", "1") == "1"
+# dev knob NPS_FUSE_PROLOGUE_1X1=0: the 1x1 convs' GroupNorm + GELU prologue materialised by frame_pack (A/B of the
+# LDS-weight kernel's fused prologue, conv1x1_wl_kernel<6, 2, true>)
+FUSE_PROLOGUE_1X1 = os.environ.get("NPS_FUSE_PROLOGUE_1X1", "1") != "0"
 CONV_PRECISION = PREC_F32 if os.environ.get("NPS_CONV_PRECISION", "x3f16") == "f32" else PREC_X3F16
 X1_LDS_WEIGHTS = os.environ.get("NPS_X3_1X1_WL", "1")[:1] != "0"  # (libnps_hip's dev knob of the same name)
 # the Downsample's 2x2 conv reads the space-to-depth view of its input directly (nps_conv2d_t.s2d) instead of
@@ -535,7 +538,8 @@ def conv2d(srcs: Sequence[Src], frame_hw, wpack: torch.Tensor, bias: Optional[to
     x3 = getattr(wpack, "nps_precision", PREC_F32) == PREC_X3F16
     aligned = not x3 or lib.nps_conv2d_x3_sources_ok(_c_src(srcs), len(srcs))
     fused = (x3 and aligned and FUSE_PROLOGUE and (gn is not None or pre_act) and stride == 1 and dil == 1 and
-             lib.nps_conv2d_x3_prologue_ok(KH, KW, Cin, gn.groups if gn is not None else 0, pre_act))
+             lib.nps_conv2d_x3_prologue_ok(KH, KW, Cin, gn.groups if gn is not None else 0, pre_act) and
+             (KH * KW != 1 or (FUSE_PROLOGUE_1X1 and Cout <= 192 and not out_nchw and phases == 1)))
     if not fused and (((gn is not None or pre_act) and stride == 1 and dil == 1 and KH == KW and KH in (1, 2, 3))
                       or not aligned):
         # the stride-1 producer/consumer convs stage raw bytes only (the split-fp16 one from 16-channel

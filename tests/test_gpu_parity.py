@@ -4,6 +4,7 @@ Tolerance: fp32 rel-L2 < 1e-5 (BASELINE.json north star; fp32 noise floor ~1e-7)
 """
 import pytest
 import torch
+import torch.nn.functional as F
 from torch import nn
 
 import oracle
@@ -468,3 +469,41 @@ def test_conv1x1_planar_output_vs_torch(cin, cout, hw):
     y = md.run([ops.Src(ops.nchw_to_nhwc(x.to(DEV)))], hw, out_nchw=True)
     assert tuple(y.shape) == (2, cout) + hw
     assert rel_l2(y.cpu(), ref) < TOL
+
+
+@pytest.mark.parametrize("cin,cout,groups,pad,xscale", [(192, 192, 8, 0, 1.0), (196, 75, 1, 1, 3e3), (36, 192, 3, 0, 1e-3)])
+def test_conv1x1_fused_groupnorm_gelu_prologue(cin, cout, groups, pad, xscale):
+    """The U-Net's final GN(8) + GELU + 1x1 (proc_unet_modern.py:191-196) as ONE launch: the LDS-weight 1x1
+    kernel applies the GroupNorm affine and GELU to each loaded element (no frame_pack materialisation); frame
+    pixels get act(GN(x)), the conv's zero padding stays 0."""
+    from nps_hip import ops
+    torch.manual_seed(11)
+    B, H, W = 2, 21, 18
+    x = torch.randn(B, cin, H, W) * xscale + 0.2 * xscale
+    gamma = torch.rand(cin) + 0.5
+    beta = torch.rand(cin) - 0.5
+    w = torch.randn(cout, cin, 1, 1) * 0.05
+    b = torch.randn(cout) * 0.1
+    ref = F.conv2d(F.gelu(F.group_norm(x.double(), groups, gamma.double(), beta.double(), 1e-5)), w.double(),
+                   b.double(), padding=pad)
+    packs = []
+    real_pack = ops.frame_pack
+    try:
+        ops.frame_pack = lambda *a, **k: packs.append(1) or real_pack(*a, **k)
+        xd = ops.nchw_to_nhwc(x.to(DEV))
+        st = ops.group_norm_stats([ops.Src(xd)], (H, W), groups)
+        gn = ops.GN(st, gamma.to(DEV), beta.to(DEV), groups, 1e-5)
+        ost = ops.new_stats(B, xd)  # the U-Net's final conv also carries its output's GroupNorm(1) moments
+        y = ops.conv2d([ops.Src(xd)], (H, W), ops.pack_conv_weight(w.to(DEV)), b.to(DEV), cout, 1, 1, pad=(pad, pad),
+                       gn=gn, pre_act=1, out_stats=ost)
+    finally:
+        ops.frame_pack = real_pack
+    assert not packs, "GroupNorm prologue of the 1x1 went through frame_pack"
+    assert rel_l2(ops.nhwc_to_nchw(y).cpu(), ref) < TOL
+    if cout % 4:  # (moments need an NHWC output with 4-aligned channels: the buffer is marked incomplete)
+        assert getattr(ost, "_nps_incomplete", False)
+        return
+    assert not getattr(ost, "_nps_incomplete", False)
+    got = ost.sum(1).cpu()
+    want = torch.stack([ref.sum((1, 2, 3)), (ref * ref).sum((1, 2, 3))], 1)
+    assert rel_l2(got, want) < TOL
