@@ -185,6 +185,10 @@ int nps_space_to_depth(const float* x, float* out, int B, int H, int W, int C, i
                        void* stream);
 /* Fill TH/TW/lattice/waves of `a` for its shape; returns the LDS bytes used. */
 int nps_conv2d_plan(nps_conv2d_t* a);
+/* Highest byte (exclusive) of the packed split-fp16 weight that the launch of the planned *a reads (host-only
+ * arithmetic of the kernel the launcher picks; must be <= 4 * nps_conv2d_packed_size).  Replaces no reference
+ * interface: a check of this build's packing (tests/test_cabi.py). */
+long nps_conv2d_x3_weight_span(const nps_conv2d_t* a);
 int nps_conv2d_fwd(const nps_conv2d_t* a, void* stream);
 
 /* Materialise a virtual frame: out[B][Hin][Win][Cin] = act(GN(frame)) using the prologue fields

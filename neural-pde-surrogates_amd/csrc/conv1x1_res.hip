@@ -303,15 +303,36 @@ void launch(const nps_conv2d_t& a, unsigned grid, int ng, int nres, hipStream_t 
 
 }  // namespace
 
-int nps_launch_conv1x1_res(const nps_conv2d_t& a, int all, hipStream_t s) {
+int nps_conv1x1_res_plan(const nps_conv2d_t& a, int all, int* ncb, int* ng, int* nres) {
     // all = 0: only the planar (NCHW) 1x1s with 192 < Cout <= 256 — the decoder's pre-output, which the LDS-staged
     // kernel (Cout <= 192, NHWC) cannot take and the co-block kernel ran at 1.4 TB/s; all = 1 (dev knob
     // NPS_X1_RES=1): every eligible 1x1
     if (!all && !(a.out_nchw && a.Cout > 192 && a.Cout <= 256)) return 0;
-    if (a.KH * a.KW != 1 || a.accumulate || a.addend1 != nullptr) return 0;
+    if (a.KH * a.KW != 1 || a.accumulate || a.addend1 != nullptr || a.gn_stats != nullptr || a.pre_act != 0) return 0;
     if (a.out_nchw && (a.addend0 != nullptr || a.out_stats != nullptr)) return 0;
     if (a.out_stats != nullptr && a.Cout > 192) return 0;  // (moments of the stored values: addend / act included)
     if ((long)a.B * ((a.Hout * a.Wout + 31) / 32) >= (1L << 31)) return 0;
+    const int nr = x1r_nres(a.Cin);
+    const int lmax = 160 * 1024;
+    int c = 0, g = 0;
+    if (a.Cout <= 192 && x1r_lds_bytes(6, nr) <= lmax) {
+        c = 6, g = 1;
+    } else if (a.Cout <= 192 && x1r_lds_bytes(3, nr) <= lmax) {
+        c = 3, g = 2;
+    } else if (a.Cout > 192 && a.Cout <= 256 && x1r_lds_bytes(4, nr) <= lmax) {
+        c = 4, g = 2;
+    } else {
+        return 0;
+    }
+    *ncb = c;
+    *ng = g;
+    *nres = nr;
+    return 1;
+}
+
+int nps_launch_conv1x1_res(const nps_conv2d_t& a, int all, hipStream_t s) {
+    int ncb = 0, ng = 0, nres = 0;
+    if (!nps_conv1x1_res_plan(a, all, &ncb, &ng, &nres)) return 0;
     static long gx = 0;
     if (gx == 0) {
         int dev = 0, n = 0;
@@ -320,16 +341,11 @@ int nps_launch_conv1x1_res(const nps_conv2d_t& a, int all, hipStream_t s) {
             n = 256;
         gx = n & ~15;  // persistent: one work-group per CU, a multiple of 16 (8 XCDs x 2 channel groups)
     }
-    const int nres = x1r_nres(a.Cin);
-    const int lmax = 160 * 1024;
-    if (a.Cout <= 192 && x1r_lds_bytes(6, nres) <= lmax) {
+    if (ncb == 6)
         launch<6, 3>(a, (unsigned)gx, 1, nres, s);
-    } else if (a.Cout <= 192 && x1r_lds_bytes(3, nres) <= lmax) {
+    else if (ncb == 3)
         launch<3, 4>(a, (unsigned)gx, 2, nres, s);
-    } else if (a.Cout > 192 && a.Cout <= 256 && x1r_lds_bytes(4, nres) <= lmax) {
+    else
         launch<4, 4>(a, (unsigned)gx, 2, nres, s);
-    } else {
-        return 0;
-    }
     return 1;
 }

@@ -312,6 +312,8 @@ int nps_launch_conv2d_x3(const nps_conv2d_t& a, int lds, hipStream_t s);
 // split-fp16 1x1 with resident weights (conv1x1_res.hip): launches and returns 1 when the conv is eligible, else 0
 // (all = 0: the planar 192 < Cout <= 256 decoder shape only)
 int nps_launch_conv1x1_res(const nps_conv2d_t& a, int all, hipStream_t s);
+// its choice: 1 (and the kernel's channel blocks per group, groups, resident chunks) when it would launch
+int nps_conv1x1_res_plan(const nps_conv2d_t& a, int all, int* ncb, int* ng, int* nres);
 // conv2d.hip: partial maxima of |x| (one per work-group, at most max_parts) to parts[]; returns their count
 // (the packed-weight trailer; nps_absmax writes a range tag)
 int nps_absmax_parts(const float* x, long n, float* parts, int max_parts, hipStream_t s);

@@ -2599,3 +2599,42 @@ extern "C" int nps_x3_stamps(unsigned long long* host, int n) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(x3_stamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -1;
 }
 #endif
+
+// Highest byte (exclusive) of the packed weight that the split-fp16 launch of *a (after nps_conv2d_plan) reads, from
+// the index arithmetic of the kernel the launcher picks for it (an over-read must be caught by a
+// host check, not by allocation luck).  tests/test_cabi.py sweeps shapes against nps_conv2d_packed_size.
+extern "C" long nps_conv2d_x3_weight_span(const nps_conv2d_t* ap) {
+    NPS_CHECK_ARG(ap != nullptr && ap->precision == NPS_PREC_X3F16, "conv2d_x3_weight_span: split-fp16 args only");
+    const nps_conv2d_t& a = *ap;
+    const int nt = a.KH * a.KW;
+    const long ncb = packed_ncb(a.Cout);      // 32-channel blocks per (chunk, tap) group: a multiple of 6
+    const long gstride = ncb * 2048;          // bytes per (chunk, tap) group
+    long span = (long)(packed_body(a.Cout, a.Cin, nt) + 1) * 4;  // the trailer's max|w| (weight scale)
+    auto top = [&](long v) { span = v > span ? v : span; };
+    if (nt == 1) {
+        const long nst = (a.Cin + 2 * CK - 1) / (2 * CK);  // 32-channel stages: chunks 2 st, 2 st + 1
+        const char* e = getenv("NPS_X1_RES");
+        const int all = (e != nullptr && e[0] == '1') ? 1 : 0;
+        int rncb = 0, rng = 0, rnres = 0;
+        const bool pro = a.gn_stats != nullptr || a.pre_act != 0;
+        if (!pro && nps_conv1x1_res_plan(a, all, &rncb, &rng, &rnres)) {
+            // conv1x1_res_kernel: chunks [0, nres), blocks [0, ng * NCB) (group grp at grp * NCB)
+            top((rnres - 1) * gstride + (long)rng * rncb * 2048);
+        } else if (a.Cout <= 192) {
+            // conv1x1_wl_kernel<6, *>: wfetch(min(st + 2, last)) -> chunks 2 last + 1, 6 blocks of the chunk
+            top((2 * nst - 1) * gstride + 6 * 2048);
+        } else {
+            // conv1x1_x3_kernel: wave block min(cob, ncb / 2 - 1) x 2 blocks, chunks 2 st + k
+            top((2 * nst - 1) * gstride + ncb * 2048);
+        }
+    } else {
+        const long nstages = (a.Cin + CK - 1) / CK;
+        const long G = nstages * nt;                  // K-groups; loads clamp to G - 1 (gclamp)
+        const bool wide = x3_wide_tile(a);
+        const long nco = wide ? 192 : 64;             // channels per work-group tile
+        const long ncob = (a.Cout + nco - 1) / nco;
+        top((G - 1) * gstride + ncob * (nco / 32) * 2048);
+    }
+    if (a.nphase > 1) span += (long)(a.nphase - 1) * a.phase_wstride * 4;  // phase p's weight at p * phase_wstride floats
+    return span;
+}

@@ -94,6 +94,7 @@ _SIGS = {
     "nps_conv2d_x1_dma": (_i, [ctypes.POINTER(Conv2dArgs)]),
     "nps_absmax": (_i, [_vp, _l, _vp, _vp]),
     "nps_conv2d_plan": (_i, [ctypes.POINTER(Conv2dArgs)]),
+    "nps_conv2d_x3_weight_span": (_l, [ctypes.POINTER(Conv2dArgs)]),
     "nps_conv2d_fwd": (_i, [ctypes.POINTER(Conv2dArgs), _vp]),
     "nps_frame_pack": (_i, [ctypes.POINTER(Conv2dArgs), _vp, _vp]),
     "nps_space_to_depth": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp]),

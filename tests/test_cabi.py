@@ -59,3 +59,53 @@ def test_ops_refuse_cpu_tensors():
     from nps_hip import ops
     with pytest.raises(RuntimeError, match="MI355X"):
         ops.nchw_to_nhwc(torch.zeros(1, 2, 3, 4))
+
+
+def _plan_args(Cin, Cout, k, H=40, W=36, pad=0, out_nchw=0, gn=False, nphase=1):
+    import nps_hip
+    from nps_hip import ops
+    a = nps_hip.Conv2dArgs()
+    a.nsrc = 1
+    a.src[0].ptr, a.src[0].C, a.src[0].H, a.src[0].W = 0x1000, Cin, H, W
+    a.B, a.Hin, a.Win, a.Cin = 2, H, W, Cin
+    a.KH = a.KW = k
+    a.stride, a.dil, a.pad_y, a.pad_x = 1, 1, pad, pad
+    a.Hout, a.Wout = H + 2 * pad - k + 1, W + 2 * pad - k + 1
+    a.Cout, a.out_C, a.out_H, a.out_W, a.out_os = Cout, Cout, a.Hout, a.Wout, 1
+    a.out_nchw = out_nchw
+    a.precision = ops.PREC_X3F16
+    if gn:
+        a.gn_stats, a.gn_gamma, a.gn_beta, a.gn_groups, a.gn_eps, a.pre_act = 0x2000, 0x3000, 0x4000, 1, 1e-5, 1
+    if nphase > 1:
+        a.nphase, a.phase_wstride = nphase, nps_hip.lib.nps_conv2d_packed_size(Cout, Cin, k * k)
+    return a
+
+
+@pytest.mark.parametrize("k", [1, 2, 3])
+def test_x3_weight_reads_stay_inside_the_packing(k):
+    """every split-fp16 conv launch reads its packed weight only inside the buffer, for the kernel the
+    launcher picks (host arithmetic of nps_conv2d_x3_weight_span: block / chunk / K-group indices of each kernel,
+    checked against nps_conv2d_packed_size) — at the packing boundaries (Cout 193, 385, 577: one past a 192-channel
+    pack; 225, 256: the resident 1x1's two channel groups) and with channel tails (Cin 20, 36, 196, 388)."""
+    import nps_hip
+    lib = nps_hip.lib
+    checked = 0
+    for Cout in (4, 32, 64, 75, 128, 160, 192, 193, 196, 225, 256, 385, 388, 577, 600):
+        for Cin in (4, 16, 20, 36, 84, 192, 196, 388):
+            variants = [dict()]
+            if k == 1:
+                variants += [dict(out_nchw=1), dict(gn=True)]
+            if k == 3:
+                variants += [dict(gn=True), dict(pad=1)]
+            if k == 2:
+                variants += [dict(nphase=4)]
+            for v in variants:
+                if v.get("gn") and (k == 1 and Cout > 192):
+                    continue  # (a 1x1 prologue needs the LDS-weight kernel: the host materialises the frame otherwise)
+                a = _plan_args(Cin, Cout, k, **v)
+                assert lib.nps_conv2d_plan(ctypes.byref(a)) >= 0, (Cin, Cout, k, v)
+                span = lib.nps_conv2d_x3_weight_span(ctypes.byref(a))
+                size = 4 * lib.nps_conv2d_packed_size(Cout, Cin, k * k) * v.get("nphase", 1)
+                assert 0 < span <= size, (Cin, Cout, k, v, span, size)
+                checked += 1
+    assert checked > 100
