@@ -294,12 +294,13 @@ __host__ __device__ inline int x3_ring_bytes(const nps_conv2d_t& a) {
     return X3_NST * ((g.PH * g.PW * X3_PIXB + 15) & ~15);
 }
 // bytes of the patch ring + epilogue tile region: 64-channel tiles reuse the ring for the tile (store phase
-// after the main loop); wide tiles keep the tile in a region of its own behind the ring, because their
-// consumer waves store tile t during tile t + 1's main loop (conv2d_x3_kernel, "spread store")
+// after the main loop); wide tiles keep the tile in a region of its own behind the ring, because tile t is
+// stored during tile t + 1's main loop (conv2d_x3_kernel: by the producer waves, or by the consumers in the
+// spread-store dev variant).  3x3 wide: 48 960 + 100 352 B.
 __host__ __device__ inline int x3_region_bytes(const nps_conv2d_t& a) {
     const int ring = x3_ring_bytes(a);
     const int tile = a.TH * a.TW * x3_tpitch(a) * 4;
-    if (NPS_X3_SPREAD && x3_wide_tile(a)) return ring + tile;
+    if (x3_wide_tile(a)) return ring + tile;
     return ring > tile ? ring : tile;
 }
 // 128-B header + region + the bias table of the LDS store phase (Cout floats, 16-B padded)

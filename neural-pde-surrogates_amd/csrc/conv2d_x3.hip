@@ -358,7 +358,7 @@ __device__ __forceinline__ void x3_consume_m16(const nps_conv2d_t& a, const Geo&
 // owns channels [96 (w & 1), +96) (3 co blocks) x pixels [64 (w >> 1), +64) (2 pixel blocks).  The staged
 // patch then feeds all 192 channels: 3x less producer work (fetch, split, prologue) and patch traffic per
 // MFMA than three 64-channel work-groups re-staging the same patch.
-template <int NTAPS, int PB, bool PRO, bool WIDE = false>
+template <int NTAPS, int PB, bool PRO, bool WIDE = false, bool PST = false>
 __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
     constexpr int KWT = NTAPS == 25 ? 5 : (NTAPS == 9 ? 3 : (NTAPS == 4 ? 2 : 1));
     constexpr int CBW = WIDE ? 3 : 2;          // 32-channel co blocks per consumer wave
@@ -368,6 +368,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
     constexpr int MAXP = (x3_patch_px_max(NTAPS, TILE_PX) * 4 + 255) / 256;
     constexpr bool SPREAD = WIDE && NPS_X3_SPREAD;  // wide tiles: spread store (dev knob: the store phase)
     constexpr bool M16 = WIDE && !SPREAD && NPS_X3_M16;  // wide tiles: tap-paired 16x16x32 consumers
+    static_assert(!PST || (WIDE && !SPREAD && !M16), "producer-side store: wide 32x32x16 tiles only");
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const Geo g = make_geo(a);
@@ -592,6 +593,182 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
         decode(l, fcob, fb, fy0, fx0, fph);
         unsigned m0 = issue(0, r0);
         unsigned m1 = issue(min(1, last), r1);
+        if constexpr (PST) {
+            // Producer-side store (wide tiles): the consumers drop tile t into the tile region Tw (its own LDS
+            // region behind the ring) and go straight on to tile t + 1; the producers store tile t from Tw during
+            // tile t + 1's stage iterations, in NCH chunks of 4 items per thread (item = one pixel's 4 channels,
+            // 16 B; consecutive threads walk a pixel's NCO channels: x3_store_phase's coalesced order and float
+            // order).  Chunk c's operand loads (addends, the accumulated output) are issued at stage s(c), after
+            // that stage's patch fetch, and the chunk is finished at the next stage iteration, after the commit —
+            // so no wait of the in-order vmcnt queue stalls a patch fetch.  The last chunk finishes before the
+            // tile's last stage barrier, after which the consumers overwrite Tw.  No store phase: per tile
+            // 1 + nstages barriers on both sides (the consumers' MFMAs run while the tile is stored).
+            constexpr int PQ = NCO / 4;                  // channel quads per pixel
+            constexpr int PITEMS = TILE_PX * PQ / 256;  // items per producer thread and tile (24)
+            static_assert(PITEMS % 4 == 0, "4-item chunks");
+            constexpr int NCH = PITEMS / 4;
+            const float* Tw = reinterpret_cast<const float*>(ring + x3_ring_bytes(a));
+            // (host-checked: at most one operand, the accumulated output or addend0)
+            const float* opp = a.accumulate ? a.out : a.addend0;
+            const bool oper = opp != nullptr;
+            const bool pipe = nstages > NCH;  // one chunk per stage, loads a stage ahead
+            int p_b = 0, p_cob = 0, p_oy0 = 0, p_ox0 = 0, p_ph = 0;  // the tile being stored
+            bool pend = false;
+            int fl_c = -1;  // chunk whose operand loads are in flight
+            double ps1 = 0.0, ps2 = 0.0;
+            f32x4 iop[4];
+            auto item_at = [&](int k, int& P, int& q, size_t& off, bool& ok) {
+                const int i = ptid + 256 * k;
+                P = i / PQ;
+                q = i - P * PQ;
+                const int co0 = p_cob * NCO + q * 4;
+                const int ti = P / a.TW, tj = P - (P / a.TW) * a.TW;
+                const int oy = p_oy0 + ti * g.T, ox = p_ox0 + tj * g.T;
+                const int dy = oy * a.out_os + a.out_off_y + (p_ph >> 1), dx = ox * a.out_os + a.out_off_x + (p_ph & 1);
+                ok = co0 < a.Cout && oy < a.Hout && ox < a.Wout && dy >= 0 && dy < a.out_H && dx >= 0 && dx < a.out_W;
+                off = ok ? (((size_t)p_b * a.out_H + dy) * a.out_W + dx) * a.out_C + co0 : 0;
+            };
+            auto chunk_issue = [&](int c) {
+                if (!oper) return;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    int P, q;
+                    size_t off;
+                    bool ok;
+                    item_at(4 * c + j, P, q, off, ok);
+                    // out-of-range items read the zero page (no branch around a load)
+                    iop[j] = *reinterpret_cast<const f32x4*>(ok ? opp + off : x3_zero16);
+                }
+            };
+            auto chunk_finish = [&](int c) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    int P, q;
+                    size_t off;
+                    bool ok;
+                    item_at(4 * c + j, P, q, off, ok);
+                    const f32x4 acc = *reinterpret_cast<const f32x4*>(Tw + P * (NCO + 4) + q * 4);
+                    const f32x4 bi = *reinterpret_cast<const f32x4*>(btab + (ok ? p_cob * NCO + q * 4 : 0));
+                    f32x4 r;
+                    float f1 = 0.f, f2 = 0.f;
+                    if (!oper) {  // x3_store_phase's operand-free form
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            float v = acc[e] + bi[e];
+                            if (a.act == 1) v = nps::gelu_erf(v);
+                            r[e] = v;
+                            pmax = ok ? fmaxf(pmax, fabsf(v)) : pmax;
+                            f1 += v;
+                            f2 += v * v;
+                        }
+                    } else if (a.accumulate) {  // x3_store_phase's float order with zero addends
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            float v = acc[e] + bi[e];
+                            if (!a.add_after_act) v = v + 0.f + 0.f;
+                            if (a.act == 1) v = nps::gelu_erf(v);
+                            if (a.add_after_act) v = v + 0.f + 0.f;
+                            v += iop[j][e];
+                            r[e] = v;
+                            pmax = ok ? fmaxf(pmax, fabsf(v)) : pmax;
+                            f1 += v - iop[j][e];
+                            f2 += (v - iop[j][e]) * (v + iop[j][e]);
+                        }
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            float v = acc[e] + bi[e];
+                            if (!a.add_after_act) v = v + iop[j][e] + 0.f;
+                            if (a.act == 1) v = nps::gelu_erf(v);
+                            if (a.add_after_act) v = v + iop[j][e] + 0.f;
+                            r[e] = v;
+                            pmax = ok ? fmaxf(pmax, fabsf(v)) : pmax;
+                            f1 += v;
+                            f2 += v * v;
+                        }
+                    }
+                    float* dst = ok ? a.out + off : x3_sink + 4 * (tid & 63);
+                    *reinterpret_cast<f32x4*>(dst) = r;
+                    ps1 += ok ? (double)f1 : 0.0;
+                    ps2 += ok ? (double)f2 : 0.0;
+                }
+            };
+            auto tile_done = [&]() {
+                stats_publish(a, p_b, ps1, ps2);  // the tile's moments: one pair per wave (no-op without out_stats)
+                ps1 = ps2 = 0.0;
+                pend = false;
+            };
+            for (;;) {
+                const int tcob = fcob, tb = fb, ty0 = fy0, tx0 = fx0, tph = fph;  // tile computed now
+                commit(0, r0, m0);
+                if (nstages > 1) commit(1, r1, m1);
+                unsigned m = issue(min(2, last), r0);
+                barrier();  // (the consumers' previous tile is in Tw)
+                const int ln = l + (int)gridDim.x;
+                const bool more = ln < nwg;
+                bool got0 = false, got1 = false;
+                for (int st = 0; st < nstages; ++st) {
+                    if (st + 2 < nstages) commit(st + 2, r0, m);
+                    if (pend) {
+                        if (pipe) {
+                            if (fl_c >= 0) chunk_finish(fl_c);
+                            fl_c = -1;
+                        } else {
+                            for (int c = 0; c < NCH; ++c)
+                                if ((c * nstages) / NCH == st) {
+                                    chunk_issue(c);
+                                    chunk_finish(c);
+                                }
+                        }
+                    }
+                    // the next patch stage, or the next tile's first two (as the spread-store loop below)
+                    if (st + 3 <= last) {
+                        m = issue(st + 3, r0);
+                    } else if (more && st == last - 2) {
+                        decode(ln, fcob, fb, fy0, fx0, fph);
+                        cur_src = -1;
+                        m0 = issue(0, r0);
+                        got0 = true;
+                    } else if (got0 && st == last - 1) {
+                        m1 = issue(min(1, last), r1);
+                        got1 = true;
+                    }
+                    if (pend && pipe) {
+#pragma unroll 1
+                        for (int c = 0; c < NCH; ++c)
+                            if ((c * (nstages - 1)) / NCH == st) {
+                                chunk_issue(c);
+                                fl_c = c;
+                            }
+                    }
+                    if (pend && st == last) tile_done();
+                    barrier();
+                }
+                p_b = tb;
+                p_cob = tcob;
+                p_oy0 = ty0;
+                p_ox0 = tx0;
+                p_ph = tph;
+                pend = true;
+                if (!more) break;
+                if (!got0) {
+                    decode(ln, fcob, fb, fy0, fx0, fph);
+                    cur_src = -1;
+                    m0 = issue(0, r0);
+                }
+                if (!got1) m1 = issue(min(1, last), r1);
+                l = ln;
+            }
+            barrier();  // the last tile is in Tw
+#pragma unroll 1
+            for (int c = 0; c < NCH; ++c) {
+                chunk_issue(c);
+                chunk_finish(c);
+            }
+            tile_done();
+            nps::tag_publish(a.out_tag, pmax, nps::wave_salt());
+            return;
+        }
         if constexpr (SPREAD) {
             // Wide tiles: the consumers store each tile during the next one's main loop, so the producers have
             // no store phase: per tile 1 + nstages barriers, and the next tile's first two stages are fetched
@@ -902,6 +1079,25 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
         if (wave == 0 && lane == 0 && l < (1 << 16)) x3_stamps[l * 16 + 6] = bar_cycles;
         bar_cycles = 0;
 #endif
+        if constexpr (PST) {
+            // the tile into Tw (the producers store it during the next tile's stages, or after the last one);
+            // no barrier: the next tile's first barrier publishes it
+#pragma unroll
+            for (int pb = 0; pb < PBW; ++pb) {
+                const int P = px0 + pb * 32 + (lane & 31);
+#pragma unroll
+                for (int cb = 0; cb < CBW; ++cb)
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) {
+                        const f32x4 v = {acc[cb][pb][4 * m] * inv, acc[cb][pb][4 * m + 1] * inv,
+                                         acc[cb][pb][4 * m + 2] * inv, acc[cb][pb][4 * m + 3] * inv};
+                        *reinterpret_cast<f32x4*>(Tw + P * (NCO + 4) + cw0 + cb * 32 + 8 * m + 4 * h) = v;
+                    }
+            }
+            X3_STAMP(3);
+            X3_RSTAMP(5);
+            continue;
+        }
         if constexpr (SPREAD) {
             // items of the previous tile the main loop had no K-group for (small Cin), then this tile's block
             // into Tw: the wave's own block only, which it alone reads back — no barrier
@@ -979,6 +1175,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
         X3_STAMP(3);
         X3_RSTAMP(5);
     }
+    if constexpr (PST) barrier();  // the last tile is in Tw: the producers store it
     if constexpr (SPREAD) {  // the last tile: no next main loop to spread it over
         while (sp_n > 0) {
             sp_issue();
@@ -2365,15 +2562,15 @@ __global__ __launch_bounds__(512) void conv1x1_dma_kernel(const nps_conv2d_t a) 
 }
 #endif  // NPS_X1_DMA_KERNEL
 
-template <int NT, int PB, bool PRO = false, bool WIDE = false>
+template <int NT, int PB, bool PRO = false, bool WIDE = false, bool PST = false>
 void launch_x3_one(const nps_conv2d_t& a, unsigned nwg, int lds, hipStream_t s) {
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)conv2d_x3_kernel<NT, PB, PRO, WIDE>,
+        (void)hipFuncSetAttribute((const void*)conv2d_x3_kernel<NT, PB, PRO, WIDE, PST>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_set = true;
     }
-    conv2d_x3_kernel<NT, PB, PRO, WIDE><<<nwg, 512, lds, s>>>(a);
+    conv2d_x3_kernel<NT, PB, PRO, WIDE, PST><<<nwg, 512, lds, s>>>(a);
 }
 
 #ifdef NPS_X3F_KERNEL
@@ -2566,6 +2763,23 @@ int nps_launch_conv2d_x3(const nps_conv2d_t& a, int lds, hipStream_t s) {
         return 0;
     }
 #endif
+    static int pst = -1;  // dev knob NPS_X3_PSTORE=1: wide tiles stored by the producers during the next tile
+    if (pst < 0) {        // instead of the store phase (5 % slower: profiles/r5/experiments/x3_producer_store_ab.txt)
+        const char* e = getenv("NPS_X3_PSTORE");
+        pst = (e != nullptr && e[0] == '1') ? 1 : 0;
+    }
+    // (the producer-side store takes at most one epilogue operand: the accumulated output or addend0)
+    if (wide && pst && !NPS_X3_SPREAD && !NPS_X3_M16 && a.addend1 == nullptr && !(a.accumulate && a.addend0 != nullptr)) {
+        if (a.KH * a.KW == 9)
+            pro ? launch_x3_one<9, 2, true, true, true>(a, grid, lds, s)
+                : launch_x3_one<9, 2, false, true, true>(a, grid, lds, s);
+        else if (a.KH * a.KW == 4)
+            launch_x3_one<4, 2, false, true, true>(a, grid, lds, s);
+        else
+            NPS_CHECK_ARG(false, "conv2d_fwd (split-fp16): wide tiles are 2x2 / 3x3 only");
+        NPS_CHECK_LAUNCH("conv2d_fwd (split-fp16, wide, producer-side store)");
+        return 0;
+    }
     if (wide) {
         if (a.KH * a.KW == 9)
             pro ? launch_x3_one<9, 2, true, true>(a, grid, lds, s) : launch_x3_one<9, 2, false, true>(a, grid, lds, s);

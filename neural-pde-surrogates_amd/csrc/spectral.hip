@@ -10,6 +10,7 @@
 #include "nps_common.hpp"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace {
 
@@ -102,6 +103,93 @@ __global__ void dft_w_kernel(nps_conv2d_t a, int m2, float2* __restrict__ X1, fl
                     const int kk = kb + k;
                     if (c2r_adj && !((kk == 0) || (2 * kk == W))) f *= 2.f;
                     X1[((size_t)(b * H + h) * m2 + kk) * C + c] = make_float2(re[k] * f, im[k] * f);
+                }
+            }
+        }
+    }
+}
+
+// The W-pass DFT as an exact-fp32 MFMA GEMM per image row (b, h): X1[k][c] = sum_w T[k][w] x[w][c], M = the 32 rows
+// [cos 2 pi k w / W (k < m2) | sin ... at row 16 + k] (zero past m2), N = 32 channels, K = 2 pixels per
+// v_mfma_f32_32x32x2_f32.  The VALU kernel above reads its twiddles as LDS broadcasts (6 ds_read_b128 per pixel for
+// 24 FMAs per channel), which bound it near 3 TB/s; here each lane reads ONE twiddle float per 2 pixels and reuses it
+// for 4 MFMAs.  A wave owns (row, 128-channel group): lane l loads the 16-B channel quad 4 (l % 32) .. +3 of pixel
+// w0 + l / 32 (two 512-B runs per load), and element i of the quad is column l % 32 of accumulator block i — block i
+// holds channels 4 n + i, a channel permutation undone at the store.  Persistent work-groups build the [W][32] table
+// once.  Same exact-fp32 products as the VALU chain (MI355X_MICROARCH: f32-input MFMA is bit-exact fmaf), another
+// summation order.  Accumulator lane l, register r: column l % 32, row 8 (r / 4) + 4 (l / 32) + r % 4 — bin k's cos
+// row k and sin row 16 + k sit in the same lane (registers r and r + 8).
+__global__ __launch_bounds__(256) void dft_w_mfma_kernel(nps_conv2d_t a, int m2, float2* __restrict__ X1, float scale,
+                                                         int c2r_adj, int nrows) {
+    extern __shared__ __attribute__((aligned(16))) float twm[];  // [W][32]
+    const int W = a.Win, H = a.Hin, C = a.Cin;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
+    for (int i = threadIdx.x; i < W * 32; i += 256) {
+        const int w = i >> 5, m = i & 31;
+        const int k = m & 15;
+        float v = 0.f;
+        if (k < m2) {
+            const float2 t = twiddle(k, w, W);  // (cos, sin)
+            v = m < 16 ? t.x : t.y;
+        }
+        twm[i] = v;
+    }
+    __syncthreads();
+    const int ng = (C + 127) / 128;
+    const int ntask = nrows * ng;
+    for (int task = blockIdx.x * 4 + wave; task < ntask; task += gridDim.x * 4) {
+        const int row = task / ng, g = task - (task / ng) * ng;
+        const int b = row / H, hh = row - (row / H) * H;
+        // this lane's channel quad: source pointer at pixel 0 and the source's pixel stride (sources are 4-aligned)
+        const int c0 = g * 128 + 4 * l32;
+        const float* base = nullptr;
+        int sC = 0, lo = 0;
+        for (int si = 0; si < a.nsrc; ++si) {
+            if (c0 >= lo && c0 < lo + a.src[si].C) {
+                sC = a.src[si].C;
+                base = a.src[si].ptr + ((size_t)(b * H + hh) * W) * sC + (c0 - lo);
+            }
+            lo += a.src[si].C;
+        }
+        const bool ok = c0 < C && base != nullptr;
+        f32x16 acc[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+        constexpr int U = 8;  // K-steps (2 pixels each) per batch of independent loads
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        int w0 = 0;
+        for (; w0 + 2 * U <= W; w0 += 2 * U) {
+            f32x4 xv[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                xv[u] = ok ? *reinterpret_cast<const f32x4*>(base + (size_t)(w0 + 2 * u + h) * sC) : z;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const float t = twm[(w0 + 2 * u + h) * 32 + l32];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(t, xv[u][j], acc[j], 0, 0, 0);
+            }
+        }
+        for (; w0 < W; w0 += 2) {  // (W % 2 == 0: host-checked)
+            const float t = twm[(w0 + h) * 32 + l32];
+            const f32x4 xq = ok ? *reinterpret_cast<const f32x4*>(base + (size_t)(w0 + h) * sC) : z;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(t, xq[j], acc[j], 0, 0, 0);
+        }
+        float2* dst = X1 + (size_t)(b * H + hh) * m2 * C;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int c = g * 128 + 4 * l32 + j;  // block j, column l32
+            if (c >= C) continue;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                const int k = 8 * (r >> 2) + 4 * h + (r & 3);  // bin of cos row k / sin row 16 + k
+                if (k < m2) {
+                    float f = scale;
+                    if (c2r_adj && !((k == 0) || (2 * k == W))) f *= 2.f;
+                    dst[(size_t)k * C + c] = make_float2(acc[j][r] * f, -acc[j][r + 8] * f);
                 }
             }
         }
@@ -743,6 +831,29 @@ size_t idft_w_lds(int m2, int W) {
 template <typename TIn = float>
 void launch_dft_w(dim3 grid, int bs, size_t lds, hipStream_t s, const nps_conv2d_t& a, int m2, float2* X1, float scale,
                   int c2r_adj) {
+    static int mfma = -1;  // dev knob NPS_DFTW_MFMA=0: the VALU W-pass
+    if (mfma < 0) {
+        const char* e = getenv("NPS_DFTW_MFMA");
+        mfma = (e != nullptr && e[0] == '0') ? 0 : 1;
+    }
+    bool quads = true;  // every source 4-channel aligned: a lane's 16-B quad lies in one source
+    for (int i = 0; i < a.nsrc; ++i) quads = quads && (a.src[i].C & 3) == 0;
+    if (std::is_same<TIn, float>::value && mfma && quads && m2 <= 16 && (a.Win & 1) == 0 &&
+        a.Win * 32 * 4 <= 64 * 1024) {
+        static int ncu = 0;
+        if (ncu == 0) {
+            int dev = 0, n = 0;
+            if (hipGetDevice(&dev) != hipSuccess ||
+                hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+                n = 256;
+            ncu = n;
+        }
+        const int nrows = (int)(grid.x * grid.y);  // (H, B) rows
+        const long tasks = (long)nrows * ((a.Cin + 127) / 128);
+        const int g = (int)((tasks + 3) / 4 < 2 * ncu ? (tasks + 3) / 4 : 2 * ncu);  // persistent, every WG resident
+        dft_w_mfma_kernel<<<g, 256, (size_t)a.Win * 32 * 4, s>>>(a, m2, X1, scale, c2r_adj, nrows);
+        return;
+    }
     switch (kc_for(m2)) {
         case 4: dft_w_kernel<4, TIn><<<grid, bs, lds, s>>>(a, m2, X1, scale, c2r_adj); break;
         case 8: dft_w_kernel<8, TIn><<<grid, bs, lds, s>>>(a, m2, X1, scale, c2r_adj); break;
