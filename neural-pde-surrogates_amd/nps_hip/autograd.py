@@ -87,6 +87,9 @@ def wgrad(a: torch.Tensor, x: torch.Tensor, KH: int, KW: int, dil=1, pad=(0, 0),
         e1.record()
         ops.conv_probe.append((e0, e1, 2.0 * B * Ha * Wa * M * N * KH * KW, (arith, KH * KW, 0),
                                4.0 * (a.numel() + x.numel() + g.numel())))
+        if ops.conv_shape_log is not None:  # (tools/call_shapes.py --train)
+            ops.conv_shape_log.append(dict(cin=N, cout=M, k=(KH, KW), hw=(Hx, Wx), out=(Ha, Wa), B=B, nsrc=1,
+                                           acc=not store, addends=0, act=0, gn=False, pre_act=0, stats=False))
     else:
         launch()
     return g

@@ -3,7 +3,7 @@
 # rocprof, and the N=2 rehearsals of `bench.py --gpus 2` (the driver's own command form; ranks share cuda:0
 # over gloo: NPS_BENCH_REHEARSAL=1, never a reported number).  Outputs: gpurun_out/${TAG}_*.
 # usage: tools/gpu_pass.sh TAG [steps...]
-#   steps: tests sel($TESTSEL) pmc bench prof b2 b2prof train trainprof tb2prof c5 c5prof reh rehroll smoke
+#   steps: tests sel($TESTSEL) pmc bench prof b2 b2prof train trainprof tb2prof c2 c4 c5 c5prof reh rehroll smoke
 set -o pipefail
 TAG=${1:-r5}; shift
 STEPS="${@:-tests bench prof b2 train c5 reh}"
@@ -31,6 +31,8 @@ for s in $STEPS; do
              > ${O}_tprof.log 2>&1 || { echo "train prof failed"; tail -20 ${O}_tprof.log; exit 1; } ;;
     tb2prof) timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d ${O}_tb2prof -o run -- python3 bench.py --mode train --steps 5 --warmup 2 --global-batch 2 --cpu-calls 0 \
              > ${O}_tb2prof.log 2>&1 || { echo "train b2 prof failed"; tail -20 ${O}_tb2prof.log; exit 1; } ;;
+    c2)    timeout -k 10 300 python -u bench.py --res 128 --num-c 1 --fno-modes 12 --cpu-calls 0 > ${O}_c2.json 2> ${O}_c2.err || { echo "c2 failed"; tail -20 ${O}_c2.err; exit 1; }; tail -c 300 ${O}_c2.json ;;
+    c4)    timeout -k 10 300 python -u bench.py --model drn --num-c 1 --cpu-calls 0 > ${O}_c4.json 2> ${O}_c4.err || { echo "c4 failed"; tail -20 ${O}_c4.err; exit 1; }; tail -c 300 ${O}_c4.json ;;
     c5)    timeout -k 10 400 python -u bench.py --model ufno3d --dtype bf16 > ${O}_c5.json 2> ${O}_c5.err || { echo "c5 failed"; tail -20 ${O}_c5.err; exit 1; }; tail -c 300 ${O}_c5.json ;;
     c5prof) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d ${O}_c5prof -o run -- python3 bench.py --model ufno3d --dtype bf16 --steps 3 --warmup 1 --cpu-calls 0 \
              > ${O}_c5prof.log 2>&1 || { echo "c5 prof failed"; tail -20 ${O}_c5prof.log; exit 1; } ;;
