@@ -1,3 +1,5 @@
+"""Dev tool (GPU box): histogram of the nps_stats_sum call sites (caller chain, parts, sub-slots) of one C3 model
+call at B = 2.  python tools/stats_sum_sites.py"""
 import collections, os, sys, traceback
 ROOT = os.environ.get("GRAFT_REPO_ROOT", "/root/repo")
 sys.path[:0] = [ROOT, os.path.join(ROOT, "neural-pde-surrogates_amd")]
