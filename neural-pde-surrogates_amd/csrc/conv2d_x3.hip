@@ -401,6 +401,17 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
     // first barrier of the tile loop
     float* btab = reinterpret_cast<float*>(ring + x3_region_bytes(a));
     for (int c = tid; c < a.Cout; c += 512) btab[c] = a.bias != nullptr ? a.bias[c] : 0.f;
+#if NPS_X3_ABL == 9
+    // dev ablation (wrong results, speed only): the wide consumers read their weight fragments from LDS — 3 K-groups
+    // (36 KiB of real packed weight bits, so the MFMA operands toggle as in the real stream) behind the store-phase
+    // tile, in the part of the wide-tile region nothing else touches — the ceiling of a weights-through-LDS design
+    // without its producer-side copy
+    if constexpr (WIDE) {
+        for (int i = tid; i < 3 * 12288 / 16; i += 512)
+            *reinterpret_cast<f32x4*>(ring + 100352 + i * 16) =
+                *reinterpret_cast<const f32x4*>(reinterpret_cast<const char*>(a.wpack) + i * 16);
+    }
+#endif
     const int nstages = (a.Cin + CK - 1) / CK;
     const int last = nstages - 1;
     const bool lds_epi = WIDE || x3_lds_epilogue(a);  // wide tiles: always (x3_wide_eligible)
@@ -875,6 +886,17 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
     f16x8 Aw[AR][CBW][2];
     f16x8 Bh[2][PBW], Bl[2][PBW];
     auto loadA = [&](int gg, f16x8 (&d)[CBW][2]) {
+#if NPS_X3_ABL == 9
+        if constexpr (WIDE) {
+            const char* q = ring + 100352 + (gg % 3) * 12288 + (cw0 / 32) * 2048 + lane * 16;
+#pragma unroll
+            for (int cb = 0; cb < CBW; ++cb) {
+                d[cb][0] = *reinterpret_cast<const f16x8*>(q + cb * 2048);
+                d[cb][1] = *reinterpret_cast<const f16x8*>(q + cb * 2048 + 1024);
+            }
+            return;
+        }
+#endif
         const char* p = wbase + (size_t)gg * gstride;
 #pragma unroll
         for (int cb = 0; cb < CBW; ++cb) {
@@ -996,7 +1018,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
 #pragma unroll
         for (int i = 0; i < 2 * CBW; ++i) {  // weights first: the longest latency gets the most cover
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
-            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // 1 VMEM read
+            __builtin_amdgcn_sched_group_barrier((NPS_X3_ABL == 9 && WIDE) ? 0x100 : 0x020, 1, 0);  // 1 VMEM read
         }
 #pragma unroll
         for (int i = 0; i < 2 * PBW; ++i) {
