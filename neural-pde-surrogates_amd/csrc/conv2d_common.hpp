@@ -294,9 +294,9 @@ __host__ __device__ inline int x3_ring_bytes(const nps_conv2d_t& a) {
     return X3_NST * ((g.PH * g.PW * X3_PIXB + 15) & ~15);
 }
 // bytes of the patch ring + epilogue tile region: 64-channel tiles reuse the ring for the tile (store phase
-// after the main loop); wide tiles keep the tile in a region of its own behind the ring, because tile t is
-// stored during tile t + 1's main loop (conv2d_x3_kernel: by the producer waves, or by the consumers in the
-// spread-store dev variant).  3x3 wide: 48 960 + 100 352 B.
+// after the main loop).  Wide tiles reserve ring + tile (3x3: 48 960 + 100 352 B; one work-group per CU either
+// way): the shipped store phase still writes the tile from the ring's start, the dev variants that store tile t
+// during tile t + 1 (NPS_X3_PSTORE=1 producers, NPS_X3_SPREAD consumers) keep it behind the ring.
 __host__ __device__ inline int x3_region_bytes(const nps_conv2d_t& a) {
     const int ring = x3_ring_bytes(a);
     const int tile = a.TH * a.TW * x3_tpitch(a) * 4;
