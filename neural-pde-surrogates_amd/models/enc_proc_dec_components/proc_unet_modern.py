@@ -275,7 +275,8 @@ class ResidualBlock(nn.Module):
         KH, KW, s, d, lo, hi, circ = self.conv1.geometry()
         Ho = (H + 2 * circ + lo[0] + hi[0] - d * (KH - 1) - 1) // s + 1
         Wo = (W + 2 * circ + lo[1] + hi[1] - d * (KW - 1) - 1) // s + 1
-        idle = ops.last_round_idle(Ho, Wo, x0.shape[0], self.conv1.out_channels, x0.device)
+        idle = ops.last_round_idle(Ho, Wo, x0.shape[0], self.conv1.out_channels, x0.device,
+                                   Cin=sum(s.t.shape[3] for s in srcs))
         return ops.Fork(x0, settle=[s.t for s in srcs]) if idle >= ops.SIDE_MIN_IDLE else None
 
     def run(self, srcs, frame_hw):

@@ -140,16 +140,41 @@ _side_depth = 0   # > 0 while launches go to a side stream
 _ncu = {}
 
 
-def last_round_idle(Ho: int, Wo: int, B: int, Cout: int, device) -> float:
-    """Fraction of the CUs left idle in the last round of a wide split-fp16 3x3 launch (the persistent grid
-    of nps_launch_conv2d_x3: one work-group per CU, 16 x 8-pixel x 192-channel tiles as nps_conv2d_plan
-    picks them for these shapes).  A fork beside such a launch pays only when this is large: every
+def x3_plan_tiles(Ho: int, Wo: int, B: int, Cout: int, Cin: int, K: int = 3) -> int:
+    """Work-group tiles of a stride-1 split-fp16 KxK launch with that output, as nps_conv2d_plan tiles it
+    (wide 192-channel or 64-channel tiles, the planner's TH x TW): host-only, cached per shape."""
+    key = (Ho, Wo, B, Cout, Cin, K)
+    n = _plan_tiles.get(key)
+    if n is None:
+        a = Conv2dArgs()
+        a.nsrc = 1
+        a.src[0].ptr, a.src[0].C, a.src[0].H, a.src[0].W = 0x1000, Cin, Ho + K - 1, Wo + K - 1
+        a.B, a.Hin, a.Win, a.Cin = B, Ho + K - 1, Wo + K - 1, Cin
+        a.KH = a.KW = K
+        a.stride, a.dil = 1, 1
+        a.Hout, a.Wout, a.Cout = Ho, Wo, Cout
+        a.out_C, a.out_H, a.out_W, a.out_os = Cout, Ho, Wo, 1
+        a.precision = PREC_X3F16
+        if lib.nps_conv2d_plan(ctypes_byref(a)) < 0:
+            raise RuntimeError("conv2d_plan failed: " + lib.nps_last_error().decode())
+        nco = 192 if a.TH * a.TW == 128 else 64
+        n = _plan_tiles[key] = -(-Ho // a.TH) * -(-Wo // a.TW) * B * -(-Cout // nco)
+    return n
+
+
+_plan_tiles = {}
+
+
+def last_round_idle(Ho: int, Wo: int, B: int, Cout: int, device, Cin: int = 192) -> float:
+    """Fraction of the CUs left idle in the last round of a split-fp16 3x3 launch: the persistent grid of
+    nps_launch_conv2d_x3 (one work-group per CU, multi_processor_count & ~7 of them) over the tiles
+    nps_conv2d_plan picks (x3_plan_tiles).  A fork beside such a launch pays only when this is large: every
     cross-stream wait costs ~15 us (profiles/r4/experiments/side_stream_forks_ab.txt)."""
     idx = device.index if device.index is not None else torch.cuda.current_device()
     n = _ncu.get(idx)
     if n is None:
         n = _ncu[idx] = torch.cuda.get_device_properties(idx).multi_processor_count & ~7
-    return idle_fraction(-(-Ho // 16) * -(-Wo // 8) * B * -(-Cout // 192), n)
+    return idle_fraction(x3_plan_tiles(Ho, Wo, B, Cout, Cin), n)
 
 
 def idle_fraction(tiles: int, workgroups: int) -> float:

@@ -109,3 +109,20 @@ def test_x3_weight_reads_stay_inside_the_packing(k):
                 assert 0 < span <= size, (Cin, Cout, k, v, span, size)
                 checked += 1
     assert checked > 100
+
+
+def test_fork_gate_reads_the_planners_tiles():
+    """the shortcut-fork gate (ops.last_round_idle) counts the tiles nps_conv2d_plan actually picks
+    (ops.x3_plan_tiles), not an assumed 16 x 8 plan.  C3 shapes: the 258^2 conv1 at B = 2 leaves >= 25 % of a
+    256-work-group grid idle in its last round (the shortcut forks), the 256^2 / 128-tile shapes fill exact rounds."""
+    from nps_hip import ops
+    for (Ho, Wo, B, Cout, Cin) in ((258, 258, 2, 192, 388), (256, 256, 2, 192, 192), (125, 125, 2, 192, 388),
+                                   (258, 258, 16, 192, 388), (40, 36, 2, 64, 36)):
+        a = _plan_args(Cin, Cout, 3, H=Ho + 2, W=Wo + 2)
+        a.B = B
+        assert ops.lib.nps_conv2d_plan(ctypes.byref(a)) >= 0
+        nco = 192 if a.TH * a.TW == 128 else 64
+        want = -(-Ho // a.TH) * -(-Wo // a.TW) * B * -(-Cout // nco)
+        assert ops.x3_plan_tiles(Ho, Wo, B, Cout, Cin) == want
+    assert ops.idle_fraction(ops.x3_plan_tiles(258, 258, 2, 192, 388), 256) >= ops.SIDE_MIN_IDLE
+    assert ops.idle_fraction(ops.x3_plan_tiles(256, 256, 2, 192, 192), 256) == 0.0
