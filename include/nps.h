@@ -435,8 +435,9 @@ typedef struct {
     int act;                    /* 0 none, 1 GELU, after bias + addend */
     int bf16;                   /* 1: bf16 storage / bf16 MFMA; 0: fp32 storage / exact fp32 MFMA */
     /* [B][NPS_STATS_SUB][2] fp64 or NULL: the launch ADDS the (sum, sum of squares) of the values it stores
-     * (as stored: bf16-rounded for bf16 storage) — the GroupNorm(1) moments of its output, carried to the next
-     * frame instead of an nps_gn_stats3d pass.  Plain epilogue only (no accumulate / addend / act / phases). */
+     * (as stored: bf16-rounded for bf16 storage; after addend and act) — with accumulate, of the change (stored
+     * minus replaced value), as nps_conv2d_t.out_stats — the GroupNorm(1) moments of its output, carried to the
+     * next frame instead of an nps_gn_stats3d pass. */
     double* out_stats;
 } nps_conv3d_t;
 

@@ -352,13 +352,20 @@ __global__ __launch_bounds__(256) void conv3d_kernel(const nps_conv3d_t a, int n
     const int pd = a.transposed ? (z >> 2) : 0, ph = a.transposed ? ((z >> 1) & 1) : 0,
               pw = a.transposed ? (z & 1) : 0;
     const int od = md * a.out_os + a.out_off_d + pd;
-    // out_stats: moments of the stored values (fp32 per 4-channel quad, fp64 across), published per wave at the
-    // end — so no early return: every lane reaches the wave-collective publish
+    // out_stats: moments of the stored values (fp32 per 4-channel quad, fp64 across) — with accumulate, of the
+    // change (stored value minus the value it replaced: s^2 - o^2 = (s - o)(s + o)), so a buffer seeded with out's
+    // moments ends with the accumulated tensor's (the 2-D convs' convention, include/nps.h out_stats) — published
+    // per wave at the end, so no early return: every lane reaches the wave-collective publish
     const bool st = a.out_stats != nullptr;
     float f1 = 0.f, f2 = 0.f;  // this lane's (at most 2 x RW x 16) stored values: fp32, then fp64 per wave
     auto mom = [&](float x0, float x1, float x2, float x3) {
         f1 += (x0 + x1) + (x2 + x3);
         f2 += (x0 * x0 + x1 * x1) + (x2 * x2 + x3 * x3);
+    };
+    auto momd = [&](const float (&x)[4], const float (&o)[4]) {  // the change of 4 accumulated values
+        f1 += ((x[0] - o[0]) + (x[1] - o[1])) + ((x[2] - o[2]) + (x[3] - o[3]));
+        f2 += ((x[0] - o[0]) * (x[0] + o[0]) + (x[1] - o[1]) * (x[1] + o[1])) +
+              ((x[2] - o[2]) * (x[2] + o[2]) + (x[3] - o[3]) * (x[3] + o[3]));
     };
     if (od >= 0 && od < a.out_D) {
     T* out = reinterpret_cast<T*>(a.out);
@@ -392,9 +399,16 @@ __global__ __launch_bounds__(256) void conv3d_kernel(const nps_conv3d_t a, int n
                     if (a.act == 1)
 #pragma unroll
                         for (int e = 0; e < 4; ++e) o[e] = nps::gelu_erf(o[e]);
-                    if (a.accumulate) o += *reinterpret_cast<const f32x4*>(op);
+                    f32x4 old = {0.f, 0.f, 0.f, 0.f};
+                    if (a.accumulate) {
+                        old = *reinterpret_cast<const f32x4*>(op);
+                        o += old;
+                    }
                     *reinterpret_cast<f32x4*>(op) = o;
-                    if (st) mom(o[0], o[1], o[2], o[3]);
+                    if (st) {
+                        const float x4[4] = {o[0], o[1], o[2], o[3]}, o4[4] = {old[0], old[1], old[2], old[3]};
+                        momd(x4, o4);
+                    }
                 } else if (vec4) {  // bf16: 4 channels = one 8-B access
                     float o[4] = {v[0], v[1], v[2], v[3]};
                     if (ap) {
@@ -405,14 +419,21 @@ __global__ __launch_bounds__(256) void conv3d_kernel(const nps_conv3d_t a, int n
                     if (a.act == 1)
 #pragma unroll
                         for (int e = 0; e < 4; ++e) o[e] = nps::gelu_erf(o[e]);
+                    float old[4] = {0.f, 0.f, 0.f, 0.f};
                     if (a.accumulate) {
                         const u32x2 w = *reinterpret_cast<const u32x2*>(op);
-                        o[0] += bf2f(w[0] & 0xffffu); o[1] += bf2f(w[0] >> 16);
-                        o[2] += bf2f(w[1] & 0xffffu); o[3] += bf2f(w[1] >> 16);
+                        old[0] = bf2f(w[0] & 0xffffu); old[1] = bf2f(w[0] >> 16);
+                        old[2] = bf2f(w[1] & 0xffffu); old[3] = bf2f(w[1] >> 16);
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) o[e] += old[e];
                     }
                     const u32x2 r = {f2bf(o[0]) | (f2bf(o[1]) << 16), f2bf(o[2]) | (f2bf(o[3]) << 16)};
                     *reinterpret_cast<u32x2*>(op) = r;
-                    if (st) mom(bf2f(r[0] & 0xffffu), bf2f(r[0] >> 16), bf2f(r[1] & 0xffffu), bf2f(r[1] >> 16));
+                    if (st) {  // (as stored)
+                        const float x4[4] = {bf2f(r[0] & 0xffffu), bf2f(r[0] >> 16), bf2f(r[1] & 0xffffu),
+                                             bf2f(r[1] >> 16)};
+                        momd(x4, old);
+                    }
                 } else {
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
@@ -420,12 +441,13 @@ __global__ __launch_bounds__(256) void conv3d_kernel(const nps_conv3d_t a, int n
                         float o = v[e];
                         if (ap) o += ld1<T>(ap + e);
                         if (a.act == 1) o = nps::gelu_erf(o);
-                        if (a.accumulate) o += ld1<T>(op + e);
+                        const float old = a.accumulate ? ld1<T>(op + e) : 0.f;
+                        if (a.accumulate) o += old;
                         st1<T>(op + e, o);
                         if (st) {
                             const float q = ld1<T>(op + e);  // (as stored)
-                            f1 += q;
-                            f2 += q * q;
+                            f1 += q - old;
+                            f2 += (q - old) * (q + old);
                         }
                     }
                 }
@@ -433,13 +455,20 @@ __global__ __launch_bounds__(256) void conv3d_kernel(const nps_conv3d_t a, int n
         }
     }
     }
-    if (st) {
+    if (st) {  // (uniform) one atomic pair per work-group: the 4 waves' sums meet in the (free) ring first
         const double s1 = nps::wave_sum((double)f1);
         const double s2 = nps::wave_sum((double)f2);
-        if ((threadIdx.x & 63) == 0) {
-            double* q = a.out_stats + ((size_t)b * NPS_STATS_SUB + nps::wave_salt() % NPS_STATS_SUB) * 2;
-            atomicAdd(q, s1);
-            atomicAdd(q + 1, s2);
+        double* red = reinterpret_cast<double*>(smem);
+        __syncthreads();  // every wave is past its last ring read
+        if (lane == 0) {
+            red[2 * wave] = s1;
+            red[2 * wave + 1] = s2;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double* q = a.out_stats + ((size_t)b * NPS_STATS_SUB + blockIdx.x % NPS_STATS_SUB) * 2;
+            atomicAdd(q, (red[0] + red[2]) + (red[4] + red[6]));
+            atomicAdd(q + 1, (red[1] + red[3]) + (red[5] + red[7]));
         }
     }
 }
@@ -819,8 +848,8 @@ extern "C" int nps_conv3d_fwd(const nps_conv3d_t* ap, void* stream) {
                                             a.Cin % a.gn_groups == 0),
                   "conv3d: bad GroupNorm prologue");
     NPS_CHECK_ARG(a.pre_act == 0 || a.pre_act == 1, "conv3d: pre_act 0 or 1");
-    NPS_CHECK_ARG(a.out_stats == nullptr || (!a.accumulate && a.addend == nullptr && a.act == 0 && !a.transposed),
-                  "conv3d: out_stats needs a plain epilogue (no accumulate / addend / act / phases)");
+    // (out_stats: moments of the values stored, after addend / act — of the change under accumulate; the 8 phases
+    // of a transposed conv write disjoint elements)
     const int nchunk = (a.Cin + 15) / 16, ntile = (a.Cout + 63) / 64;
     hipStream_t s = (hipStream_t)stream;
     return a.bf16 ? dispatch<bf16_t>(a, nchunk, ntile, s) : dispatch<float>(a, nchunk, ntile, s);

@@ -195,7 +195,10 @@ class UNetModern(nn.Module):
         h = self.middle.run3d(h, vb)
         for m in self.up:
             if isinstance(m, Upsample):
-                h = m.conv.run3d(h)
+                st = ops.new_stats(h.shape[0], h) if ops.CARRY3D else None  # (moments of the 8 phases' outputs)
+                h = m.conv.run3d(h, out_stats=st)
+                if st is not None:
+                    ops.attach_stats(h, st)
             else:
                 _check_no_attn(m)
                 s = feats.pop()
@@ -217,8 +220,13 @@ class UNetModern(nn.Module):
         out = torch.empty(tuple(h_shape[:4]) + (self.final.out_channels,), dtype=h.dtype, device=h.device)
         if any(o > 0 for o in off):
             out.zero_()  # crop_Nd zero-pads when the output is smaller than the input
+        # the output's moments (the next U-FNO block's first norm1): those of the values the final conv stores
+        # (after the addend and act_after; the crop border stays zero)
+        st = ops.new_stats(out.shape[0], out) if ops.CARRY3D else None
         self.final.run3d([ops.Src3(h)], dhw, gn=gn, pre_act=activation_code(self.activation), out=out, out_off=off,
-                         addend=addend, act=act_after)
+                         addend=addend, act=act_after, out_stats=st)
+        if st is not None:
+            ops.attach_stats(out, st)
         return out
 
     def final_out_hw(self, H, W):
@@ -334,20 +342,28 @@ class ResidualBlock(nn.Module):
         act = activation_code(self.activation)
         gn1 = gn2 = None
         if isinstance(self.norm1, nn.GroupNorm):
-            gn1 = _gn_args(self.norm1, ops.gn_stats3d(srcs, frame_dhw, self.norm1.num_groups))
+            # GroupNorm(1) of a frame of carried-moment sources: their sum, no pass (ops.group_norm_stats3d)
+            gn1 = _gn_args(self.norm1, ops.group_norm_stats3d(srcs, frame_dhw, self.norm1.num_groups))
         # conv1 adds the moments of what it stores (nps_conv3d_t.out_stats): norm2's GroupNorm(1) statistics
         # without a pass over h1
         B = srcs[0].t.shape[0]
         carry = isinstance(self.norm2, nn.GroupNorm) and self.norm2.num_groups == 1
         st1 = ops.new_stats(B, srcs[0].t) if carry else None
         h1 = self.conv1.run3d(srcs, frame_dhw, gn=gn1, pre_act=act, out_stats=st1)
+        # the block output's moments (the next block's norm1): the shortcut output's — x's own for the identity,
+        # else added by the 1x1x1 conv — plus the change conv2 makes accumulating into it (as the 2-D run())
+        carry_out = ops.CARRY3D and isinstance(self.norm1, nn.GroupNorm)
+        st_out = None
         if isinstance(self.shortcut, nn.Identity):
             s0 = srcs[0]
             if len(srcs) != 1 or s0.off_d or s0.off_h or s0.off_w or tuple(s0.t.shape[1:4]) != tuple(frame_dhw):
                 raise RuntimeError("identity shortcut on a concatenated input")
             out = s0.t.clone()
+            if carry_out:
+                st_out = ops.copy_stats(ops.source_stats3d(s0.t))
         else:
-            out = self.shortcut.run3d(srcs, frame_dhw)
+            st_out = ops.new_stats(B, srcs[0].t) if carry_out else None
+            out = self.shortcut.run3d(srcs, frame_dhw, out_stats=st_out)
         d1 = tuple(h1.shape[1:4])
         if isinstance(self.norm2, nn.GroupNorm):
             st2 = (ops._stats_sum([st1], B, ops.new_stats(B, h1, 1)) if carry
@@ -356,7 +372,9 @@ class ResidualBlock(nn.Module):
         K, s, circ, zpad = self.conv2.geometry3d()
         d2 = tuple((n + 2 * (circ + zpad) - K) // s + 1 for n in d1)
         self.conv2.run3d([ops.Src3(h1)], d1, gn=gn2, pre_act=act, out=out,
-                         out_off=crop_offsets3(d2, out.shape[1:4]), accumulate=True)
+                         out_off=crop_offsets3(d2, out.shape[1:4]), accumulate=True, out_stats=st_out)
+        if st_out is not None:
+            ops.attach_stats(out, st_out)
         return out
 
     def run_ad(self, srcs, frame_hw):
@@ -553,7 +571,10 @@ class Downsample(nn.Module):
         return h, vb
 
     def run3d(self, x, vb):
-        h = self.conv.run3d([ops.Src3(x)], x.shape[1:4])
+        st = ops.new_stats(x.shape[0], x) if ops.CARRY3D else None  # the next ResidualBlock's norm1 moments of h
+        h = self.conv.run3d([ops.Src3(x)], x.shape[1:4], out_stats=st)
+        if st is not None:
+            ops.attach_stats(h, st)
         if vb is not None:
             vb = self.conv_variables_broadcast.run3d([ops.Src3(vb)], vb.shape[1:4])
         return h, vb

@@ -948,6 +948,34 @@ def gn_stats3d(srcs: Sequence[Src3], frame_dhw, groups: int) -> torch.Tensor:
     return st
 
 
+# 3-D GroupNorm(1) frames take their sources' carried moments (the 3-D convs' out_stats) instead of an nps_gn_stats3d
+# pass over the frame (dev knob NPS_CARRY3D=0: always the pass)
+CARRY3D = os.environ.get("NPS_CARRY3D", "1") != "0"
+
+
+def source_stats3d(t: torch.Tensor) -> torch.Tensor:
+    """NDHWC t's GroupNorm(1) moments: carried, or one nps_gn_stats3d pass (then carried)."""
+    st = stats_of(t)
+    if st is None:
+        st = gn_stats3d([Src3(t)], tuple(t.shape[1:4]), 1)
+        attach_stats(t, st)
+    return st
+
+
+def group_norm_stats3d(srcs: Sequence[Src3], frame_dhw, groups: int) -> torch.Tensor:
+    """gn_stats3d of a 3-D frame; GroupNorm(1) of sources that lie wholly inside the frame (crop_Nd zero-pads them,
+    it does not cut them): the sum of the sources' carried moments (source_stats3d), as the 2-D group_norm_stats."""
+    t0 = srcs[0].t
+    if CARRY3D and groups == 1 and all(
+            all(0 <= o and o + n <= f for o, n, f in zip((s.off_d, s.off_h, s.off_w), s.t.shape[1:4], frame_dhw))
+            for s in srcs):
+        parts = [source_stats3d(s.t) for s in srcs]
+        if len(parts) == 1 and parts[0].shape[1] == 1:
+            return parts[0]
+        return _stats_sum(parts, t0.shape[0], new_stats(t0.shape[0], t0, 1))
+    return gn_stats3d(srcs, frame_dhw, groups)
+
+
 # Materialise act(GN(frame)) before a K > 1 conv whose frame needs a prologue or several / offset / unaligned
 # sources (nps_frame_pack3d), so the conv runs its single-source fast path (dev knob NPS_CONV3D_PACK=0: off)
 CONV3D_PACK = os.environ.get("NPS_CONV3D_PACK", "1") == "1"

@@ -210,3 +210,42 @@ def test_conv3d_out_stats_carry_moments(dt):
     torch.testing.assert_close(got, ref, rtol=1e-6, atol=1e-3)
     torch.testing.assert_close(got[:, 0], yd.sum(1), rtol=1e-6, atol=1e-3)
     torch.testing.assert_close(got[:, 1], (yd ** 2).sum(1), rtol=1e-6, atol=1e-3)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+def test_conv3d_out_stats_with_accumulate_addend_act_and_phases(dt):
+    """out_stats for the 3-D producers whose outputs feed the next GroupNorm(1) (ops.group_norm_stats3d carries them
+    instead of a gn_stats3d pass): conv2 accumulating into the shortcut output (the CHANGE's moments, added to a
+    buffer seeded with the old output's), the U-Net's final conv with the U-FNO addend + GELU, and the 8 phases of
+    the 3-D Upsample — each equal to a gn_stats3d pass over the stored tensor."""
+    from nps_hip import ops
+    torch.manual_seed(11)
+    B, dhw = 2, (6, 10, 21)
+    bf = dt == torch.bfloat16
+    x = _ndhwc(torch.randn(B, 32, *dhw), dt)
+    w, b = torch.randn(32, 32, 3, 3, 3) * 0.05, torch.randn(32) * 0.1
+
+    def passes(t):
+        return ops.gn_stats3d([ops.Src3(t)], t.shape[1:4], 1).cpu()[:, 0]
+
+    def carried(st):
+        return ops._stats_sum([st], B, ops.new_stats(B, st, 1)).cpu()[:, 0]
+
+    # accumulate into a (cropped) output seeded with its own moments
+    out = _ndhwc(torch.randn(B, 32, 6, 12, 23), dt)
+    st = ops.copy_stats(ops.gn_stats3d([ops.Src3(out)], out.shape[1:4], 1))
+    ops.conv3d([ops.Src3(x)], dhw, ops.pack_conv3d_weight(w.to(DEV), bf16=bf), b.to(DEV), 32, 3, zpad=1, out=out,
+               out_off=(0, 1, 1), accumulate=True, out_stats=st)
+    torch.testing.assert_close(carried(st), passes(out), rtol=1e-5, atol=1e-2)
+    # addend + GELU
+    add = _ndhwc(torch.randn(B, 32, *dhw), dt)
+    st = ops.new_stats(B, x)
+    y = ops.conv3d([ops.Src3(x)], dhw, ops.pack_conv3d_weight(w.to(DEV), bf16=bf), b.to(DEV), 32, 3, zpad=1,
+                   addend=add, act=1, out_stats=st)
+    torch.testing.assert_close(carried(st), passes(y), rtol=1e-5, atol=1e-2)
+    # the 3-D Upsample's 8 phases (circular pad 1, ConvTranspose3d k4 s2)
+    wt = torch.randn(32, 32, 4, 4, 4) * 0.05
+    st = ops.new_stats(B, x)
+    u = ops.conv3d([ops.Src3(x)], dhw, ops.pack_conv3d_weight(wt.to(DEV), transposed=True, bf16=bf), None, 32, 2,
+                   transposed=True, circ=1, zpad=1, out_stats=st)
+    torch.testing.assert_close(carried(st), passes(u), rtol=1e-5, atol=1e-2)
