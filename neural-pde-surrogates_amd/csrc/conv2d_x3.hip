@@ -107,7 +107,8 @@ __host__ __device__ __forceinline__ bool x3_lds_epilogue(const nps_conv2d_t& a) 
 // the fused bias / addends / GELU / accumulate of store_tile, in the same float order.
 template <int TILE_PX, int NCO>
 __device__ __forceinline__ void x3_store_phase(const nps_conv2d_t& a, int b, int cob, int oy0, int ox0, int lat,
-                                               int ph, const float* T, const float* btab, int tid, float& amax) {
+                                               int ph, const float* T, const float* btab, int tid, float& amax,
+                                               double* red) {
     const int poy = a.out_off_y + (ph >> 1), pox = a.out_off_x + (ph & 1);  // transposed-conv phase offset
     constexpr int Q = NCO / 4;
     const bool st = a.out_stats != nullptr;
@@ -150,7 +151,7 @@ __device__ __forceinline__ void x3_store_phase(const nps_conv2d_t& a, int b, int
                 s2 += ok ? (double)f2 : 0.0;
             }
         }
-        stats_publish(a, b, s1, s2);
+        stats_publish_wg(a, b, s1, s2, red);
         return;
     }
 #pragma unroll 4
@@ -192,7 +193,7 @@ __device__ __forceinline__ void x3_store_phase(const nps_conv2d_t& a, int b, int
             s2 += (double)f2;
         }
     }
-    stats_publish(a, b, s1, s2);  // the next GroupNorm(1)'s moments of this sample: one pair per wave
+    stats_publish_wg(a, b, s1, s2, red);  // the next GroupNorm(1)'s moments of this sample: one pair per tile
 }
 
 // Wide-tile consumers on v_mfma_f32_16x16x32_f16 with TAP-PAIRED K (NPS_X3_M16, default).  Under the DVFS
@@ -346,7 +347,8 @@ __device__ __forceinline__ void x3_consume_m16(const nps_conv2d_t& a, const Geo&
             }
         }
         barrier();
-        x3_store_phase<TILE_PX, NCO>(a, b, cob, oy0, ox0, g.T, ph, T, btab, tid, amax);
+        x3_store_phase<TILE_PX, NCO>(a, b, cob, oy0, ox0, g.T, ph, T, btab, tid, amax,
+                                     reinterpret_cast<double*>(const_cast<char*>(ring) - 128));
         barrier();  // the staged tile is fully read: the producers may refill the ring
     }
     nps::tag_publish(a.out_tag, amax, nps::wave_salt());
@@ -853,7 +855,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
             barrier();  // the consumers' tile is in LDS
             if (lds_epi)
                 x3_store_phase<TILE_PX, NCO>(a, sb, scob, soy0, sox0, g.T, sph, reinterpret_cast<const float*>(ring), btab, tid,
-                                             pmax);
+                                             pmax, reinterpret_cast<double*>(smem));  // (red: the unused 128-B header)
             barrier();  // every read of the staged tile is done: the ring may be refilled
             if (!more) break;
             l = ln;
@@ -1171,7 +1173,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
             }
             barrier();
             X3_STAMP(8);
-            x3_store_phase<TILE_PX, NCO>(a, b, cob, oy0, ox0, g.T, ph, T, btab, tid, amax);
+            x3_store_phase<TILE_PX, NCO>(a, b, cob, oy0, ox0, g.T, ph, T, btab, tid, amax, reinterpret_cast<double*>(smem));
             X3_STAMP(9);
         } else if constexpr (!WIDE) {
             static_for<PBW>([&](auto pbc) {  // compile-time pb: acc stays in registers
@@ -2204,7 +2206,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
         else
             epi(std::false_type{});
         nps::tag_publish(a.out_tag, amax, nps::wave_salt());
-        stats_publish(a, b, s1, s2);  // no-op without out_stats
+        // (every LDS read of the main loop is behind its last barrier: the weight buffers hold the reduction)
+        stats_publish_wg(a, b, s1, s2, reinterpret_cast<double*>(wl));  // no-op without out_stats
         return;
     }
     if (pout) {
