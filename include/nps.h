@@ -135,7 +135,10 @@ typedef struct {
 #define NPS_TAG_STRIDE 64
 #define NPS_TAG_FLOATS (NPS_TAG_SUB * NPS_TAG_STRIDE)
 /* sub-slots per sample of a moments buffer (nps_conv2d_t.out_stats) */
+#ifndef NPS_STATS_SUB
 #define NPS_STATS_SUB 16
+#endif
+int nps_stats_sub(void); /* NPS_STATS_SUB of this build (the moments buffers' sub-slot count) */
 
 #define NPS_PREC_F32 0
 #define NPS_PREC_X3F16 1

@@ -972,6 +972,8 @@ __global__ void stats_sum_kernel(const double* __restrict__ p0, int n0, const do
 }
 }  // namespace
 
+extern "C" int nps_stats_sub(void) { return NPS_STATS_SUB; }
+
 extern "C" int nps_stats_sum(const double* p0, int n0, const double* p1, int n1, const double* p2, int n2, int B,
                              double* out, int n_out, void* stream) {
     NPS_CHECK_ARG(p0 && out && B > 0 && n0 > 0 && (!p1 || n1 > 0) && (!p2 || n2 > 0) && n_out > 0,

@@ -100,6 +100,7 @@ _SIGS = {
     "nps_space_to_depth": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp]),
     "nps_group_norm_stats": (_i, [ctypes.POINTER(Src), _i, _i, _i, _i, _i, _i, _vp, _i, _vp]),
     "nps_stats_sum": (_i, [_vp, _i, _vp, _i, _vp, _i, _i, _vp, _i, _vp]),
+    "nps_stats_sub": (_i, []),
     "nps_x3_set_grid": (_i, [ctypes.c_long]),
     "nps_spectral_dft_w": (_i, [ctypes.POINTER(Src), _i, _i, _i, _i, _i, _i, _vp, _vp]),
     "nps_spectral_dft_h": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp]),

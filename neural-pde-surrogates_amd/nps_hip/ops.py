@@ -319,7 +319,7 @@ def input_tag(t: torch.Tensor) -> int:
 # moments get them from one nps_group_norm_stats pass over that source alone, kept for later frames.
 # Moments are valid while the tensor is unchanged: torch's in-place ops bump t._version, and the HIP ops
 # that write into an existing tensor drop them (drop_stats).
-STATS_SUB = 16  # NPS_STATS_SUB
+STATS_SUB = lib.nps_stats_sub()  # NPS_STATS_SUB of the loaded library (sub-slots of a moments buffer)
 
 
 _STATS_CHUNK = 1 << 15      # doubles zeroed at once; slices are handed out and never re-zeroed
