@@ -150,6 +150,52 @@ __device__ __forceinline__ void stats_publish_wg(const nps_conv2d_t& a, int b, d
 #endif
 }
 
+#ifndef NPS_TAG_WG
+#define NPS_TAG_WG 1  // 1: the 1x1 fused epilogue raises the range tag once per work-group (publish_wg), 0: per wave
+#endif
+// Work-group-collective range-tag raise + moments publish (one LDS exchange, one barrier): red holds 2 doubles and
+// 1 float per wave.  Every thread of the work-group calls it at the same point with the same b.
+__device__ __forceinline__ void publish_wg(const nps_conv2d_t& a, int b, float amax, double s1, double s2,
+                                           double* red) {
+#if NPS_TAG_WG
+    const bool st = a.out_stats != nullptr, tg = a.out_tag != nullptr;
+    if (!st && !tg) return;
+    const int w = (int)(threadIdx.x >> 6), nw = (int)(blockDim.x >> 6);
+    float* rm = reinterpret_cast<float*>(red + 2 * nw);
+    if (st) {
+        s1 = nps::wave_sum(s1);
+        s2 = nps::wave_sum(s2);
+    }
+    amax = nps::wave_max(amax);
+    if ((threadIdx.x & 63) == 0) {
+        red[2 * w] = s1;
+        red[2 * w + 1] = s2;
+        rm[w] = amax;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t1 = 0.0, t2 = 0.0;
+        float m = 0.f;
+        for (int i = 0; i < nw; ++i) {
+            t1 += red[2 * i];
+            t2 += red[2 * i + 1];
+            m = fmaxf(m, rm[i]);
+        }
+        if (st) {
+            double* p = a.out_stats + ((size_t)b * NPS_STATS_SUB + blockIdx.x % NPS_STATS_SUB) * 2;
+            atomicAdd(p, t1);
+            atomicAdd(p + 1, t2);
+        }
+        if (tg && m > 0.f)
+            atomicMax(reinterpret_cast<unsigned int*>(a.out_tag + (blockIdx.x % NPS_TAG_SUB) * NPS_TAG_STRIDE),
+                      __float_as_uint(m));
+    }
+#else
+    nps::tag_publish(a.out_tag, amax, nps::wave_salt());
+    stats_publish_wg(a, b, s1, s2, red);
+#endif
+}
+
 // store_tile that also accumulates the stored values' moments into (s1, s2) when out_stats is set
 // (NHWC 4-aligned outputs only: nps_conv2d_fwd refuses out_stats otherwise)
 __device__ __forceinline__ void store_tile_s(const nps_conv2d_t& a, int b, int co_base, int h, const f32x16& acc,

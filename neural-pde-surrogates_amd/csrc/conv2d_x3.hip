@@ -2205,9 +2205,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
             epi(std::true_type{});
         else
             epi(std::false_type{});
-        nps::tag_publish(a.out_tag, amax, nps::wave_salt());
-        // (every LDS read of the main loop is behind its last barrier: the weight buffers hold the reduction)
-        stats_publish_wg(a, b, s1, s2, reinterpret_cast<double*>(wl));  // no-op without out_stats
+        // range tag + moments, once per work-group (every LDS read of the main loop is behind its last barrier:
+        // the weight buffers hold the exchange)
+        publish_wg(a, b, amax, s1, s2, reinterpret_cast<double*>(wl));
         return;
     }
     if (pout) {
