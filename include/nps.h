@@ -127,6 +127,15 @@ typedef struct {
      * without materialising the space-to-depth copy. */
     int s2d;
     int s2d_pad;
+    /* FNO layer fusion (1x1 split-fp16 convs on the LDS-weight kernel only; NULL = off): the truncated c2r W pass
+     * of the spectral conv is added to the conv's result before the bias / act epilogue — out[b][y][x][o] =
+     * act(w(x) + bias + spec_scale * sum_k c_k Re(spec_z[b][y][k][o] e^{2 pi i k x / W})), c_k = 2 except DC /
+     * Nyquist (Im dropped), as nps_spectral_idft_w with accumulate (proc_fno.py:142-146: conv(x) + w(x)) — so the
+     * separate idft_w read-modify-write of the output is gone.  spec_z: [B][Hout][spec_m2][Cout] complex64 (the
+     * spectral pipeline's Z), Wout % 128 == 0, spec_m2 <= 16, no addend / accumulate. */
+    const float* spec_z;
+    int spec_m2;
+    float spec_scale;
 } nps_conv2d_t;
 
 /* Range tags (nps_conv2d_t.in_scale / in_tag* / out_tag): 64 sub-slots 256 B apart, so the atomics of

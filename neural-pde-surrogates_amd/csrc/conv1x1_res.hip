@@ -308,7 +308,9 @@ int nps_conv1x1_res_plan(const nps_conv2d_t& a, int all, int* ncb, int* ng, int*
     // kernel (Cout <= 192, NHWC) cannot take and the co-block kernel ran at 1.4 TB/s; all = 1 (dev knob
     // NPS_X1_RES=1): every eligible 1x1
     if (!all && !(a.out_nchw && a.Cout > 192 && a.Cout <= 256)) return 0;
-    if (a.KH * a.KW != 1 || a.accumulate || a.addend1 != nullptr || a.gn_stats != nullptr || a.pre_act != 0) return 0;
+    if (a.KH * a.KW != 1 || a.accumulate || a.addend1 != nullptr || a.gn_stats != nullptr || a.pre_act != 0 ||
+        a.spec_z != nullptr)
+        return 0;
     if (a.out_nchw && (a.addend0 != nullptr || a.out_stats != nullptr)) return 0;
     if (a.out_stats != nullptr && a.Cout > 192) return 0;  // (moments of the stored values: addend / act included)
     if ((long)a.B * ((a.Hout * a.Wout + 31) / 32) >= (1L << 31)) return 0;

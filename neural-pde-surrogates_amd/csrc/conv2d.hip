@@ -816,6 +816,14 @@ extern "C" int nps_conv2d_fwd(const nps_conv2d_t* ap, void* stream) {
                                   a.gn_beta),
                   "conv2d_fwd: bad GroupNorm prologue");
     NPS_CHECK_ARG(a.circ == 0 || (a.Hin > 0 && a.Win > 0), "conv2d_fwd: circular padding of empty frame");
+    NPS_CHECK_ARG(a.spec_z == nullptr ||
+                      (a.precision == NPS_PREC_X3F16 && a.KH == 1 && a.KW == 1 && a.stride == 1 && a.Cout <= 192 &&
+                       !a.gn_stats && !a.pre_act && !a.accumulate && !a.addend0 && !a.addend1 && !a.out_nchw &&
+                       (a.out_C & 3) == 0 && (a.Cout & 3) == 0 && a.spec_m2 > 0 && a.spec_m2 <= 16 &&
+                       (a.Wout & 127) == 0 && a.pad_y == 0 && a.pad_x == 0 && a.circ == 0 && a.out_os == 1 &&
+                       a.out_off_y == 0 && a.out_off_x == 0 && a.out_H == a.Hout && a.out_W == a.Wout),
+                  "conv2d_fwd: the fused c2r term (spec_z) needs a plain split-fp16 1x1 on the LDS-weight kernel "
+                  "(Cout <= 192, no prologue / addend / accumulate, Wout %% 128 == 0, m2 <= 16)");
     NPS_CHECK_ARG(a.waves == 1 || a.waves == 2 || a.waves == 4 || a.waves == 8, "conv2d_fwd: call nps_conv2d_plan first");
     NPS_CHECK_ARG(a.precision == NPS_PREC_F32 || x3_sources_aligned(a),
                   "conv2d_fwd: split-fp16 conv needs sources on 16-channel boundaries with C %% 4 == 0 (frame_pack first)");

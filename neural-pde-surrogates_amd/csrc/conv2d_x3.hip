@@ -2133,6 +2133,48 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     X3_STAMP(2);
 #endif
     const float inv = 1.f / (pow2_scale_for(a.wpack[packed_body(a.Cout, a.Cin, 1)]) * xs);
+    if constexpr (!PRO) {
+        if (a.spec_z != nullptr) {
+            // FNO layer fusion (nps_conv2d_t.spec_z): the c2r W pass of the spectral conv on the same accumulators,
+            // out[co][px] += sum_k' Z'[k'][co] T[k'][px] on exact-fp32 v_mfma_f32_32x32x2f32 (one K-step per bin:
+            // k' = 2k Re Z c_k against cos 2 pi k x / W, 2k + 1 Im Z c_k against -sin), Z' pre-scaled by
+            // spec_scale / inv (exact powers of 2 both), so the epilogue's acc * inv + bias carries it.  The
+            // work-group's 128 pixels lie in one row (Wout % 128 == 0, host-checked): Z' of that row and the
+            // pixels' twiddles are staged in the (free) weight buffers, behind the exchange slot at their start.
+            const int m2 = a.spec_m2, K2 = 2 * m2;
+            const int t0 = (int)blockIdx.x * 128, y0 = t0 / a.Wout, x0 = t0 - y0 * a.Wout;
+            float* zs = reinterpret_cast<float*>(wl + 256);                 // [K2][NCB * 32]
+            float* ts = zs + K2 * NCB * 32;                                   // [128][K2]
+            const float fac = a.spec_scale / inv;
+            const float2* zrow = reinterpret_cast<const float2*>(a.spec_z) + ((size_t)b * a.Hout + y0) * m2 * a.Cout;
+            for (int i = threadIdx.x; i < m2 * NCB * 32; i += 256) {
+                const int k = i / (NCB * 32), o = i - k * (NCB * 32);
+                const bool self_conj = (k == 0) || (2 * k == a.Wout);
+                const float cm = self_conj ? 1.f : 2.f;
+                float2 z = make_float2(0.f, 0.f);
+                if (o < a.Cout) z = zrow[(size_t)k * a.Cout + o];
+                zs[(2 * k) * NCB * 32 + o] = z.x * cm * fac;
+                zs[(2 * k + 1) * NCB * 32 + o] = self_conj ? 0.f : z.y * cm * fac;
+            }
+            for (int i = threadIdx.x; i < 128 * m2; i += 256) {
+                const int p = i / m2, k = i - (i / m2) * m2;
+                const int ph = (int)(((long)k * (x0 + p)) % a.Wout);
+                float sn, cs;
+                sincospif(2.0f * (float)ph / (float)a.Wout, &sn, &cs);
+                ts[p * K2 + 2 * k] = cs;
+                ts[p * K2 + 2 * k + 1] = -sn;
+            }
+            __syncthreads();
+            const float* tl = ts + (wv * 32 + (lane & 31)) * K2 + h;  // B: pixel lane % 32, k' parity lane / 32
+            for (int k = 0; k < m2; ++k) {
+                const float bt = tl[2 * k];
+#pragma unroll
+                for (int cb = 0; cb < NCB; ++cb)
+                    acc[cb] = __builtin_amdgcn_mfma_f32_32x32x2f32(zs[(2 * k + h) * NCB * 32 + cb * 32 + (lane & 31)], bt,
+                                                                  acc[cb], 0, 0, 0);
+            }
+        }
+    }
     const int oy = P / a.Wout, ox = P - (P / a.Wout) * a.Wout;
     const int dy = oy * a.out_os + a.out_off_y, dx = ox * a.out_os + a.out_off_x;
     float amax = 0.f;
@@ -2652,6 +2694,15 @@ extern "C" int nps_conv2d_x1_dma(const nps_conv2d_t* a) { return a != nullptr &&
 
 // test hook (nps_x3_set_grid): persistent-grid size override (> 0)
 static long g_x3_grid_override = 0;
+
+static bool wl_on() {  // 1x1 convs with Cout <= 192 on the LDS-weight kernel (dev knob NPS_X3_1X1_WL=0: off)
+    static int wl = -1;
+    if (wl < 0) {
+        const char* e = getenv("NPS_X3_1X1_WL");
+        wl = (e != nullptr && e[0] == '0') ? 0 : 1;
+    }
+    return wl == 1;
+}
 extern "C" int nps_x3_set_grid(long wgs) {
     g_x3_grid_override = wgs > 0 ? wgs : 0;
     return 0;
@@ -2691,8 +2742,10 @@ int nps_launch_conv2d_x3(const nps_conv2d_t& a, int lds, hipStream_t s) {
     if (a.KH * a.KW == 1) {
         NPS_CHECK_ARG(!pro || a.Cout <= 192, "conv2d_fwd (split-fp16): a 1x1 prologue needs the LDS-weight kernel "
                       "(Cout <= 192)");
+        NPS_CHECK_ARG(a.spec_z == nullptr || (wl_on() && a.Cout <= 192),
+                      "conv2d_fwd (split-fp16 1x1): the fused c2r term needs the LDS-weight kernel");
 #ifdef NPS_X1_DMA_KERNEL
-        if (x1_dma_ok(a)) {
+        if (x1_dma_ok(a) && a.spec_z == nullptr) {
             const int ncb = (a.Cout + 31) / 32;
             const long ntiles = (((long)a.Hout * a.Wout + 127) / 128) * a.B;
             NPS_CHECK_ARG(ntiles < (1L << 31), "conv2d_fwd: grid too large");
@@ -2713,11 +2766,7 @@ int nps_launch_conv2d_x3(const nps_conv2d_t& a, int lds, hipStream_t s) {
             cfg = e != nullptr ? atoi(e) % 3 : 0;
         }
         const int ncob = (a.Cout + 63) / 64;
-        static int wl = -1;  // dev knob NPS_X3_1X1_WL=0: co-block waves instead of LDS-staged weights
-        if (wl < 0) {
-            const char* e = getenv("NPS_X3_1X1_WL");
-            wl = (e != nullptr && e[0] == '0') ? 0 : 1;
-        }
+        const int wl = wl_on() ? 1 : 0;  // dev knob NPS_X3_1X1_WL=0: co-block waves instead of LDS-staged weights
         // out_stats: the LDS-weight kernel's fused register epilogue takes the moments of the values it stores
         // (after the addend and the activation); its store_tile fallback (two addends, accumulate) cannot
         NPS_CHECK_ARG(a.out_stats == nullptr || (wl && a.Cout <= 192 && !a.accumulate && a.addend1 == nullptr && lds_epi),

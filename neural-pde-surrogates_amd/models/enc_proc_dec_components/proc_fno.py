@@ -161,6 +161,12 @@ class FNO_Layer(nn.Module):
         H, W = srcs[0].t.shape[1:3]
         self._check_modes((H, W))
         act = activation_code(self.act) if act_override is None else act_override
+        if (self.conv_mode != "double" and not self.conv.feature_transform and
+                ops.spectral_fusable(W, self.conv.modes2, self.conv.out_channels)):
+            # conv(x) + w(x) in one output pass: the 1x1's epilogue synthesises the spectral conv's W pass
+            # (nps_conv2d_t.spec_z; scale 1 / (H W) of irfft2's norm), then the activation
+            Z = self.conv.run_z(srcs)
+            return self.w.run(srcs, (H, W), spec=(Z, self.conv.modes2, 1.0 / (H * W)), act=act)
         out = self.w.run(srcs, (H, W))
         if self.conv_mode == "double":
             self.w2.run(srcs, (H, W), out=out, accumulate=True)
@@ -243,6 +249,14 @@ class SpectralConv2d(nn.Module):
         H = srcs[0].t.shape[1]
         return ops.spectral_conv2d(srcs, self.packed(H), self.modes1, self.modes2, self.out_channels, out=out,
                                    accumulate=accumulate, addend=addend, act=act)
+
+    def run_z(self, srcs):
+        """The spectrum Z (B, H, m2, Cout) before the W-pass synthesis (ops.spectral_z): the FNO layer hands it to
+        its 1x1 `w`, whose epilogue synthesises it (conv2d(spec=...))."""
+        if self.feature_transform:
+            raise NotImplementedError("FiLM spectral conditioning is not on the MI355X path")
+        H = srcs[0].t.shape[1]
+        return ops.spectral_z(srcs, self.packed(H), self.modes1, self.modes2, self.out_channels)
 
     def forward(self, x, p=None):
         if self.feature_transform:

@@ -49,6 +49,7 @@ class Conv2dArgs(ctypes.Structure):
         ("precision", ctypes.c_int), ("in_scale", ctypes.c_void_p), ("in_tag1", ctypes.c_void_p),
         ("in_tag2", ctypes.c_void_p), ("out_tag", ctypes.c_void_p), ("out_stats", ctypes.c_void_p),
         ("nphase", ctypes.c_int), ("phase_wstride", ctypes.c_long), ("s2d", ctypes.c_int), ("s2d_pad", ctypes.c_int),
+        ("spec_z", ctypes.c_void_p), ("spec_m2", ctypes.c_int), ("spec_scale", ctypes.c_float),
     ]
 
 

@@ -542,7 +542,7 @@ def conv2d(srcs: Sequence[Src], frame_hw, wpack: torch.Tensor, bias: Optional[to
            out: Optional[torch.Tensor] = None, out_nchw=False, out_os=1, out_off=(0, 0), accumulate=False,
            addends: Sequence[torch.Tensor] = (), act=0, add_after_act=False, pad_bottom=None,
            in_scale: Optional[Union[torch.Tensor, int]] = None, out_stats: Optional[torch.Tensor] = None, phases: int = 1,
-           s2d_pad: Optional[int] = None):
+           s2d_pad: Optional[int] = None, spec: Optional[tuple] = None):
     """One fused conv launch.  `pad` = top/left zero padding (in the circularly
     extended frame), `pad_bottom` defaults to `pad`.  `out_stats`: a new_stats() buffer the launch adds
     the GroupNorm(1) moments of its stored values to (marked incomplete when this conv's kernel cannot;
@@ -613,6 +613,11 @@ def conv2d(srcs: Sequence[Src], frame_hw, wpack: torch.Tensor, bias: Optional[to
     a.addend1 = ptr(ads[1]) if len(ads) > 1 else None
     a.act, a.add_after_act = act, (1 if add_after_act else 0)
     a.precision = getattr(wpack, "nps_precision", PREC_F32)
+    if spec is not None:  # (Z, m2, scale): the spectral conv's W pass added in the epilogue (spectral_fusable)
+        Z, m2s, sc = spec
+        if Z.dtype != torch.complex64 or not Z.is_contiguous() or tuple(Z.shape) != (B, Hout, m2s, Cout):
+            raise RuntimeError("conv2d: spec Z must be contiguous complex64 (B, Hout, m2, Cout)")
+        a.spec_z, a.spec_m2, a.spec_scale = ptr(Z), m2s, float(sc)
     if phases > 1:
         if a.precision != PREC_X3F16 or phases != 4 or out_os != 2:
             raise ValueError("conv2d: merged transposed-conv phases need the split-fp16 2x2 packing and out_os 2")
@@ -706,9 +711,10 @@ def ctypes_byref(x):
 
 
 # --------------------------------------------------------------- spectral -----
-def spectral_conv2d(srcs: Sequence[Src], wpack: torch.Tensor, m1: int, m2: int, Cout: int,
-                    out: Optional[torch.Tensor] = None, accumulate=False, addend=None, act=0):
-    """y = irfft2(P(rfft2(x))) on the retained modes (proc_fno.py:257-288), NHWC in/out."""
+def spectral_z(srcs: Sequence[Src], wpack: torch.Tensor, m1: int, m2: int, Cout: int) -> torch.Tensor:
+    """Z (B, H, m2, Cout) complex64: the spectral conv up to its W-pass synthesis (rfft2 W and H passes on the
+    retained modes, the mode mixing, the inverse H pass; proc_fno.py:257-288) — spectral_conv2d's idft_w input, or the
+    spec_z a 1x1 conv's epilogue synthesises itself (conv2d(spec=...), the FNO layer fusion)."""
     t0 = srcs[0].t
     B, H, W = t0.shape[0], t0.shape[1], t0.shape[2]
     Cin = sum(s.t.shape[3] for s in srcs)
@@ -720,6 +726,31 @@ def spectral_conv2d(srcs: Sequence[Src], wpack: torch.Tensor, m1: int, m2: int, 
     X2 = torch.empty((B, R, m2, Cin), dtype=torch.complex64, device=dev)
     Y = torch.empty((B, R, m2, Cout), dtype=torch.complex64, device=dev)
     Z = torch.empty((B, H, m2, Cout), dtype=torch.complex64, device=dev)
+    s = stream_ptr()
+    check(lib.nps_spectral_dft_w(_c_src(srcs), len(srcs), B, H, W, Cin, m2, ptr(X1), s), "spectral_dft_w")
+    check(lib.nps_spectral_dft_h(ptr(X1), ptr(X2), B, H, m1, m2, Cin, s), "spectral_dft_h")
+    check(lib.nps_spectral_mix(ptr(X2), ptr(wpack), ptr(Y), B, R, m2, Cin, Cout, s), "spectral_mix")
+    check(lib.nps_spectral_idft_h(ptr(Y), ptr(Z), B, H, m1, m2, Cout, s), "spectral_idft_h")
+    return Z
+
+
+# the FNO layer's 1x1 `w` synthesises the spectral conv's W pass in its epilogue (nps_conv2d_t.spec_z) instead of a
+# separate idft_w read-modify-write of its output (dev knob NPS_FUSE_IDFT=0: off)
+FUSE_IDFT = os.environ.get("NPS_FUSE_IDFT", "1") != "0"
+
+
+def spectral_fusable(W: int, m2: int, Cout: int) -> bool:
+    """Whether conv2d(spec=...) can take this spectral conv's W pass (nps_conv2d_t.spec_z conditions)."""
+    return (FUSE_IDFT and CONV_PRECISION == PREC_X3F16 and X1_LDS_WEIGHTS and W % 128 == 0 and m2 <= 16
+            and Cout <= 192 and Cout % 4 == 0)
+
+
+def spectral_conv2d(srcs: Sequence[Src], wpack: torch.Tensor, m1: int, m2: int, Cout: int,
+                    out: Optional[torch.Tensor] = None, accumulate=False, addend=None, act=0):
+    """y = irfft2(P(rfft2(x))) on the retained modes (proc_fno.py:257-288), NHWC in/out."""
+    t0 = srcs[0].t
+    B, H, W = t0.shape[0], t0.shape[1], t0.shape[2]
+    Z = spectral_z(srcs, wpack, m1, m2, Cout)
     if out is not None:
         drop_stats(out)
     if out is None:
@@ -728,13 +759,8 @@ def spectral_conv2d(srcs: Sequence[Src], wpack: torch.Tensor, m1: int, m2: int, 
         tag = new_tag(out)
     else:
         tag = out_tag(out, accumulate)
-    s = stream_ptr()
-    check(lib.nps_spectral_dft_w(_c_src(srcs), len(srcs), B, H, W, Cin, m2, ptr(X1), s), "spectral_dft_w")
-    check(lib.nps_spectral_dft_h(ptr(X1), ptr(X2), B, H, m1, m2, Cin, s), "spectral_dft_h")
-    check(lib.nps_spectral_mix(ptr(X2), ptr(wpack), ptr(Y), B, R, m2, Cin, Cout, s), "spectral_mix")
-    check(lib.nps_spectral_idft_h(ptr(Y), ptr(Z), B, H, m1, m2, Cout, s), "spectral_idft_h")
     check(lib.nps_spectral_idft_w(ptr(Z), ptr(out), B, H, W, m2, Cout, 1 if accumulate else 0, ptr(addend), act,
-                                  tag, s), "spectral_idft_w")
+                                  tag, stream_ptr()), "spectral_idft_w")
     return out
 
 

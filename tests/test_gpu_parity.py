@@ -268,6 +268,34 @@ def test_fno_layer_golden():
     assert rel_l2(y, g["y"]) < TOL
 
 
+@pytest.mark.parametrize("H,W,m,cin,cout", [(256, 256, 10, 196, 192), (128, 128, 12, 196, 192), (64, 128, 5, 36, 44)])
+def test_fno_layer_fused_synthesis(H, W, m, cin, cout, monkeypatch):
+    """FNO_Layer (proc_fno.py:142-146: act(conv(x) + w(x))) with the spectral conv's W-pass synthesis done by the
+    1x1 `w`'s epilogue (nps_conv2d_t.spec_z, no idft_w launch) against the unfused HIP path (1x1, then idft_w
+    accumulating) and against torch (the oracle's spectral conv + a 1x1 conv + GELU)."""
+    from models.enc_proc_dec_components.proc_fno import FNO_Layer
+    from nps_hip import ops
+    if not ops.spectral_fusable(W, m, cout):
+        pytest.skip("fused synthesis off (split-fp16 1x1 on the LDS-weight kernel only)")
+    torch.manual_seed(3)
+    layer = FNO_Layer(cin, num_spatial_dims=2, modes=m, hidden_dim_out=cout).to(DEV)
+    x = torch.randn(2, cin, H, W)
+    calls = []
+    real = ops.lib.nps_spectral_idft_w
+    monkeypatch.setattr(ops.lib, "nps_spectral_idft_w", lambda *a: calls.append(1) or real(*a))
+    with torch.no_grad():  # (the inference path: the differentiable one runs the unfused kernels)
+        y = layer(x.to(DEV)).cpu()
+        assert calls == []  # synthesised in the 1x1 epilogue
+        monkeypatch.setattr(ops, "FUSE_IDFT", False)
+        y_ref = layer(x.to(DEV)).cpu()
+    assert calls == [1]
+    assert rel_l2(y, y_ref) < 1e-6
+    sc = layer.conv
+    ref = F.gelu(Fo.spectral_conv2d(x, sc.weights1.detach().cpu(), sc.weights2.detach().cpu()) +
+                 F.conv2d(x, layer.w.weight.detach().cpu(), layer.w.bias.detach().cpu()))
+    assert rel_l2(y, ref) < TOL
+
+
 # ------------------------------------------------------------------ processors
 def _proc(name):
     from models.enc_proc_dec_components import UNetModern, DilatedResnet, UFNO, FNO
