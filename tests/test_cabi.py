@@ -126,3 +126,30 @@ def test_fork_gate_reads_the_planners_tiles():
         assert ops.x3_plan_tiles(Ho, Wo, B, Cout, Cin) == want
     assert ops.idle_fraction(ops.x3_plan_tiles(258, 258, 2, 192, 388), 256) >= ops.SIDE_MIN_IDLE
     assert ops.idle_fraction(ops.x3_plan_tiles(256, 256, 2, 192, 192), 256) == 0.0
+
+
+def test_fused_synthesis_arguments_are_checked_on_the_host():
+    """nps_conv2d_t.spec_z (the FNO layer's W-pass synthesis in the 1x1 epilogue) is refused by nps_conv2d_fwd's
+    host checks — before any launch — outside its conditions (an accumulating conv, a 3x3, a row not a multiple of
+    128 pixels, m2 > 16); ops.spectral_fusable mirrors them on the Python side."""
+    import nps_hip
+    from nps_hip import ops
+    lib = nps_hip.lib
+    bad = []
+    for tweak in ("accumulate", "k3", "w", "m2"):
+        k = 3 if tweak == "k3" else 1
+        W = 200 if tweak == "w" else 256
+        a = _plan_args(192, 192, k, H=8 + k - 1, W=W + k - 1)
+        a.out = 0x5000
+        a.wpack = 0x6000
+        a.spec_z, a.spec_m2, a.spec_scale = 0x7000, (20 if tweak == "m2" else 10), 1.0 / (8 * W)
+        if tweak == "accumulate":
+            a.accumulate = 1
+        assert lib.nps_conv2d_plan(ctypes.byref(a)) >= 0
+        rc = lib.nps_conv2d_fwd(ctypes.byref(a), None)
+        bad.append((tweak, rc, lib.nps_last_error().decode()))
+    assert all(rc < 0 and "spec_z" in msg for _, rc, msg in bad), bad
+    assert ops.spectral_fusable(256, 10, 192) == (ops.FUSE_IDFT and ops.CONV_PRECISION == ops.PREC_X3F16 and
+                                                  ops.X1_LDS_WEIGHTS)
+    assert not ops.spectral_fusable(200, 10, 192) and not ops.spectral_fusable(256, 17, 192)
+    assert not ops.spectral_fusable(256, 10, 225)
