@@ -12,6 +12,7 @@ Reference semantics: trainers/base.py:492 `loss.backward()` over the modules of
 models/ (see each Function's docstring for the op it differentiates).
 """
 import ctypes
+import os
 from typing import List, Optional, Sequence
 
 import torch
@@ -121,6 +122,20 @@ def channel_sums(x: torch.Tensor) -> torch.Tensor:
     out = torch.zeros(C, dtype=torch.float32, device=x.device)
     check(lib.nps_channel_sums(ptr(x), x.numel() // C, C, ptr(out), stream_ptr()), "channel_sums")
     return out
+
+
+# Training forward convs carry the GroupNorm(1) moments of their outputs (nps_conv2d_t.out_stats), so the
+# differentiable frames' group_norm_stats sums them instead of a statistics pass (dev knob NPS_CARRY_TRAIN=0: off)
+CARRY_TRAIN = os.environ.get("NPS_CARRY_TRAIN", "1") != "0"
+
+
+def _carry_buffer(x):
+    return ops.new_stats(x.shape[0], x) if CARRY_TRAIN and x.is_cuda and ops.CONV_PRECISION == ops.PREC_X3F16 else None
+
+
+def _carry(y, st):
+    if st is not None:
+        ops.attach_stats(y, st)  # (ignored when the conv's kernel could not take the moments: incomplete)
 
 
 def _pack_plain(w, dil=1):
@@ -240,14 +255,18 @@ class Conv2dFn(torch.autograd.Function):
             p = lo[0]
             Ho, Wo = (H + 2 * p - 3) // 2 + 1, (W + 2 * p - 3) // 2 + 1
             xq = ops.space_to_depth(x, p, Ho + 1, Wo + 1)
+            st = _carry_buffer(x)
             y = ops.conv2d([Src(xq)], (Ho + 1, Wo + 1), ops.cached_pack(weight, "s2d", ops.pack_conv_weight_s2d),
                            bias, Cout, 2, 2,
-                           out_hw=(Ho, Wo))
+                           out_hw=(Ho, Wo), out_stats=st)
+            _carry(y, st)
             ctx.save_for_backward(xq, weight)
         elif s == 1:
             wp = ops.cached_pack(weight, ("conv", 1, d), lambda w: ops.pack_conv_weight(w, 1, d))
+            st = _carry_buffer(x)
             y = ops.conv2d([Src(x)], (H, W), wp, bias, Cout, KH, KW, dil=d, pad=lo,
-                           pad_bottom=hi, circ=circ)
+                           pad_bottom=hi, circ=circ, out_stats=st)
+            _carry(y, st)
             ctx.save_for_backward(x, weight)
         else:
             raise NotImplementedError(f"conv stride {s}")
@@ -323,10 +342,12 @@ class ConvTranspose2dFn(torch.autograd.Function):
         Ho, Wo = 2 * Hp + 2 - 2 * p, 2 * Wp + 2 - 2 * p
         out = ops.empty_nhwc(B, Ho, Wo, Cout, x)
         phases = ops.cached_pack(weight, "convT", ops.pack_convT_phases)
+        st = _carry_buffer(x)  # (the 4 phases write disjoint elements: their moments add up to out's)
         for ph in range(4):
             py, px = ph >> 1, ph & 1
             ops.conv2d([Src(x)], (H, W), phases[ph], bias, Cout, 2, 2, pad=(1, 1), circ=c, out_hw=(Hp + 1, Wp + 1),
-                       out=out, out_os=2, out_off=(py - p, px - p))
+                       out=out, out_os=2, out_off=(py - p, px - p), out_stats=st)
+        _carry(out, st)
         ctx.geo, ctx.has_bias = geo, bias is not None
         ctx.save_for_backward(x, weight)
         return out
