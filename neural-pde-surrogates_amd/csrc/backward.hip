@@ -254,6 +254,29 @@ __global__ void add_at_kernel(float* __restrict__ out, const float* __restrict__
     }
 }
 
+// out = base + crop_Nd(src) at (oy, ox) in one pass (4-channel quads; the residual of proc_unet_modern.py:250 in the
+// differentiable path): out pixel (Y, X) adds src pixel (Y - oy, X - ox) where that lies inside src — instead of
+// clone(base) + add_at (5 tensor streams -> 3)
+__global__ void add_at_copy4_kernel(float* __restrict__ out, const float* __restrict__ base,
+                                    const float* __restrict__ src, int Ho, int Wo, int Hs, int Ws, int C, int oy,
+                                    int ox) {
+    const int b = blockIdx.y;
+    const int Q = C >> 2;
+    const long n = (long)Ho * Wo * Q;
+    const f32x4* bq = reinterpret_cast<const f32x4*>(base) + (size_t)b * n;
+    f32x4* oq = reinterpret_cast<f32x4*>(out) + (size_t)b * n;
+    const f32x4* sq = reinterpret_cast<const f32x4*>(src) + (size_t)b * Hs * Ws * Q;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+        const int q = (int)(i % Q);
+        const long pix = i / Q;
+        const int Y = (int)(pix / Wo), X = (int)(pix - (long)Y * Wo);
+        const int y = Y - oy, x = X - ox;
+        f32x4 v = bq[i];
+        if (y >= 0 && y < Hs && x >= 0 && x < Ws) v += sq[((size_t)y * Ws + x) * Q + q];
+        oq[i] = v;
+    }
+}
+
 // out[b][Y][X][c] = x[b][(Y - pad) mod H][(X - pad) mod W][c]   (circular_pad_2d, common.py:61-90)
 __global__ void circ_pad_kernel(const float* __restrict__ x, float* __restrict__ out, int H, int W, int C, int pad) {
     const int b = blockIdx.y;
@@ -692,6 +715,18 @@ extern "C" int nps_add_at(float* out, const float* src, int B, int Ho, int Wo, i
     add_at_kernel<<<dim3(grid_for((long)Hs * Ws * C, 256 * 8, 2048), B), 256, 0, (hipStream_t)stream>>>(
         out, src, Ho, Wo, Hs, Ws, C, off_y, off_x);
     NPS_CHECK_LAUNCH("add_at");
+    return 0;
+}
+
+extern "C" int nps_add_at_copy(float* out, const float* base, const float* src, int B, int Ho, int Wo, int Hs, int Ws,
+                               int C, int off_y, int off_x, void* stream) {
+    NPS_CHECK_ARG(out && base && src && B > 0 && Ho > 0 && Wo > 0 && Hs > 0 && Ws > 0 && C > 0 && (C & 3) == 0 &&
+                      ((reinterpret_cast<size_t>(out) | reinterpret_cast<size_t>(base) |
+                        reinterpret_cast<size_t>(src)) & 15) == 0,
+                  "add_at_copy: bad args (C %% 4 == 0, 16-B aligned tensors)");
+    add_at_copy4_kernel<<<dim3(grid_for((long)Ho * Wo * (C / 4), 256 * 4, 2048), B), 256, 0, (hipStream_t)stream>>>(
+        out, base, src, Ho, Wo, Hs, Ws, C, off_y, off_x);
+    NPS_CHECK_LAUNCH("add_at_copy");
     return 0;
 }
 

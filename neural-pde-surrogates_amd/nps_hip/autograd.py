@@ -129,6 +129,11 @@ def channel_sums(x: torch.Tensor) -> torch.Tensor:
 CARRY_TRAIN = os.environ.get("NPS_CARRY_TRAIN", "1") != "0"
 
 
+# the residual add of the differentiable path in one pass (nps_add_at_copy) instead of clone + nps_add_at
+# (dev knob NPS_ADD_AT_COPY=0: off)
+ADD_AT_COPY = os.environ.get("NPS_ADD_AT_COPY", "1") != "0"
+
+
 def _carry_buffer(x):
     return ops.new_stats(x.shape[0], x) if CARRY_TRAIN and x.is_cuda and ops.CONV_PRECISION == ops.PREC_X3F16 else None
 
@@ -439,10 +444,15 @@ class AddAtFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, off, base, src):
         base, src = _c(base), _c(src)
-        out = base.clone()
         B, Ho, Wo, C = base.shape
         Hs, Ws = src.shape[1:3]
-        check(lib.nps_add_at(ptr(out), ptr(src), B, Ho, Wo, Hs, Ws, C, off[0], off[1], stream_ptr()), "add_at")
+        if C % 4 == 0 and ADD_AT_COPY:  # one pass: out = base + crop_Nd(src) (nps_add_at_copy)
+            out = torch.empty_like(base)
+            check(lib.nps_add_at_copy(ptr(out), ptr(base), ptr(src), B, Ho, Wo, Hs, Ws, C, off[0], off[1],
+                                      stream_ptr()), "add_at_copy")
+        else:
+            out = base.clone()
+            check(lib.nps_add_at(ptr(out), ptr(src), B, Ho, Wo, Hs, Ws, C, off[0], off[1], stream_ptr()), "add_at")
         ctx.off, ctx.src_hw = off, (Hs, Ws)
         return out
 

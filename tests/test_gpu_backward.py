@@ -459,3 +459,29 @@ def test_dgrad_packing_equals_flipped_transpose(cout, cin, k, dil):
     assert got.nps_precision == ref.nps_precision
     body = got.numel() - 64 + 1  # fragment body + trailer[0] (max|w|); the rest of the trailer is unwritten
     assert torch.equal(got[:body], ref[:body])
+
+
+@pytest.mark.parametrize("off,src_hw,C", [((1, -1), (10, 16), 8), ((0, 0), (12, 14), 4), ((-2, 3), (15, 9), 6)])
+def test_add_at_forward_and_backward(off, src_hw, C):
+    """ad.add_at (the residual crop_Nd(h) + shortcut, proc_unet_modern.py:250) — the one-pass nps_add_at_copy for
+    C % 4 == 0, clone + nps_add_at otherwise — and its gradients, against torch on the same placement."""
+    from nps_hip import autograd as ad
+    torch.manual_seed(2)
+    base = torch.randn(2, 12, 14, C, device=DEV, requires_grad=True)
+    src = torch.randn(2, *src_hw, C, device=DEV, requires_grad=True)
+    y = ad.add_at(base, src, off)
+    g = torch.randn_like(y)
+    y.backward(g)
+    bd, sd = base.detach().cpu().double(), src.detach().cpu().double()
+    ref = bd.clone()
+    oy, ox = off
+    Hs, Ws = src_hw
+    y0, y1 = max(0, oy), min(12, oy + Hs)
+    x0, x1 = max(0, ox), min(14, ox + Ws)
+    ref[:, y0:y1, x0:x1] += sd[:, y0 - oy:y1 - oy, x0 - ox:x1 - ox]
+    assert torch.allclose(y.detach().cpu().double(), ref, atol=1e-6)
+    gd = g.cpu().double()
+    assert torch.allclose(base.grad.cpu().double(), gd, atol=1e-6)
+    gs = torch.zeros_like(sd)
+    gs[:, y0 - oy:y1 - oy, x0 - ox:x1 - ox] = gd[:, y0:y1, x0:x1]
+    assert torch.allclose(src.grad.cpu().double(), gs, atol=1e-6)
