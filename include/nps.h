@@ -358,9 +358,11 @@ int nps_gelu_bwd(const float* x, const float* gy, float* gx, long n, void* strea
 /* out[b][y+off_y][x+off_x][c] += src[b][y][x][c] (crop_Nd(h) + shortcut, proc_unet_modern.py:250) */
 int nps_add_at(float* out, const float* src, int B, int Ho, int Wo, int Hs, int Ws, int C, int off_y, int off_x,
                void* stream);
-/* out = base + that placement of src, in one pass (out, base: [B][Ho][Wo][C]; C % 4 == 0, 16-B aligned) */
+/* out = base + that placement of src, in one pass (out, base: [B][Ho][Wo][C]; C % 4 == 0, 16-B aligned);
+   out_stats: NULL, or [B][NPS_STATS_SUB][2] fp64 to which the launch ADDS out's GroupNorm(1) moments (sum, sum of
+   squares per sample), as nps_conv2d_t.out_stats */
 int nps_add_at_copy(float* out, const float* base, const float* src, int B, int Ho, int Wo, int Hs, int Ws, int C,
-                    int off_y, int off_x, void* stream);
+                    int off_y, int off_x, double* out_stats, void* stream);
 /* circular_pad_2d (models/common.py:61-90) on NHWC and its adjoint (wrap-sum) */
 int nps_circular_pad(const float* x, float* out, int B, int H, int W, int C, int pad, void* stream);
 int nps_circular_fold(const float* gp, float* gx, int B, int H, int W, int C, int pad, void* stream);

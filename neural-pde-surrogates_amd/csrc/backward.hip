@@ -257,15 +257,19 @@ __global__ void add_at_kernel(float* __restrict__ out, const float* __restrict__
 // out = base + crop_Nd(src) at (oy, ox) in one pass (4-channel quads; the residual of proc_unet_modern.py:250 in the
 // differentiable path): out pixel (Y, X) adds src pixel (Y - oy, X - ox) where that lies inside src — instead of
 // clone(base) + add_at (5 tensor streams -> 3)
-__global__ void add_at_copy4_kernel(float* __restrict__ out, const float* __restrict__ base,
-                                    const float* __restrict__ src, int Ho, int Wo, int Hs, int Ws, int C, int oy,
-                                    int ox) {
+// out = base + crop_Nd(src) in one pass; STATS: also ADDS out's per-sample (sum, sum of squares) into
+// out_stats[b][blockIdx.x % NPS_STATS_SUB] (fp64; one atomic pair per work-group after an LDS reduction)
+template <bool STATS>
+__global__ __launch_bounds__(256) void add_at_copy4_kernel(float* __restrict__ out, const float* __restrict__ base,
+                                                           const float* __restrict__ src, int Ho, int Wo, int Hs,
+                                                           int Ws, int C, int oy, int ox, double* out_stats) {
     const int b = blockIdx.y;
     const int Q = C >> 2;
     const long n = (long)Ho * Wo * Q;
     const f32x4* bq = reinterpret_cast<const f32x4*>(base) + (size_t)b * n;
     f32x4* oq = reinterpret_cast<f32x4*>(out) + (size_t)b * n;
     const f32x4* sq = reinterpret_cast<const f32x4*>(src) + (size_t)b * Hs * Ws * Q;
+    double s1 = 0.0, s2 = 0.0;
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
         const int q = (int)(i % Q);
         const long pix = i / Q;
@@ -274,6 +278,27 @@ __global__ void add_at_copy4_kernel(float* __restrict__ out, const float* __rest
         f32x4 v = bq[i];
         if (y >= 0 && y < Hs && x >= 0 && x < Ws) v += sq[((size_t)y * Ws + x) * Q + q];
         oq[i] = v;
+        if constexpr (STATS) {
+            // (the 4 lanes' partials in fp32 as the conv epilogues' store_tile_s, then fp64)
+            s1 += (double)((v[0] + v[1]) + (v[2] + v[3]));
+            s2 += (double)((v[0] * v[0] + v[1] * v[1]) + (v[2] * v[2] + v[3] * v[3]));
+        }
+    }
+    if constexpr (STATS) {
+        __shared__ double red[2 * 4];
+        s1 = nps::wave_sum(s1);
+        s2 = nps::wave_sum(s2);
+        const int w = (int)(threadIdx.x >> 6);
+        if ((threadIdx.x & 63) == 0) {
+            red[2 * w] = s1;
+            red[2 * w + 1] = s2;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double* p = out_stats + ((size_t)b * NPS_STATS_SUB + blockIdx.x % NPS_STATS_SUB) * 2;
+            atomicAdd(p, ((red[0] + red[2]) + (red[4] + red[6])));
+            atomicAdd(p + 1, ((red[1] + red[3]) + (red[5] + red[7])));
+        }
     }
 }
 
@@ -719,13 +744,18 @@ extern "C" int nps_add_at(float* out, const float* src, int B, int Ho, int Wo, i
 }
 
 extern "C" int nps_add_at_copy(float* out, const float* base, const float* src, int B, int Ho, int Wo, int Hs, int Ws,
-                               int C, int off_y, int off_x, void* stream) {
+                               int C, int off_y, int off_x, double* out_stats, void* stream) {
     NPS_CHECK_ARG(out && base && src && B > 0 && Ho > 0 && Wo > 0 && Hs > 0 && Ws > 0 && C > 0 && (C & 3) == 0 &&
                       ((reinterpret_cast<size_t>(out) | reinterpret_cast<size_t>(base) |
                         reinterpret_cast<size_t>(src)) & 15) == 0,
                   "add_at_copy: bad args (C %% 4 == 0, 16-B aligned tensors)");
-    add_at_copy4_kernel<<<dim3(grid_for((long)Ho * Wo * (C / 4), 256 * 4, 2048), B), 256, 0, (hipStream_t)stream>>>(
-        out, base, src, Ho, Wo, Hs, Ws, C, off_y, off_x);
+    const dim3 grid(grid_for((long)Ho * Wo * (C / 4), 256 * 4, 2048), B);
+    if (out_stats)
+        add_at_copy4_kernel<true><<<grid, 256, 0, (hipStream_t)stream>>>(out, base, src, Ho, Wo, Hs, Ws, C, off_y,
+                                                                          off_x, out_stats);
+    else
+        add_at_copy4_kernel<false><<<grid, 256, 0, (hipStream_t)stream>>>(out, base, src, Ho, Wo, Hs, Ws, C, off_y,
+                                                                           off_x, nullptr);
     NPS_CHECK_LAUNCH("add_at_copy");
     return 0;
 }

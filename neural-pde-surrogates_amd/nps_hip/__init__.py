@@ -130,7 +130,7 @@ _SIGS = {
     "nps_gelu": (_i, [_vp, _vp, _l, _vp]),
     "nps_gelu_bwd": (_i, [_vp, _vp, _vp, _l, _vp]),
     "nps_add_at": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp]),
-    "nps_add_at_copy": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp]),
+    "nps_add_at_copy": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
     "nps_circular_pad": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp]),
     "nps_circular_fold": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp]),
     "nps_scaled_diff": (_i, [_vp, _vp, _vp, _vp, _l, _vp]),

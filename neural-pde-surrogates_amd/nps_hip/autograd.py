@@ -132,6 +132,12 @@ CARRY_TRAIN = os.environ.get("NPS_CARRY_TRAIN", "1") != "0"
 # the residual add of the differentiable path in one pass (nps_add_at_copy) instead of clone + nps_add_at
 # (dev knob NPS_ADD_AT_COPY=0: off)
 ADD_AT_COPY = os.environ.get("NPS_ADD_AT_COPY", "1") != "0"
+# ... which also carries the sum's GroupNorm(1) moments (dev knob NPS_CARRY_ADD=0: off)
+CARRY_ADD = os.environ.get("NPS_CARRY_ADD", "1") != "0"
+
+
+# bias gradients (channel sums of dy) on the weight gradient's side stream (dev knob NPS_SIDE_DB=0: main stream)
+SIDE_DB = os.environ.get("NPS_SIDE_DB", "1") != "0"
 
 
 def _carry_buffer(x):
@@ -327,8 +333,10 @@ class Conv2dFn(torch.autograd.Function):
                     G = wgrad(gy, xs, 2, 2, a_range=rng)                       # [Cout][4C][2][2]
                     G = G.view(Cout, 2, 2, C, 2, 2).permute(0, 3, 4, 1, 5, 2).reshape(Cout, C, 4, 4)
                     dw = G[:, :, :3, :3].contiguous()
-            fork.join(dw)
-        if ctx.has_bias and ctx.needs_input_grad[3]:
+                if ctx.has_bias and ctx.needs_input_grad[3] and SIDE_DB:
+                    db = channel_sums(gy)  # (reads gy only: beside the input-gradient conv too)
+            fork.join(dw, db)
+        if ctx.has_bias and ctx.needs_input_grad[3] and db is None:
             db = channel_sums(gy)
         return None, dx, dw, db
 
@@ -389,8 +397,10 @@ class ConvTranspose2dFn(torch.autograd.Function):
                     xp = x
                 G = wgrad(xp, dq, 2, 2)                                            # [Cin][4 Cout][2][2]
                 dw = G.view(Cin, 2, 2, Cout, 2, 2).permute(0, 3, 4, 1, 5, 2).reshape(Cin, Cout, 4, 4).contiguous()
-            fork.join(dw)
-        if ctx.has_bias and ctx.needs_input_grad[3]:
+                if ctx.has_bias and ctx.needs_input_grad[3] and SIDE_DB:
+                    db = channel_sums(gout)
+            fork.join(dw, db)
+        if ctx.has_bias and ctx.needs_input_grad[3] and db is None:
             db = channel_sums(gout)
         return None, dx, dw, db
 
@@ -448,8 +458,10 @@ class AddAtFn(torch.autograd.Function):
         Hs, Ws = src.shape[1:3]
         if C % 4 == 0 and ADD_AT_COPY:  # one pass: out = base + crop_Nd(src) (nps_add_at_copy)
             out = torch.empty_like(base)
-            check(lib.nps_add_at_copy(ptr(out), ptr(base), ptr(src), B, Ho, Wo, Hs, Ws, C, off[0], off[1],
+            st = _carry_buffer(base) if CARRY_ADD else None  # out's GroupNorm(1) moments, for the next frame
+            check(lib.nps_add_at_copy(ptr(out), ptr(base), ptr(src), B, Ho, Wo, Hs, Ws, C, off[0], off[1], ptr(st),
                                       stream_ptr()), "add_at_copy")
+            _carry(out, st)
         else:
             out = base.clone()
             check(lib.nps_add_at(ptr(out), ptr(src), B, Ho, Wo, Hs, Ws, C, off[0], off[1], stream_ptr()), "add_at")

@@ -480,6 +480,15 @@ def test_add_at_forward_and_backward(off, src_hw, C):
     x0, x1 = max(0, ox), min(14, ox + Ws)
     ref[:, y0:y1, x0:x1] += sd[:, y0 - oy:y1 - oy, x0 - ox:x1 - ox]
     assert torch.allclose(y.detach().cpu().double(), ref, atol=1e-6)
+    from nps_hip import ops
+    st = ops.stats_of(y)  # the one-pass form carries y's GroupNorm(1) moments for the next frame
+    if C % 4 == 0 and ad.ADD_AT_COPY and ad.CARRY_ADD and ops.CONV_PRECISION == ops.PREC_X3F16:
+        assert st is not None
+        m = st.detach().cpu().sum(1)
+        assert torch.allclose(m[:, 0], ref.sum((1, 2, 3)), rtol=1e-6, atol=1e-6)
+        assert torch.allclose(m[:, 1], (ref * ref).sum((1, 2, 3)), rtol=1e-6)
+    else:
+        assert st is None
     gd = g.cpu().double()
     assert torch.allclose(base.grad.cpu().double(), gd, atol=1e-6)
     gs = torch.zeros_like(sd)
