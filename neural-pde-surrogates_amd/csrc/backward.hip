@@ -412,6 +412,47 @@ __global__ void frame_bwd_reduce_kernel(nps_conv2d_t a, const float* __restrict_
     }
 }
 
+// s12[g] = (sum over the group's channels of gamma[c] * (P, Q)[b][c]) / N, the GroupNorm backward's two group
+// means, computed by the whole work-group (every thread a strided share of its group's channels, wave sums,
+// fp64 LDS adds); then __syncthreads.  (Was one thread per group walking Cin / groups channels of L2 loads while
+// the work-group's other waves waited: with GroupNorm(1), 2 x Cin dependent-issue loads before any pixel.)
+__device__ __forceinline__ void frame_bwd_s12(const nps_conv2d_t& a, const double* __restrict__ PQ, int b, int cpg,
+                                              float (*s12)[2]) {
+    __shared__ double acc[16][2];
+    const int G = a.gn_groups;
+    if (threadIdx.x < 2 * G) (&acc[0][0])[threadIdx.x] = 0.0;
+    __syncthreads();
+    const int tpg = (int)blockDim.x / G;  // (G <= 16: >= 16 threads per group)
+    const int g = (int)threadIdx.x / tpg, j = (int)threadIdx.x - g * tpg;
+    const double* P = PQ + (size_t)(b * 2) * a.Cin;
+    const double* Q = P + a.Cin;
+    double s1 = 0.0, s2 = 0.0;
+    if (g < G)
+        for (int c = g * cpg + j; c < (g + 1) * cpg; c += tpg) {
+            const double ga = (double)a.gn_gamma[c];
+            s1 += ga * P[c];
+            s2 += ga * Q[c];
+        }
+    const int wg0 = __shfl(g, 0), wg1 = __shfl(g, 63);
+    if (wg0 == wg1) {  // the whole wave in one group: one LDS add pair per wave
+        s1 = nps::wave_sum(s1);
+        s2 = nps::wave_sum(s2);
+        if ((threadIdx.x & 63) == 0 && g < G) {
+            atomicAdd(&acc[g][0], s1);
+            atomicAdd(&acc[g][1], s2);
+        }
+    } else if (g < G) {
+        atomicAdd(&acc[g][0], s1);
+        atomicAdd(&acc[g][1], s2);
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < G) {
+        const double N = (double)cpg * a.Hin * a.Win;
+        s12[threadIdx.x][0] = (float)(acc[threadIdx.x][0] / N);
+        s12[threadIdx.x][1] = (float)(acc[threadIdx.x][1] / N);
+    }
+}
+
 __global__ void frame_bwd_apply_kernel(nps_conv2d_t a, const float* __restrict__ gy, const double* __restrict__ PQ,
                                        float* d0, float* d1, float* d2, float* __restrict__ dgamma,
                                        float* __restrict__ dbeta) {
@@ -420,16 +461,7 @@ __global__ void frame_bwd_apply_kernel(nps_conv2d_t a, const float* __restrict__
     const int b = blockIdx.y, si = blockIdx.z;
     gn_tab_fill(a, b, tab);
     const int cpg = a.gn_stats ? a.Cin / a.gn_groups : 1;
-    if (a.gn_stats && threadIdx.x < a.gn_groups) {
-        double s1 = 0.0, s2 = 0.0;
-        for (int c = threadIdx.x * cpg; c < (threadIdx.x + 1) * cpg; ++c) {
-            s1 += (double)a.gn_gamma[c] * PQ[(b * 2) * a.Cin + c];
-            s2 += (double)a.gn_gamma[c] * PQ[(b * 2 + 1) * a.Cin + c];
-        }
-        const double N = (double)cpg * a.Hin * a.Win;
-        s12[threadIdx.x][0] = (float)(s1 / N);
-        s12[threadIdx.x][1] = (float)(s2 / N);
-    }
+    if (a.gn_stats) frame_bwd_s12(a, PQ, b, cpg, s12);
     if (a.gn_stats && b == 0 && si == 0 && blockIdx.x == 0 && dgamma) {
         for (int c = threadIdx.x; c < a.Cin; c += blockDim.x) {
             double sg = 0.0, sb = 0.0;
@@ -478,6 +510,9 @@ __global__ void frame_bwd_apply_kernel(nps_conv2d_t a, const float* __restrict__
 // a channel quad lies in one source and one group): thread = one fixed channel quad x pixels lr, lr + per,
 // ... of the block's pixel range (row / column stepped, no per-element division), 16-B loads and stores,
 // the reduce pass's sums in registers until one LDS add per channel per thread.
+#ifndef FB_U
+#define FB_U 4  // pixels per loop step of the quad frame-backward kernels
+#endif
 struct FrameQuad {  // the source, GroupNorm operands and source origin of a thread's channel quad
     const float* ptr;
     int C, H, W, oy, ox, cs;
@@ -538,24 +573,38 @@ __global__ void frame_bwd_reduce4_kernel(nps_conv2d_t a, const float* __restrict
         int pix = p0 + lr;
         int y = pix / a.Win, x = pix - y * a.Win;
         const int dy = per / a.Win, dx = per - dy * a.Win;
-        for (; pix < p1; pix += per) {
-            const int yy = y - f.oy, xx = x - f.ox;
-            f32x4 v = {0.f, 0.f, 0.f, 0.f};
-            if (yy >= 0 && yy < f.H && xx >= 0 && xx < f.W) v = *reinterpret_cast<const f32x4*>(sb + ((size_t)yy * f.W + xx) * f.C);
-            f32x4 gz = *reinterpret_cast<const f32x4*>(g + (size_t)pix * a.Cin);
+        // FB_U pixels per step: all their loads issue before the first use (memory-level parallelism)
+        for (; pix < p1; pix += FB_U * per) {
+            f32x4 v[FB_U], gz[FB_U];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const float xh = a.gn_stats ? (v[e] - f.mr.x) * f.mr.y : v[e];
-                const float z = a.gn_stats ? xh * f.gam[e] + f.bet[e] : v[e];
-                if (a.pre_act == 1) gz[e] *= gelu_grad(z);
-                P[e] += gz[e];
-                Qs[e] = fmaf(gz[e], xh, Qs[e]);
+            for (int k = 0; k < FB_U; ++k) {
+                const int pk = pix + k * per;
+                const int yy = y - f.oy, xx = x - f.ox;
+                v[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+                gz[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+                if (pk < p1) {
+                    if (yy >= 0 && yy < f.H && xx >= 0 && xx < f.W)
+                        v[k] = *reinterpret_cast<const f32x4*>(sb + ((size_t)yy * f.W + xx) * f.C);
+                    gz[k] = *reinterpret_cast<const f32x4*>(g + (size_t)pk * a.Cin);
+                }
+                x += dx;
+                y += dy;
+                if (x >= a.Win) {
+                    x -= a.Win;
+                    ++y;
+                }
             }
-            x += dx;
-            y += dy;
-            if (x >= a.Win) {
-                x -= a.Win;
-                ++y;
+#pragma unroll
+            for (int k = 0; k < FB_U; ++k) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {  // (a pixel past p1 has gz = 0: adds nothing)
+                    const float xh = a.gn_stats ? (v[k][e] - f.mr.x) * f.mr.y : v[k][e];
+                    const float z = a.gn_stats ? xh * f.gam[e] + f.bet[e] : v[k][e];
+                    float gk = gz[k][e];
+                    if (a.pre_act == 1) gk *= gelu_grad(z);
+                    P[e] += gk;
+                    Qs[e] = fmaf(gk, xh, Qs[e]);
+                }
             }
         }
 #pragma unroll
@@ -582,16 +631,7 @@ __global__ void frame_bwd_apply4_kernel(nps_conv2d_t a, const float* __restrict_
     const int b = blockIdx.y, si = blockIdx.z;
     gn_tab_fill(a, b, tab);
     const int cpg = a.gn_stats ? a.Cin / a.gn_groups : 1;
-    if (a.gn_stats && threadIdx.x < a.gn_groups) {
-        double s1 = 0.0, s2 = 0.0;
-        for (int c = threadIdx.x * cpg; c < (threadIdx.x + 1) * cpg; ++c) {
-            s1 += (double)a.gn_gamma[c] * PQ[(b * 2) * a.Cin + c];
-            s2 += (double)a.gn_gamma[c] * PQ[(b * 2 + 1) * a.Cin + c];
-        }
-        const double N = (double)cpg * a.Hin * a.Win;
-        s12[threadIdx.x][0] = (float)(s1 / N);
-        s12[threadIdx.x][1] = (float)(s2 / N);
-    }
+    if (a.gn_stats) frame_bwd_s12(a, PQ, b, cpg, s12);
     if (a.gn_stats && b == 0 && si == 0 && blockIdx.x == 0 && dgamma) {
         for (int c = threadIdx.x; c < a.Cin; c += blockDim.x) {
             double sg = 0.0, sb = 0.0;
@@ -629,31 +669,49 @@ __global__ void frame_bwd_apply4_kernel(nps_conv2d_t a, const float* __restrict_
     int pix = p0 + lr;
     int ys = pix / S.W, xs = pix - ys * S.W;
     const int dy = per / S.W, dx = per - dy * S.W;
-    for (; pix < p1; pix += per) {
-        const int y = ys + S.off_y, x = xs + S.off_x;
-        f32x4 d = {0.f, 0.f, 0.f, 0.f};
-        if (y >= 0 && y < a.Hin && x >= 0 && x < a.Win) {
-            const f32x4 v = *reinterpret_cast<const f32x4*>(sp + (size_t)pix * S.C);
-            f32x4 gz = *reinterpret_cast<const f32x4*>(g + ((size_t)y * a.Win + x) * a.Cin);
+    for (; pix < p1; pix += FB_U * per) {
+        f32x4 v[FB_U], gz[FB_U];
+        bool in[FB_U];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                if (a.gn_stats) {
-                    const float xh = (v[e] - mr.x) * mr.y;
-                    if (a.pre_act == 1) gz[e] *= gelu_grad(xh * gam[e] + bet[e]);
-                    d[e] = mr.y * (gam[e] * gz[e] - t1 - xh * t2);
-                } else {
-                    if (a.pre_act == 1) gz[e] *= gelu_grad(v[e]);
-                    d[e] = gz[e];
-                }
+        for (int k = 0; k < FB_U; ++k) {  // FB_U pixels' loads first, then their math and stores
+            const int pk = pix + k * per;
+            const int y = ys + S.off_y, x = xs + S.off_x;
+            in[k] = pk < p1 && y >= 0 && y < a.Hin && x >= 0 && x < a.Win;
+            v[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+            gz[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (in[k]) {
+                v[k] = *reinterpret_cast<const f32x4*>(sp + (size_t)pk * S.C);
+                gz[k] = *reinterpret_cast<const f32x4*>(g + ((size_t)y * a.Win + x) * a.Cin);
+            }
+            xs += dx;
+            ys += dy;
+            if (xs >= S.W) {
+                xs -= S.W;
+                ++ys;
             }
         }
-        *reinterpret_cast<f32x4*>(dp + (size_t)pix * S.C) = d;
-        amax = fmaxf(amax, fmaxf(fmaxf(fabsf(d[0]), fabsf(d[1])), fmaxf(fabsf(d[2]), fabsf(d[3]))));
-        xs += dx;
-        ys += dy;
-        if (xs >= S.W) {
-            xs -= S.W;
-            ++ys;
+#pragma unroll
+        for (int k = 0; k < FB_U; ++k) {
+            const int pk = pix + k * per;
+            if (pk >= p1) break;
+            f32x4 d = {0.f, 0.f, 0.f, 0.f};
+            if (in[k]) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    if (a.gn_stats) {
+                        const float xh = (v[k][e] - mr.x) * mr.y;
+                        float gk = gz[k][e];
+                        if (a.pre_act == 1) gk *= gelu_grad(xh * gam[e] + bet[e]);
+                        d[e] = mr.y * (gam[e] * gk - t1 - xh * t2);
+                    } else {
+                        float gk = gz[k][e];
+                        if (a.pre_act == 1) gk *= gelu_grad(v[k][e]);
+                        d[e] = gk;
+                    }
+                }
+            }
+            *reinterpret_cast<f32x4*>(dp + (size_t)pk * S.C) = d;
+            amax = fmaxf(amax, fmaxf(fmaxf(fabsf(d[0]), fabsf(d[1])), fmaxf(fabsf(d[2]), fabsf(d[3]))));
         }
     }
     }
