@@ -136,10 +136,6 @@ ADD_AT_COPY = os.environ.get("NPS_ADD_AT_COPY", "1") != "0"
 CARRY_ADD = os.environ.get("NPS_CARRY_ADD", "1") != "0"
 
 
-# bias gradients (channel sums of dy) on the weight gradient's side stream (dev knob NPS_SIDE_DB=0: main stream)
-SIDE_DB = os.environ.get("NPS_SIDE_DB", "1") != "0"
-
-
 def _carry_buffer(x):
     return ops.new_stats(x.shape[0], x) if CARRY_TRAIN and x.is_cuda and ops.CONV_PRECISION == ops.PREC_X3F16 else None
 
@@ -333,10 +329,8 @@ class Conv2dFn(torch.autograd.Function):
                     G = wgrad(gy, xs, 2, 2, a_range=rng)                       # [Cout][4C][2][2]
                     G = G.view(Cout, 2, 2, C, 2, 2).permute(0, 3, 4, 1, 5, 2).reshape(Cout, C, 4, 4)
                     dw = G[:, :, :3, :3].contiguous()
-                if ctx.has_bias and ctx.needs_input_grad[3] and SIDE_DB:
-                    db = channel_sums(gy)  # (reads gy only: beside the input-gradient conv too)
-            fork.join(dw, db)
-        if ctx.has_bias and ctx.needs_input_grad[3] and db is None:
+            fork.join(dw)
+        if ctx.has_bias and ctx.needs_input_grad[3]:
             db = channel_sums(gy)
         return None, dx, dw, db
 
@@ -397,10 +391,8 @@ class ConvTranspose2dFn(torch.autograd.Function):
                     xp = x
                 G = wgrad(xp, dq, 2, 2)                                            # [Cin][4 Cout][2][2]
                 dw = G.view(Cin, 2, 2, Cout, 2, 2).permute(0, 3, 4, 1, 5, 2).reshape(Cin, Cout, 4, 4).contiguous()
-                if ctx.has_bias and ctx.needs_input_grad[3] and SIDE_DB:
-                    db = channel_sums(gout)
-            fork.join(dw, db)
-        if ctx.has_bias and ctx.needs_input_grad[3] and db is None:
+            fork.join(dw)
+        if ctx.has_bias and ctx.needs_input_grad[3]:
             db = channel_sums(gout)
         return None, dx, dw, db
 
