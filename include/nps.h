@@ -183,10 +183,6 @@ int nps_conv2d_x3_prologue_ok(int KH, int KW, int Cin, int gn_groups, int pre_ac
 /* 1 when the split-fp16 kernel can stage this virtual frame directly: every source boundary on a
  * multiple of 16 channels, every source's C a multiple of 4 (otherwise nps_frame_pack it first). */
 int nps_conv2d_x3_sources_ok(const nps_src_t* src, int nsrc);
-/* 1 when nps_conv2d_fwd runs this split-fp16 1x1 conv (with `a` filled in) on the persistent DMA-stream
- * kernel (Cout <= 192, sources 4-channel aligned, NHWC output with 4-aligned channels): it then also fills
- * out_stats for any epilogue. */
-int nps_conv2d_x1_dma(const nps_conv2d_t* a);
 /* Range tag `tag` (NPS_TAG_FLOATS floats) := max |x[i]| (zeroed, then raised) — the input range a
  * split-fp16 conv scales by (nps_conv2d_t.in_scale / in_tag*). */
 int nps_absmax(const float* x, long n, float* tag, void* stream);

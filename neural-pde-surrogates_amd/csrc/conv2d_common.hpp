@@ -116,16 +116,12 @@ __device__ __forceinline__ void stats_publish(const nps_conv2d_t& a, int b, doub
     }
 }
 
-#ifndef NPS_STATS_WG
-#define NPS_STATS_WG 1  // 1: one out_stats atomic pair per work-group (stats_publish_wg), 0: one per wave
-#endif
 // Work-group-collective form of stats_publish (every thread of the work-group calls it at the same point, with
 // the same b): the waves' sums meet in `red` (2 doubles per wave of LDS nobody else touches until the caller's
 // next barrier), then one thread adds them — 4-8x fewer fp64 atomics on the 16 sub-slots of a sample, whose
 // contention measured +50 us per 1x1x1 launch in the 3-D convs
 __device__ __forceinline__ void stats_publish_wg(const nps_conv2d_t& a, int b, double s1, double s2, double* red) {
     if (a.out_stats == nullptr) return;
-#if NPS_STATS_WG
     s1 = nps::wave_sum(s1);
     s2 = nps::wave_sum(s2);
     const int w = (int)(threadIdx.x >> 6), nw = (int)(blockDim.x >> 6);
@@ -144,20 +140,12 @@ __device__ __forceinline__ void stats_publish_wg(const nps_conv2d_t& a, int b, d
         atomicAdd(p, t1);
         atomicAdd(p + 1, t2);
     }
-#else
-    (void)red;
-    stats_publish(a, b, s1, s2);
-#endif
 }
 
-#ifndef NPS_TAG_WG
-#define NPS_TAG_WG 1  // 1: the 1x1 fused epilogue raises the range tag once per work-group (publish_wg), 0: per wave
-#endif
 // Work-group-collective range-tag raise + moments publish (one LDS exchange, one barrier): red holds 2 doubles and
 // 1 float per wave.  Every thread of the work-group calls it at the same point with the same b.
 __device__ __forceinline__ void publish_wg(const nps_conv2d_t& a, int b, float amax, double s1, double s2,
                                            double* red) {
-#if NPS_TAG_WG
     const bool st = a.out_stats != nullptr, tg = a.out_tag != nullptr;
     if (!st && !tg) return;
     const int w = (int)(threadIdx.x >> 6), nw = (int)(blockDim.x >> 6);
@@ -190,10 +178,6 @@ __device__ __forceinline__ void publish_wg(const nps_conv2d_t& a, int b, float a
             atomicMax(reinterpret_cast<unsigned int*>(a.out_tag + (blockIdx.x % NPS_TAG_SUB) * NPS_TAG_STRIDE),
                       __float_as_uint(m));
     }
-#else
-    nps::tag_publish(a.out_tag, amax, nps::wave_salt());
-    stats_publish_wg(a, b, s1, s2, red);
-#endif
 }
 
 // store_tile that also accumulates the stored values' moments into (s1, s2) when out_stats is set
@@ -361,22 +345,13 @@ __host__ __device__ inline bool x3_wide_tile(const nps_conv2d_t& a) { return a.T
 // floats per pixel of the LDS-staged output tile: the work-group's channels + 4 (pad)
 __host__ __device__ inline int x3_tpitch(const nps_conv2d_t& a) { return (x3_wide_tile(a) ? 192 : 64) + 4; }
 
-#ifndef NPS_X3_SPREAD
-// wide tiles of conv2d_x3_kernel: 1 = spread store (the consumers store tile t during tile t + 1's main loop),
-// 0 = the store phase after the main loop.  Round 4 A/B (profiles/r4/x3_fused_spread_ab.txt): the spread store is
-// 8-10 % slower — every weight load issued after a store waits for it (vmcnt retires in order) — so 0 ships.
-#define NPS_X3_SPREAD 0
-#endif
-
 // bytes of the split-fp16 kernel's patch ring
 __host__ __device__ inline int x3_ring_bytes(const nps_conv2d_t& a) {
     const Geo g = make_geo(a);
     return X3_NST * ((g.PH * g.PW * X3_PIXB + 15) & ~15);
 }
-// bytes of the patch ring + epilogue tile region: 64-channel tiles reuse the ring for the tile (store phase
-// after the main loop).  Wide tiles reserve ring + tile (3x3: 48 960 + 100 352 B; one work-group per CU either
-// way): the shipped store phase still writes the tile from the ring's start, the dev variants that store tile t
-// during tile t + 1 (NPS_X3_PSTORE=1 producers, NPS_X3_SPREAD consumers) keep it behind the ring.
+// bytes of the patch ring + epilogue tile region: the store phase after the main loop writes the tile from the
+// ring's start.  Wide tiles reserve ring + tile (3x3: 48 960 + 100 352 B; one work-group per CU either way).
 __host__ __device__ inline int x3_region_bytes(const nps_conv2d_t& a) {
     const int ring = x3_ring_bytes(a);
     const int tile = a.TH * a.TW * x3_tpitch(a) * 4;

@@ -92,7 +92,6 @@ _SIGS = {
     "nps_conv2d_x3_eligible": (_i, [_i, _i, _i, _i]),
     "nps_conv2d_x3_sources_ok": (_i, [ctypes.POINTER(Src), _i]),
     "nps_conv2d_x3_prologue_ok": (_i, [_i, _i, _i, _i, _i]),
-    "nps_conv2d_x1_dma": (_i, [ctypes.POINTER(Conv2dArgs)]),
     "nps_absmax": (_i, [_vp, _l, _vp, _vp]),
     "nps_conv2d_plan": (_i, [ctypes.POINTER(Conv2dArgs)]),
     "nps_conv2d_x3_weight_span": (_l, [ctypes.POINTER(Conv2dArgs)]),

@@ -26,7 +26,6 @@ FUSE_PROLOGUE = os.environ.get("NPS_FUSE_PROLOGUE", "1") == "1"
 # LDS-weight kernel's fused prologue, conv1x1_wl_kernel<6, 2, true>)
 FUSE_PROLOGUE_1X1 = os.environ.get("NPS_FUSE_PROLOGUE_1X1", "1") != "0"
 CONV_PRECISION = PREC_F32 if os.environ.get("NPS_CONV_PRECISION", "x3f16") == "f32" else PREC_X3F16
-X1_LDS_WEIGHTS = os.environ.get("NPS_X3_1X1_WL", "1")[:1] != "0"  # (libnps_hip's dev knob of the same name)
 # the Downsample's 2x2 conv reads the space-to-depth view of its input directly (nps_conv2d_t.s2d) instead of
 # a space_to_depth copy (dev knob NPS_S2D_VIEW=0: the copy)
 S2D_VIEW = os.environ.get("NPS_S2D_VIEW", "1") == "1"
@@ -637,7 +636,7 @@ def conv2d(srcs: Sequence[Src], frame_hw, wpack: torch.Tensor, bias: Optional[to
         # 1x1: the LDS-weight kernel's fused epilogue (at most one addend, no accumulate) takes the moments of the
         # stored values, activation and addend included
         plain = not accumulate and len(ads) <= 1
-        x1_ok = lib.nps_conv2d_x1_dma(ctypes_byref(a)) == 1 or (Cout <= 192 and X1_LDS_WEIGHTS and plain)
+        x1_ok = Cout <= 192 and plain
         if (a.precision == PREC_X3F16 and (KH * KW != 1 or x1_ok)
                 and not out_nchw and oC % 4 == 0 and Cout % 4 == 0):
             a.out_stats = ptr(out_stats)
@@ -741,7 +740,7 @@ FUSE_IDFT = os.environ.get("NPS_FUSE_IDFT", "1") != "0"
 
 def spectral_fusable(W: int, m2: int, Cout: int) -> bool:
     """Whether conv2d(spec=...) can take this spectral conv's W pass (nps_conv2d_t.spec_z conditions)."""
-    return (FUSE_IDFT and CONV_PRECISION == PREC_X3F16 and X1_LDS_WEIGHTS and W % 128 == 0 and m2 <= 16
+    return (FUSE_IDFT and CONV_PRECISION == PREC_X3F16 and W % 128 == 0 and m2 <= 16
             and Cout <= 192 and Cout % 4 == 0)
 
 

@@ -149,7 +149,6 @@ def test_fused_synthesis_arguments_are_checked_on_the_host():
         rc = lib.nps_conv2d_fwd(ctypes.byref(a), None)
         bad.append((tweak, rc, lib.nps_last_error().decode()))
     assert all(rc < 0 and "spec_z" in msg for _, rc, msg in bad), bad
-    assert ops.spectral_fusable(256, 10, 192) == (ops.FUSE_IDFT and ops.CONV_PRECISION == ops.PREC_X3F16 and
-                                                  ops.X1_LDS_WEIGHTS)
+    assert ops.spectral_fusable(256, 10, 192) == (ops.FUSE_IDFT and ops.CONV_PRECISION == ops.PREC_X3F16)
     assert not ops.spectral_fusable(200, 10, 192) and not ops.spectral_fusable(256, 17, 192)
     assert not ops.spectral_fusable(256, 10, 225)
