@@ -172,6 +172,18 @@ int nps_conv2d_pack_weights(const float* w, float* wpack, int Cout, int Cin, int
  * owns a contiguous 16-channel run), so the chunk count of a 1x1 packing is even. */
 int nps_conv2d_pack_weights_x3(const float* w, float* wpack, int Cout, int Cin, int KH, int KW,
                                int transposed_phase, void* stream);
+/* One weight of a batched split-fp16 packing: the arguments of nps_conv2d_pack_weights_x3. */
+typedef struct {
+    const float* w;
+    float* wpack;
+    int Cout, Cin, KH, KW;
+    int transposed_phase;
+} nps_pack_job_t;
+/* n nps_conv2d_pack_weights_x3 calls (same results, bit for bit) in two launches per 48 jobs instead of two per job:
+ * after an optimizer step every conv weight of the model is repacked (forward and input-gradient forms, trainers/
+ * base.py:493 -> the next forward / backward), ~200 packings per U-FNO training step whose launch cost, not their
+ * bytes, dominated.  jobs: a host array (copied into the launches' arguments). */
+int nps_conv2d_pack_weights_x3_batch(const nps_pack_job_t* jobs, int n, void* stream);
 /* 1 when a conv of this geometry runs on the split-fp16 kernel (stride-1: undilated 1x1 / 2x2 / 3x3, and
  * 5x5 at any dilation — the dilated ResNet's convs, proc_dilatedresnet.py:15-84). */
 int nps_conv2d_x3_eligible(int KH, int KW, int stride, int dil);
@@ -246,6 +258,41 @@ int nps_spectral_idft_h(const float* Y, float* Z, int B, int H, int m1, int m2, 
  * output's range tag, raised to cover every value written (nps_conv2d_t.out_tag) */
 int nps_spectral_idft_w(const float* Z, float* out, int B, int H, int W, int m2, int Cout, int accumulate,
                         const float* addend, int act, float* out_tag, void* stream);
+
+/* ---- one call per module: SpectralConv2d / SpectralConv3d / FNO_Layer (composites of the stages) ------
+ * The stage entry points above and below, sequenced inside the library, so a C caller runs a whole module
+ * from this header alone.  x / y / dx: fp32 NHWC ([B][H][W][C]; 3-D: NDHWC, i.e. [B][D*H][W][C]); w1..w4 /
+ * dw1..dw4: the modules' complex64 nn.Parameters in the reference layout ([Cin][Cout][m1][m2](+[m3]),
+ * interleaved re/im), packed per call into the workspace; ws: caller-owned device memory of at least the
+ * *_workspace() bytes (the same size serves forward and backward; 0 = bad shape).  No range tags or carried
+ * moments: the plain reference semantics.  Errors: as every entry point (mode bounds as proc_fno.py:134-139). */
+size_t nps_spectral_conv2d_workspace(int B, int Cin, int Cout, int H, int W, int m1, int m2);
+/* SpectralConv2d.forward (proc_fno.py:257-288): y = irfft2(P(rfft2(x))) with accumulate = 0 (act = 0);
+ * y = act(y + irfft2(...)) with accumulate = 1 (act 0 none / 1 GELU: FNO_Layer's sum + activation, :142-146). */
+int nps_spectral_conv2d_fwd(const float* x, const float* w1, const float* w2, float* y, void* ws, int B, int Cin,
+                            int Cout, int H, int W, int m1, int m2, int accumulate, int act, void* stream);
+/* Its backward under torch.fft / complex-einsum autograd: dx = dL/dx (written; NULL = skip),
+ * dw1 / dw2 = dL/dweights1, dL/dweights2 (written, PyTorch's conj(x) * g convention; both or neither). */
+int nps_spectral_conv2d_bwd(const float* x, const float* w1, const float* w2, const float* dy, float* dx, float* dw1,
+                            float* dw2, void* ws, int B, int Cin, int Cout, int H, int W, int m1, int m2,
+                            void* stream);
+/* FNO_Layer.forward (proc_fno.py:142-146, 2-D, conv_mode 'single'): w->out = act(SpectralConv2d(x) + w(x)).  `w`
+ * is the layer's 1x1 conv `w`, filled in and nps_conv2d_plan()ned by the caller (src = the layer's input frame
+ * covered by its sources, wpack, bias, out = y, act = the layer's activation, range tags), spec_z unset.  The
+ * library picks the synthesis: fused into the 1x1's epilogue (nps_conv2d_t.spec_z: split-fp16, Wout % 128 == 0,
+ * m2 <= 16, Cout <= 192, Cout % 4 == 0, no addend / accumulate), else the 1x1 then nps_spectral_idft_w
+ * accumulating with the activation.  ws: nps_fno_layer2d_workspace bytes. */
+size_t nps_fno_layer2d_workspace(int B, int Cin, int Cout, int H, int W, int m1, int m2);
+int nps_fno_layer2d_fwd(const nps_conv2d_t* w, const float* w1, const float* w2, int m1, int m2, void* ws,
+                        void* stream);
+/* SpectralConv3d (proc_fno.py:291-376): the same pair over (D, H, W) with the four corner weights. */
+size_t nps_spectral_conv3d_workspace(int B, int Cin, int Cout, int D, int H, int W, int m1, int m2, int m3);
+int nps_spectral_conv3d_fwd(const float* x, const float* w1, const float* w2, const float* w3, const float* w4,
+                            float* y, void* ws, int B, int Cin, int Cout, int D, int H, int W, int m1, int m2, int m3,
+                            int accumulate, int act, void* stream);
+int nps_spectral_conv3d_bwd(const float* x, const float* w1, const float* w2, const float* w3, const float* w4,
+                            const float* dy, float* dx, float* dw1, float* dw2, float* dw3, float* dw4, void* ws,
+                            int B, int Cin, int Cout, int D, int H, int W, int m1, int m2, int m3, void* stream);
 
 /* ---- bf16 storage (BASELINE config C5: the 3-D rFFT spectral conv in bf16) ----------------------------
  * Activations in HBM as bf16 (16-bit storage of NDHWC tensors viewed as (B, D*H, W, C)), every sum in fp32:

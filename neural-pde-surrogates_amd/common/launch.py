@@ -10,7 +10,11 @@ so the cfg's device "cuda" is this rank's card) and opens the group — "nccl" (
 is present, "gloo" otherwise.  TrainInterface.__init__ then sees the group and wires data parallelism
 (trainers/base.py).  Nothing happens in a plain single process or when a caller already opened a group.
 
-NPS_AUTO_DIST=0 turns it off; NPS_DIST_BACKEND=gloo|nccl overrides the backend choice.
+NPS_AUTO_DIST=0 turns it off; NPS_DIST_BACKEND=gloo|nccl overrides the backend choice.  An entry point that opens
+its own group under torchrun's environment (another backend, init_method or device binding) must either call
+`dist.init_process_group` BEFORE importing `data` / `models` / `trainers` (this then sees the open group and does
+nothing) or set NPS_AUTO_DIST=0 first, as bench.py does; otherwise its own init fails with "already initialized".
+The repo's gloo tests spawn workers without RANK / MASTER_ADDR (file:// rendezvous), so the hook never fires there.
 """
 import os
 

@@ -4,6 +4,7 @@
 // Input gradients of convs are NOT here: they are forward convs of dy with re-packed weights
 // (nps_conv2d_fwd), see nps_hip/autograd.py.
 #include "nps_common.hpp"
+#include <cstdlib>
 
 namespace {
 
@@ -414,8 +415,10 @@ __global__ void frame_bwd_reduce_kernel(nps_conv2d_t a, const float* __restrict_
 
 // s12[g] = (sum over the group's channels of gamma[c] * (P, Q)[b][c]) / N, the GroupNorm backward's two group
 // means, computed by the whole work-group (every thread a strided share of its group's channels, wave sums,
-// fp64 LDS adds); then __syncthreads.  (Was one thread per group walking Cin / groups channels of L2 loads while
-// the work-group's other waves waited: with GroupNorm(1), 2 x Cin dependent-issue loads before any pixel.)
+// fp64 LDS adds), written to s12 by threads < G.  It ends WITHOUT a barrier after those writes: the caller must
+// __syncthreads before any thread reads s12 (both callers do, behind their own table setup).  (Was one thread per
+// group walking Cin / groups channels of L2 loads while the work-group's other waves waited: with GroupNorm(1),
+// 2 x Cin dependent-issue loads before any pixel.)
 __device__ __forceinline__ void frame_bwd_s12(const nps_conv2d_t& a, const double* __restrict__ PQ, int b, int cpg,
                                               float (*s12)[2]) {
     __shared__ double acc[16][2];
@@ -868,7 +871,12 @@ extern "C" int nps_frame_pack_bwd_tagged(const nps_conv2d_t* ap, const float* gy
         quad = quad && (a.src[i].C & 3) == 0 && (reinterpret_cast<size_t>(a.src[i].ptr) & 15) == 0 &&
                (dsrc[i] == nullptr || (reinterpret_cast<size_t>(dsrc[i]) & 15) == 0);
     const int npix = a.Hin * a.Win;
-    const int PXB = 256;  // pixels per block of the quad kernels
+    static int fb_pxb = -1;  // TEMP dev knob NPS_FB_PXB: pixels per block of the quad kernels
+    if (fb_pxb < 0) {
+        const char* e = getenv("NPS_FB_PXB");
+        fb_pxb = (e != nullptr && atoi(e) > 0) ? atoi(e) : 256;
+    }
+    const int PXB = fb_pxb;  // pixels per block of the quad kernels
     if (a.gn_stats) {
         NPS_CHECK_ARG(a.Cin <= 4096, "frame_pack_bwd: Cin too large");
         if (hipMemsetAsync(work, 0, sizeof(double) * 2 * a.B * a.Cin, s) != hipSuccess) {

@@ -492,22 +492,9 @@ __global__ void pack_weights_kernel(const float* __restrict__ w, float* __restri
 // element j of lane = (hi | lo) of s * w[co = cb*32 + (lane&31)][ci = chunk*16 + (lane>>5)*8 + j][tap],
 // s = pow2_scale_for(max|w|): max|w| from the per-work-group partials nps_absmax_parts left in trailer[1 ..],
 // written back to trailer[0] (where the conv kernels read it)
-__global__ void pack_weights_x3_kernel(const float* __restrict__ w, _Float16* __restrict__ wp, int Cout, int Cin,
-                                       int KH, int KW, int tphase, size_t total_pairs, float* __restrict__ wmax,
-                                       int nparts) {
-    // max|w| from the absmax partials in trailer[1 .. nparts] (wave 0 reduces them, LDS broadcast); the first
-    // thread of the launch publishes it as trailer[0]
-    __shared__ float s_max;
-    if (threadIdx.x < 64) {
-        const float p = (int)threadIdx.x < nparts ? wmax[1 + threadIdx.x] : 0.f;
-        const float mw = nps::wave_max(p);
-        if (threadIdx.x == 0) s_max = mw;
-    }
-    __syncthreads();
-    const float m = s_max;
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // (hi, lo) pair index
-    if (i >= total_pairs) return;
-    if (i == 0) wmax[0] = m;
+// pair i of one weight's split-fp16 packing, given max|w| = m
+__device__ __forceinline__ void pack_x3_pair(const float* __restrict__ w, _Float16* __restrict__ wp, int Cout, int Cin,
+                                             int KH, int KW, int tphase, size_t i, float m) {
     const int ntaps = KH * KW;
     const int ncb = packed_ncb(Cout);
     const int j = i & 7;
@@ -528,6 +515,93 @@ __global__ void pack_weights_x3_kernel(const float* __restrict__ w, _Float16* __
     const h2f lv = pkrtz(v - (float)hv[0], 0.f);
     wp[o] = hv[0];
     wp[o + 512] = lv[0];
+}
+
+// max|w| from the absmax partials in trailer[1 .. nparts] (wave 0 reduces them, LDS broadcast)
+__device__ __forceinline__ float pack_x3_max(const float* __restrict__ wmax, int nparts) {
+    __shared__ float s_max;
+    if (threadIdx.x < 64) {
+        const float p = (int)threadIdx.x < nparts ? wmax[1 + threadIdx.x] : 0.f;
+        const float mw = nps::wave_max(p);
+        if (threadIdx.x == 0) s_max = mw;
+    }
+    __syncthreads();
+    return s_max;
+}
+
+__global__ void pack_weights_x3_kernel(const float* __restrict__ w, _Float16* __restrict__ wp, int Cout, int Cin,
+                                       int KH, int KW, int tphase, size_t total_pairs, float* __restrict__ wmax,
+                                       int nparts) {
+    const float m = pack_x3_max(wmax, nparts);
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // (hi, lo) pair index
+    if (i >= total_pairs) return;
+    if (i == 0) wmax[0] = m;  // the first thread of the launch publishes it as trailer[0]
+    pack_x3_pair(w, wp, Cout, Cin, KH, KW, tphase, i, m);
+}
+
+// ---- batched packing (nps_conv2d_pack_weights_x3_batch): up to PACK_BATCH weights per launch pair, the jobs passed
+// by value; work-group b belongs to the job whose block range [start[j], start[j + 1]) holds it (uniform scan)
+constexpr int PACK_BATCH = 48;
+struct PackBatch {
+    nps_pack_job_t job[PACK_BATCH];
+    int start[PACK_BATCH + 1];  // prefix sums of the jobs' work-group counts
+    int n;
+};
+__device__ __forceinline__ int batch_job(const PackBatch& pb, int blk) {
+    int j = 0;
+    while (j + 1 < pb.n && pb.start[j + 1] <= blk) ++j;
+    return j;
+}
+__host__ __device__ inline long pack_job_nw(const nps_pack_job_t& J) {  // weight elements the job reads
+    return J.transposed_phase == -1 || J.transposed_phase == -3
+               ? (long)J.Cout * J.Cin * J.KH * J.KW
+               : (J.transposed_phase == -2 ? (long)J.Cout * (J.Cin / 4) * 9 : (long)J.Cout * J.Cin * 16);
+}
+__host__ __device__ inline int pack_job_nparts(const nps_pack_job_t& J) {  // = nps_absmax_parts' partial count
+    long nb = (pack_job_nw(J) + 1024 * 16 - 1) / (1024 * 16);
+    return (int)(nb < 1 ? 1 : (nb > PACK_TRAILER - 1 ? PACK_TRAILER - 1 : nb));
+}
+// one partial max |w| per work-group of 1024 threads (absmax_parts_kernel's form), into the job's trailer[1 + k]
+__global__ __launch_bounds__(1024) void absmax_parts_batch_kernel(const PackBatch pb) {
+    const int j = batch_job(pb, blockIdx.x);
+    const nps_pack_job_t& J = pb.job[j];
+    const int k = blockIdx.x - pb.start[j], nb = pb.start[j + 1] - pb.start[j];
+    const long n = pack_job_nw(J);
+    const float* x = J.w;
+    __shared__ float wm[16];
+    float m = 0.f;
+    const long t0 = (long)k * blockDim.x + threadIdx.x, step = (long)nb * blockDim.x;
+    long tail = 0;
+    if ((reinterpret_cast<size_t>(x) & 15) == 0) {
+        const long n4 = n >> 2;
+        const float4* x4 = reinterpret_cast<const float4*>(x);
+        for (long i = t0; i < n4; i += step) {
+            const float4 v = x4[i];
+            m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+        }
+        tail = n4 << 2;
+    }
+    for (long i = tail + t0; i < n; i += step) m = fmaxf(m, fabsf(x[i]));
+    m = nps::wave_max(m);
+    if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        float v = (int)threadIdx.x < (int)(blockDim.x >> 6) ? wm[threadIdx.x] : 0.f;
+        v = nps::wave_max(v);
+        if (threadIdx.x == 0)
+            J.wpack[packed_body(J.Cout, J.Cin, J.KH * J.KW) + 1 + k] = v;
+    }
+}
+__global__ void pack_weights_x3_batch_kernel(const PackBatch pb) {
+    const int j = batch_job(pb, blockIdx.x);
+    const nps_pack_job_t& J = pb.job[j];
+    const size_t pairs = packed_body(J.Cout, J.Cin, J.KH * J.KW);
+    float* wmax = J.wpack + pairs;
+    const float m = pack_x3_max(wmax, pack_job_nparts(J));
+    const size_t i = (size_t)(blockIdx.x - pb.start[j]) * blockDim.x + threadIdx.x;
+    if (i >= pairs) return;
+    if (i == 0) wmax[0] = m;
+    pack_x3_pair(J.w, reinterpret_cast<_Float16*>(J.wpack), J.Cout, J.Cin, J.KH, J.KW, J.transposed_phase, i, m);
 }
 
 size_t packed_size(int Cout, int Cin, int ntaps) { return packed_body(Cout, Cin, ntaps) + PACK_TRAILER; }
@@ -611,6 +685,35 @@ extern "C" int nps_conv2d_pack_weights_x3(const float* w, float* wpack, int Cout
     pack_weights_x3_kernel<<<(unsigned)((pairs + bs - 1) / bs), bs, 0, (hipStream_t)stream>>>(
         w, reinterpret_cast<_Float16*>(wpack), Cout, Cin, KH, KW, transposed_phase, pairs, wmax, nparts);
     NPS_CHECK_LAUNCH("conv2d_pack_weights_x3");
+    return 0;
+}
+
+extern "C" int nps_conv2d_pack_weights_x3_batch(const nps_pack_job_t* jobs, int n, void* stream) {
+    NPS_CHECK_ARG(jobs != nullptr && n >= 0, "conv2d_pack_weights_x3_batch: bad args");
+    hipStream_t s = (hipStream_t)stream;
+    for (int c0 = 0; c0 < n; c0 += PACK_BATCH) {
+        PackBatch pa = {}, pp = {};
+        pa.n = pp.n = n - c0 < PACK_BATCH ? n - c0 : PACK_BATCH;
+        for (int k = 0; k < pa.n; ++k) {
+            const nps_pack_job_t& J = jobs[c0 + k];
+            const int tp = J.transposed_phase;
+            NPS_CHECK_ARG(J.w && J.wpack && J.Cout > 0 && J.Cin > 0 && J.KH > 0 && J.KW > 0, "conv2d_pack_weights_x3_batch: "
+                          "job %d: bad args", c0 + k);
+            NPS_CHECK_ARG(tp == -1 || tp == -3 || ((tp == -2 || (tp >= 0 && tp < 4)) && J.KH == 2 && J.KW == 2 &&
+                                                   (tp != -2 || J.Cin % 4 == 0)),
+                          "conv2d_pack_weights_x3_batch: job %d: phase / space-to-depth packing needs KH=KW=2", c0 + k);
+            pa.job[k] = pp.job[k] = J;
+            const long pairs = (long)packed_body(J.Cout, J.Cin, J.KH * J.KW);
+            pa.start[k + 1] = pa.start[k] + pack_job_nparts(J);
+            pp.start[k + 1] = pp.start[k] + (int)((pairs + 255) / 256);
+            NPS_CHECK_ARG(pp.start[k + 1] < (1 << 30), "conv2d_pack_weights_x3_batch: too large");
+        }
+        if (pa.n == 0) break;
+        absmax_parts_batch_kernel<<<(unsigned)pa.start[pa.n], 1024, 0, s>>>(pa);
+        NPS_CHECK_LAUNCH("conv2d_pack_weights_x3_batch (absmax)");
+        pack_weights_x3_batch_kernel<<<(unsigned)pp.start[pp.n], 256, 0, s>>>(pp);
+        NPS_CHECK_LAUNCH("conv2d_pack_weights_x3_batch");
+    }
     return 0;
 }
 

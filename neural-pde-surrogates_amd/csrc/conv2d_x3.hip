@@ -14,7 +14,8 @@ namespace {
 // 512 threads.  Work-group = 64 output channels x TILE_PX = 4*PB*32 output pixels (TH x TW) of one
 // sample; consumer wave w (0-3) owns 64 co x PB*32 px (2 x PB accumulators of 32x32, one per tile).
 //   * LDS holds only the input patch: a ring of NST = 3 stages of 16 channels, each pixel as
-//     [16 hi | 16 lo] fp16 + 16 B pad (80 B, conflict-free ds_read_b128).  Producer waves 4-7 fetch
+//     [16 hi | 16 lo] fp16 + 16 B pad (80 B), patch rows padded to x3_row_bytes so the B-operand
+//     ds_read_b128 are bank-conflict-free.  Producer waves 4-7 fetch
 //     stage s+4 while stage s+2 is being committed (two register sets), so each global load has two
 //     consumer stages to land; one s_barrier per stage.
 //   * The weight fragments (2 KiB per (chunk, tap, 32-co block): [hi | lo] x 64 lanes x 16 B) are read
@@ -192,7 +193,8 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
         ox0 = (tx % g.T) + (tx / g.T) * a.TW * g.T;
     };
     const int npix = g.PH * g.PW;
-    const int stage_b = (npix * X3_PIXB + 15) & ~15;
+    const int rowb = x3_row_bytes(a.TW, g.PW);  // LDS bytes per patch row (bank-conflict-free B reads)
+    const int stage_b = g.PH * rowb;
     char* ring = reinterpret_cast<char*>(smem) + 128;
     // bias table of the LDS store phase, behind the ring / tile region (x3_lds_bytes); first read after the
     // first barrier of the tile loop
@@ -223,6 +225,14 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
         // [4*gq, 4*gq + 4) of the stage, gq = ptid & 3 for every k.
         const int gq = ptid & 3;
         const float* sbase[MAXP];
+        int soff[MAXP];  // LDS byte offset of each slot inside a stage (fixed for the launch)
+#pragma unroll
+        for (int k = 0; k < MAXP; ++k) {
+            const int idx = ptid + k * 256;
+            const int p = x3_slot_px(idx);
+            const int pr = p / g.PW, pc = p - pr * g.PW;
+            soff[k] = pr * rowb + pc * X3_PIXB + (idx & 3) * 8;
+        }
         unsigned pixm = 0;  // slots whose pixel lies inside the current source
         unsigned finm = 0;  // slots whose pixel lies inside the (circularly extended) frame
         int cur_src = -1;
@@ -355,7 +365,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
                         }
                     }
                     split4(v * xs, hi, lo);
-                    char* base = Pt + x3_slot_px(idx) * X3_PIXB + (idx & 3) * 8;
+                    char* base = Pt + soff[k];
                     *reinterpret_cast<f16x4*>(base) = hi;
                     *reinterpret_cast<f16x4*>(base + 32) = lo;
                 }
@@ -413,7 +423,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
     for (int pb = 0; pb < PBW; ++pb) {
         const int P = px0 + pb * 32 + (lane & 31);
         const int ti = P / a.TW, tj = P - (P / a.TW) * a.TW;
-        boff[pb] = (ti * g.PW + tj) * X3_PIXB + (lane >> 5) * 16;
+        boff[pb] = ti * rowb + tj * X3_PIXB + (lane >> 5) * 16;
     }
     f32x16 acc[CBW][PBW];
     const int ncb = packed_ncb(a.Cout);
@@ -435,7 +445,7 @@ __global__ __launch_bounds__(512) void conv2d_x3_kernel(const nps_conv2d_t a) {
     };
     auto boffs = [&](int gg) {  // byte offset of K-group gg's patch window in the LDS ring
         const int st = gg / NTAPS, tap = gg - (gg / NTAPS) * NTAPS;
-        return (st % X3_NST) * stage_b + ((tap / KWT) * g.PW + tap % KWT) * X3_PIXB;
+        return (st % X3_NST) * stage_b + (tap / KWT) * rowb + (tap % KWT) * X3_PIXB;
     };
     auto loadB = [&](int gg, f16x8 (&d)[PBW], int half) {
         const char* p = ring + boffs(gg) + half * 32;

@@ -13,7 +13,7 @@ import os
 
 import torch
 
-__all__ = ["lib", "Src", "Conv2dArgs", "WgradArgs", "Src3", "Conv3dArgs", "check", "stream_ptr", "ptr", "LIB_PATH"]
+__all__ = ["lib", "Src", "Conv2dArgs", "WgradArgs", "Src3", "Conv3dArgs", "PackJob", "check", "stream_ptr", "ptr", "LIB_PATH"]
 
 LIB_PATH = os.environ.get("NPS_HIP_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "libnps_hip.so"))
 if not os.path.exists(LIB_PATH):
@@ -62,6 +62,11 @@ class WgradArgs(ctypes.Structure):
     ]
 
 
+class PackJob(ctypes.Structure):
+    _fields_ = [("w", ctypes.c_void_p), ("wpack", ctypes.c_void_p), ("Cout", ctypes.c_int), ("Cin", ctypes.c_int),
+                ("KH", ctypes.c_int), ("KW", ctypes.c_int), ("transposed_phase", ctypes.c_int)]
+
+
 class Src3(ctypes.Structure):
     _fields_ = [("ptr", ctypes.c_void_p), ("C", ctypes.c_int), ("D", ctypes.c_int), ("H", ctypes.c_int),
                 ("W", ctypes.c_int), ("off_d", ctypes.c_int), ("off_h", ctypes.c_int), ("off_w", ctypes.c_int)]
@@ -89,6 +94,7 @@ _SIGS = {
     "nps_conv2d_packed_size": (_sz, [_i, _i, _i]),
     "nps_conv2d_pack_weights": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp]),
     "nps_conv2d_pack_weights_x3": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp]),
+    "nps_conv2d_pack_weights_x3_batch": (_i, [ctypes.POINTER(PackJob), _i, _vp]),
     "nps_conv2d_x3_eligible": (_i, [_i, _i, _i, _i]),
     "nps_conv2d_x3_sources_ok": (_i, [ctypes.POINTER(Src), _i]),
     "nps_conv2d_x3_prologue_ok": (_i, [_i, _i, _i, _i, _i]),
@@ -144,6 +150,15 @@ _SIGS = {
                                      _i, _i, _vp]),
     "nps_plane_dot": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp]),
     "nps_volume_rescale_bwd": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp, _i, _i, _i, _i, _i, _vp]),
+    # one call per module (composites of the spectral stages)
+    "nps_spectral_conv2d_workspace": (_sz, [_i] * 7),
+    "nps_spectral_conv2d_fwd": (_i, [_vp] * 5 + [_i] * 9 + [_vp]),
+    "nps_spectral_conv2d_bwd": (_i, [_vp] * 8 + [_i] * 7 + [_vp]),
+    "nps_fno_layer2d_workspace": (_sz, [_i] * 7),
+    "nps_fno_layer2d_fwd": (_i, [ctypes.POINTER(Conv2dArgs), _vp, _vp, _i, _i, _vp, _vp]),
+    "nps_spectral_conv3d_workspace": (_sz, [_i] * 9),
+    "nps_spectral_conv3d_fwd": (_i, [_vp] * 7 + [_i] * 11 + [_vp]),
+    "nps_spectral_conv3d_bwd": (_i, [_vp] * 12 + [_i] * 9 + [_vp]),
     # bf16 storage (C5)
     "nps_spectral_dft_w_bf16": (_i, [ctypes.POINTER(Src), _i, _i, _i, _i, _i, _i, _vp, _vp]),
     "nps_spectral_mix_bf16": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _vp]),

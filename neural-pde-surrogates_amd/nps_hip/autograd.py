@@ -278,6 +278,7 @@ class Conv2dFn(torch.autograd.Function):
         else:
             raise NotImplementedError(f"conv stride {s}")
         ctx.geo, ctx.in_hw, ctx.has_bias = geo, (H, W), bias is not None
+        ctx.param = weight  # the nn.Parameter itself: its input-gradient packing is cached on it (ops.cached_pack)
         return y
 
     @staticmethod
@@ -300,12 +301,13 @@ class Conv2dFn(torch.autograd.Function):
         fork = ops.Fork(gy, on=ops.SIDE_WGRAD and ctx.needs_input_grad[1] and ctx.needs_input_grad[2])
         if ctx.needs_input_grad[1]:
             if s == 1:
+                wd = ops.cached_pack(ctx.param, ("dgrad", d), lambda p: ops.pack_conv_weight_dgrad(p, d))
                 if circ:
-                    dx = ops.conv2d([Src(gy)], (Ho, Wo), ops.pack_conv_weight_dgrad(w, d), None, Cin, KH, KW, dil=d,
+                    dx = ops.conv2d([Src(gy)], (Ho, Wo), wd, None, Cin, KH, KW, dil=d,
                                     circ=circ, out_hw=(H, W), in_scale=rng)
                 else:
                     pt = (d * (KH - 1) - lo[0], d * (KW - 1) - lo[1])
-                    dx = ops.conv2d([Src(gy)], (Ho, Wo), ops.pack_conv_weight_dgrad(w, d), None, Cin, KH, KW, dil=d,
+                    dx = ops.conv2d([Src(gy)], (Ho, Wo), wd, None, Cin, KH, KW, dil=d,
                                     pad=pt, out_hw=(H, W), in_scale=rng)
             else:
                 p = lo[0]

@@ -7,11 +7,12 @@ cat / pad / crop is ever materialised.
 """
 import math
 import os
+import weakref
 from typing import List, NamedTuple, Optional, Sequence, Union
 
 import torch
 
-from . import Conv2dArgs, Conv3dArgs, Src as _CSrc, Src3 as _CSrc3, check, lib, ptr, stream_ptr
+from . import Conv2dArgs, Conv3dArgs, PackJob, Src as _CSrc, Src3 as _CSrc3, check, lib, ptr, stream_ptr
 
 GELU = 1
 
@@ -426,21 +427,72 @@ def _pack(w, Cout, Cin, KH, KW, mode, precision):
     fn = lib.nps_conv2d_pack_weights_x3 if precision == PREC_X3F16 else lib.nps_conv2d_pack_weights
     check(fn(ptr(w), ptr(out), Cout, Cin, KH, KW, mode, stream_ptr()), "conv2d_pack_weights")
     out.nps_precision = precision   # read back by conv2d(): the kernel must match the packing
+    # how to redo it in place (_repack_stale): the source pointer and the pack arguments (split-fp16 packings only)
+    out._nps_job = (w.data_ptr(), Cout, Cin, KH, KW, mode) if precision == PREC_X3F16 else None
     return out
+
+
+# After an optimizer step every cached packing is stale (trainers/base.py:493 bumps every parameter's version):
+# the first stale lookup repacks ALL stale split-fp16 packings of the device in one batched call
+# (nps_conv2d_pack_weights_x3_batch, two launches per 48 weights) into their existing buffers, instead of two
+# launches per weight and kind (~430 per U-FNO training step, launch-bound).  Dev knob NPS_PACK_BATCH=0: off.
+PACK_BATCH = os.environ.get("NPS_PACK_BATCH", "1") != "0"
+_PACK_OWNERS = weakref.WeakValueDictionary()  # id(parameter) -> parameter holding a pack cache
+
+
+def _pack_key(w):
+    return (w.data_ptr(), w._version, str(w.device), CONV_PRECISION)
+
+
+def _replay_jobs(w, packed):
+    """The batch jobs that redo `packed` (one tensor or the convT phase list) from w in place, or None."""
+    ts = packed if isinstance(packed, list) else [packed]
+    jobs = []
+    for t in ts:
+        j = getattr(t, "_nps_job", None)
+        if j is None or j[0] != w.data_ptr():
+            return None
+        jobs.append(PackJob(w.data_ptr(), t.data_ptr(), *j[1:]))
+    return jobs
+
+
+def _repack_stale(device):
+    jobs, fresh = [], []
+    for p in list(_PACK_OWNERS.values()):
+        if p.device != device:
+            continue
+        key = _pack_key(p)
+        for kind, (k, packed) in list(getattr(p, "_nps_packs", {}).items()):
+            if k == key or k[3] != CONV_PRECISION:
+                continue
+            js = _replay_jobs(p, packed)
+            if js is not None:
+                jobs += js
+                fresh.append((p, kind, key, packed))
+    if jobs:
+        check(lib.nps_conv2d_pack_weights_x3_batch((PackJob * len(jobs))(*jobs), len(jobs), stream_ptr()),
+              "conv2d_pack_weights_x3_batch")
+    for p, kind, key, packed in fresh:
+        p._nps_packs[kind] = (key, packed)
 
 
 def cached_pack(w: torch.Tensor, kind, fn):
     """fn(w) — a packed copy of the parameter w — cached on w per `kind` until w changes (data pointer,
     w._version: the optimizer's in-place step bumps it) or the conv precision does.  The inference run()
     paths and the autograd functions share the cache, so a training step packs each weight once for the
-    no-grad pushforward unroll and the differentiable forward together."""
-    key = (w.data_ptr(), w._version, str(w.device), CONV_PRECISION)
+    no-grad pushforward unroll and the differentiable forward together; a stale entry first triggers the batched
+    repack of every stale packing on the device (_repack_stale)."""
+    key = _pack_key(w)
     cache = getattr(w, "_nps_packs", None)
     if cache is None:
         cache = w._nps_packs = {}
     ent = cache.get(kind)
+    if ent is not None and ent[0] != key and PACK_BATCH and ent[0][3] == CONV_PRECISION:
+        _repack_stale(w.device)
+        ent = cache.get(kind)
     if ent is None or ent[0] != key:
         ent = cache[kind] = (key, fn(w))
+        _PACK_OWNERS[id(w)] = w
     return ent[1]
 
 
@@ -488,6 +540,7 @@ def pack_convT_phases(w: torch.Tensor) -> List[torch.Tensor]:
         v = buf[ph * n:(ph + 1) * n]
         v.nps_precision = prec
         v.nps_phase_stride = n
+        v._nps_job = (w.data_ptr(), Cout, Cin, 2, 2, ph) if prec == PREC_X3F16 else None
         views.append(v)
     return views
 

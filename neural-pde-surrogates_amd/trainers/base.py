@@ -88,7 +88,8 @@ class TrainInterface:
         self.grad_world_scale = 1.0
         if self.world > 1:
             # data parallelism wired here, so an unchanged train.py under torchrun trains one model
-            from trainers.distributed import GradAllReducer, sync_python_random
+            from trainers.distributed import GradAllReducer, check_rank_device, sync_python_random
+            check_rank_device(self.model.parameters())  # every rank's model on its own card
             sync_python_random()  # every rank draws rank 0's unroll depths / start steps, whatever the reducer
             if grad_sync is None:
                 grad_sync = GradAllReducer(self.model.parameters())

@@ -71,6 +71,27 @@ def global_sqrt_loss(s_local: torch.Tensor, count_local: Optional[int] = None, g
     return (root + share).to(out_dtype).reshape(s_local.shape)
 
 
+def check_rank_device(params: Iterable, current_device: Optional[int] = None) -> None:
+    """Raise when a rank's model sits on a GPU other than the one this rank is bound to.
+
+    Under torchrun every rank binds its own card (`common/launch.py`: set_device(LOCAL_RANK)), but train.py takes the
+    device string from the cfg (reference src/train.py:24,32) — `--trainer.device=cuda:0` would put every rank's model
+    on card 0 and all ranks would silently share it.  Every CUDA parameter must be on `current_device` (default
+    torch.cuda.current_device()); CPU parameters (gloo runs) are not checked."""
+    cur = None
+    for p in params:
+        dev = p.device
+        if dev.type != "cuda":
+            continue
+        if cur is None:
+            cur = current_device if current_device is not None else torch.cuda.current_device()
+        idx = dev.index if dev.index is not None else cur
+        if idx != cur:
+            raise RuntimeError(f"data-parallel rank bound to cuda:{cur} holds a model parameter on {dev}: give the "
+                               f"trainer device as 'cuda' (this rank's card) instead of a fixed index, or bind the "
+                               f"rank with torch.cuda.set_device before building the model")
+
+
 def sync_python_random(group=None, src: int = 0):
     """Give every rank rank `src`'s Python `random` state (one object broadcast), so the unroll depth and
     start steps the trainer draws per step are the same on every rank and equal the 1-process draws."""

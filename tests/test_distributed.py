@@ -207,3 +207,20 @@ def test_bench_traffic_keyed_on_per_gpu_workload():
         w = dict(bench.PMC_WORKLOAD, per_gpu_batch=16 // n)
         got = bench.attach_traffic(dict(roof), w)
         assert got["traffic"] is None and "no PMC pass" in got["traffic_note"]
+
+
+def test_rank_device_guard():
+    """a rank whose model sits on another card (train.py's cfg device `cuda:0` under torchrun)
+    is refused before any collective runs; the rank's own card, an index-less 'cuda' and CPU parameters pass.
+    (torch.device objects only: no CUDA call is made.)"""
+    from trainers.distributed import check_rank_device
+
+    class P:
+        def __init__(self, dev):
+            self.device = torch.device(dev)
+
+    check_rank_device([P("cuda:3"), P("cuda:3")], current_device=3)
+    check_rank_device([P("cuda"), P("cpu")], current_device=5)
+    check_rank_device([P("cpu")])  # no CUDA parameter: nothing to check, no CUDA call
+    with pytest.raises(RuntimeError, match="cuda:0"):
+        check_rank_device([P("cuda:3"), P("cuda:0")], current_device=3)

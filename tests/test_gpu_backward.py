@@ -494,3 +494,83 @@ def test_add_at_forward_and_backward(off, src_hw, C):
     gs = torch.zeros_like(sd)
     gs[:, y0 - oy:y1 - oy, x0 - ox:x1 - ox] = gd[:, y0:y1, x0:x1]
     assert torch.allclose(src.grad.cpu().double(), gs, atol=1e-6)
+
+
+CARRY_CASES = [
+    # (kind, Cin, Cout, k, stride, padding, padding_mode, H, W) — the autograd outputs that carry their GroupNorm(1)
+    # moments from the conv epilogues (autograd._carry_buffer)
+    ("conv", 16, 64, 3, 1, 0, "zeros", 21, 19),       # valid 3x3, ragged tiles
+    ("conv", 192, 192, 3, 1, 0, "zeros", 20, 22),     # wide 192-channel tiles
+    ("conv", 12, 40, 3, 2, 0, "zeros", 31, 29),       # Downsample s2: out_hw one row / column short of the grid
+    ("conv", 12, 40, 3, 2, 1, "zeros", 16, 16),       # Downsample s2, pad 1
+    ("conv", 8, 8, 5, 1, "same", "circular", 24, 24),  # DRN 5x5 dilated circular
+    ("conv", 196, 192, 1, 1, 0, "zeros", 19, 23),     # 1x1, Cout <= 192 (LDS-weight kernel)
+    ("conv", 192, 75, 1, 1, 0, "zeros", 16, 16),      # 1x1, Cout % 4 != 0: no carried moments
+    ("convT", 64, 64, 4, 2, 0, 1, 13, 11),            # Upsample: circular pre-pad 1, 4 phase launches
+    ("convT", 40, 40, 4, 2, 1, 0, 9, 12),             # transposed conv with padding 1 (crop of every phase)
+]
+
+
+@pytest.mark.parametrize("case", CARRY_CASES)
+def test_autograd_outputs_carry_exact_moments(case):
+    """the GroupNorm(1) moments the training forward's convs carry (Conv2dFn stride 1 / 2, 1x1,
+    ConvTranspose2dFn's 4 phases with a crop offset) equal the fp64 (sum, sum of squares) of the stored output."""
+    from models.common import Conv2d, ConvTranspose2d, ConvTranspose2d_padded
+    from nps_hip import autograd as ad
+    from nps_hip import ops
+    kind, Cin, Cout, k, s, p, pm, H, W = case
+    torch.manual_seed(1)
+    if kind == "conv":
+        m = Conv2d(Cin, Cout, k, stride=s, padding=p, padding_mode=pm, dilation=2 if k == 5 else 1).to(DEV)
+    elif pm:
+        m = ConvTranspose2d_padded(pm, Cin, Cout, k, stride=s, padding=p).to(DEV)
+    else:
+        m = ConvTranspose2d(Cin, Cout, k, stride=s, padding=p).to(DEV)
+    x = (torch.randn(2, H, W, Cin, device=DEV) + 0.3).requires_grad_(True)
+    y = ad.conv2d(m, x) if kind == "conv" else ad.conv_transpose2d(m, x)
+    st = ops.stats_of(y)
+    if not (ad.CARRY_TRAIN and ops.CONV_PRECISION == ops.PREC_X3F16):
+        pytest.skip("moments not carried in training (NPS_CARRY_TRAIN=0 / exact fp32 convs)")
+    if Cout % 4 != 0:
+        assert st is None  # the planar / off-quad epilogue cannot take them: a statistics pass instead
+        return
+    assert st is not None
+    yd = y.detach().double().cpu()
+    m1 = st.detach().cpu().sum(1)
+    ref = torch.stack([yd.sum((1, 2, 3)), (yd * yd).sum((1, 2, 3))], 1)
+    assert torch.allclose(m1, ref, rtol=1e-6, atol=1e-6 * ref.abs().max().item()), (m1, ref)
+    y.sum().backward()  # the carried buffer does not disturb the backward
+    assert x.grad is not None and torch.isfinite(x.grad).all()
+
+
+def test_batched_repack_equals_individual_packs():
+    """ops._repack_stale (one nps_conv2d_pack_weights_x3_batch call after an optimizer step) writes, into the cached
+    buffers, exactly the bytes of fresh nps_conv2d_pack_weights_x3 calls: forward, input-gradient (mode -3),
+    space-to-depth (-2) and transposed-conv phase packings, over more weights than one batch launch takes (48)."""
+    from nps_hip import ops
+    if ops.CONV_PRECISION != ops.PREC_X3F16 or not ops.PACK_BATCH:
+        pytest.skip("split-fp16 batched packing off")
+    torch.manual_seed(9)
+    shapes = [(192, 196, 3, 3), (192, 388, 3, 3), (64, 36, 1, 1), (225, 192, 1, 1), (128, 132, 5, 5), (40, 12, 3, 3)]
+    ws = [torch.nn.Parameter(torch.randn(*shapes[i % len(shapes)], device=DEV) * 10 ** (i % 5 - 2)) for i in range(30)]
+    convT = torch.nn.Parameter(torch.randn(64, 48, 4, 4, device=DEV))
+    kinds = []
+    for i, w in enumerate(ws):
+        kinds.append((w, "conv", lambda p: ops.pack_conv_weight(p)))
+        if w.shape[2] != 5:
+            kinds.append((w, "dgrad", lambda p: ops.pack_conv_weight_dgrad(p)))
+        if w.shape[2] == 3:
+            kinds.append((w, "s2d", ops.pack_conv_weight_s2d))
+    kinds.append((convT, "convT", ops.pack_convT_phases))
+    for w, kind, fn in kinds:
+        ops.cached_pack(w, kind, fn)
+    assert sum(len(ops._replay_jobs(w, w._nps_packs[k][1]) or []) for w, k, _ in kinds) > 48
+    with torch.no_grad():  # the optimizer's in-place step: every version bumps
+        for w in ws + [convT]:
+            w.mul_(-1.5).add_(0.25)
+    got = [ops.cached_pack(w, kind, fn) for w, kind, fn in kinds]  # the first lookup repacks everything in a batch
+    for (w, kind, fn), g in zip(kinds, got):
+        ref = fn(w)
+        gs, rs = (g, ref) if isinstance(g, list) else ([g], [ref])
+        for a, b in zip(gs, rs):
+            assert torch.equal(a.view(torch.int32), b.view(torch.int32)), kind
