@@ -394,6 +394,11 @@ int nps_frame_pack_bwd(const nps_conv2d_t* a, const float* gy, float* const* dsr
  * cover |dsrc[i]| — the range of the gradient the next conv backward reads as its dy. */
 int nps_frame_pack_bwd_tagged(const nps_conv2d_t* a, const float* gy, float* const* dsrc, float* const* dtag,
                               float* dgamma, float* dbeta, double* work, void* stream);
+/* The same with gy_plain (or NULL): the gradient of the plain concatenation of the same sources (the frame without
+ * prologue, shaped like gy) from a second consumer — the ResidualBlock's shortcut conv or identity path
+ * (proc_unet_modern.py:243-250) — added into dsrc in the same pass instead of by a separate accumulation. */
+int nps_frame_pack_bwd2(const nps_conv2d_t* a, const float* gy, const float* gy_plain, float* const* dsrc,
+                        float* const* dtag, float* dgamma, float* dbeta, double* work, void* stream);
 
 /* element-wise pieces of the differentiated graph */
 int nps_gelu(const float* x, float* y, long n, void* stream);                                /* nn.GELU() */

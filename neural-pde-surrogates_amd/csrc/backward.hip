@@ -458,7 +458,7 @@ __device__ __forceinline__ void frame_bwd_s12(const nps_conv2d_t& a, const doubl
 
 __global__ void frame_bwd_apply_kernel(nps_conv2d_t a, const float* __restrict__ gy, const double* __restrict__ PQ,
                                        float* d0, float* d1, float* d2, float* __restrict__ dgamma,
-                                       float* __restrict__ dbeta) {
+                                       float* __restrict__ dbeta, const float* __restrict__ gy2) {
     __shared__ float2 tab[16];
     __shared__ float s12[16][2];
     const int b = blockIdx.y, si = blockIdx.z;
@@ -483,6 +483,7 @@ __global__ void frame_bwd_apply_kernel(nps_conv2d_t a, const float* __restrict__
     const int lo = si == 0 ? 0 : (si == 1 ? a.src[0].C : a.src[0].C + a.src[1].C);
     const long n = (long)S.H * S.W * S.C;
     const float* g = gy + (size_t)b * a.Hin * a.Win * a.Cin;
+    const float* g2 = gy2 != nullptr ? gy2 + (size_t)b * a.Hin * a.Win * a.Cin : nullptr;
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
         const int cs = (int)(i % S.C);
         const long pix = i / S.C;
@@ -504,6 +505,7 @@ __global__ void frame_bwd_apply_kernel(nps_conv2d_t a, const float* __restrict__
                 if (a.pre_act == 1) gz *= gelu_grad(v);
                 d = gz;
             }
+            if (g2 != nullptr) d += g2[((size_t)y * a.Win + x) * a.Cin + c];  // the plain frame's gradient
         }
         dst[(size_t)b * n + i] = d;
     }
@@ -628,7 +630,7 @@ __global__ void frame_bwd_reduce4_kernel(nps_conv2d_t a, const float* __restrict
 __global__ void frame_bwd_apply4_kernel(nps_conv2d_t a, const float* __restrict__ gy, const double* __restrict__ PQ,
                                         float* d0, float* d1, float* d2, float* __restrict__ dgamma,
                                         float* __restrict__ dbeta, int px_per_block, float* t0, float* t1,
-                                        float* t2) {
+                                        float* t2, const float* __restrict__ gy2) {
     __shared__ float2 tab[16];
     __shared__ float s12[16][2];
     const int b = blockIdx.y, si = blockIdx.z;
@@ -669,11 +671,14 @@ __global__ void frame_bwd_apply4_kernel(nps_conv2d_t a, const float* __restrict_
     const float* sp = S.ptr + (size_t)b * npix * S.C + 4 * q;
     float* dp = dst + (size_t)b * npix * S.C + 4 * q;
     const float* g = gy + (size_t)b * a.Hin * a.Win * a.Cin + c0;
+    // gy2 (or NULL): the gradient of the same frame from a second consumer of the plain concatenation (the
+    // ResidualBlock's shortcut / identity path), added here instead of by autograd's accumulation pass
+    const float* g2 = gy2 != nullptr ? gy2 + (size_t)b * a.Hin * a.Win * a.Cin + c0 : nullptr;
     int pix = p0 + lr;
     int ys = pix / S.W, xs = pix - ys * S.W;
     const int dy = per / S.W, dx = per - dy * S.W;
     for (; pix < p1; pix += FB_U * per) {
-        f32x4 v[FB_U], gz[FB_U];
+        f32x4 v[FB_U], gz[FB_U], gp[FB_U];
         bool in[FB_U];
 #pragma unroll
         for (int k = 0; k < FB_U; ++k) {  // FB_U pixels' loads first, then their math and stores
@@ -682,9 +687,11 @@ __global__ void frame_bwd_apply4_kernel(nps_conv2d_t a, const float* __restrict_
             in[k] = pk < p1 && y >= 0 && y < a.Hin && x >= 0 && x < a.Win;
             v[k] = f32x4{0.f, 0.f, 0.f, 0.f};
             gz[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+            gp[k] = f32x4{0.f, 0.f, 0.f, 0.f};
             if (in[k]) {
                 v[k] = *reinterpret_cast<const f32x4*>(sp + (size_t)pk * S.C);
                 gz[k] = *reinterpret_cast<const f32x4*>(g + ((size_t)y * a.Win + x) * a.Cin);
+                if (g2 != nullptr) gp[k] = *reinterpret_cast<const f32x4*>(g2 + ((size_t)y * a.Win + x) * a.Cin);
             }
             xs += dx;
             ys += dy;
@@ -711,6 +718,7 @@ __global__ void frame_bwd_apply4_kernel(nps_conv2d_t a, const float* __restrict_
                         if (a.pre_act == 1) gk *= gelu_grad(v[k][e]);
                         d[e] = gk;
                     }
+                    d[e] += gp[k][e];
                 }
             }
             *reinterpret_cast<f32x4*>(dp + (size_t)pk * S.C) = d;
@@ -853,6 +861,11 @@ extern "C" int nps_frame_pack_bwd(const nps_conv2d_t* ap, const float* gy, float
 extern "C" int nps_frame_pack_bwd_tagged(const nps_conv2d_t* ap, const float* gy, float* const* dsrc,
                                          float* const* dtag, float* dgamma, float* dbeta, double* work,
                                          void* stream) {
+    return nps_frame_pack_bwd2(ap, gy, nullptr, dsrc, dtag, dgamma, dbeta, work, stream);
+}
+
+extern "C" int nps_frame_pack_bwd2(const nps_conv2d_t* ap, const float* gy, const float* gy_plain, float* const* dsrc,
+                                   float* const* dtag, float* dgamma, float* dbeta, double* work, void* stream) {
     NPS_CHECK_ARG(ap && gy && dsrc, "frame_pack_bwd: null");
     const nps_conv2d_t& a = *ap;
     NPS_CHECK_ARG(a.nsrc >= 1 && a.nsrc <= NPS_MAX_SRC && a.B > 0 && a.Hin > 0 && a.Win > 0 && a.Cin > 0,
@@ -867,16 +880,17 @@ extern "C" int nps_frame_pack_bwd_tagged(const nps_conv2d_t* ap, const float* gy
     // quad kernels: every channel count a multiple of 4 (so is the GroupNorm group), 16-B aligned tensors
     bool quad = (a.Cin & 3) == 0 && a.Cin <= 1024 && (reinterpret_cast<size_t>(gy) & 15) == 0 &&
                 (!a.gn_stats || ((a.Cin / a.gn_groups) & 3) == 0);
+    quad = quad && (reinterpret_cast<size_t>(gy_plain) & 15) == 0;
     for (int i = 0; i < a.nsrc; ++i)
         quad = quad && (a.src[i].C & 3) == 0 && (reinterpret_cast<size_t>(a.src[i].ptr) & 15) == 0 &&
                (dsrc[i] == nullptr || (reinterpret_cast<size_t>(dsrc[i]) & 15) == 0);
     const int npix = a.Hin * a.Win;
-    static int fb_pxb = -1;  // TEMP dev knob NPS_FB_PXB: pixels per block of the quad kernels
-    if (fb_pxb < 0) {
-        const char* e = getenv("NPS_FB_PXB");
-        fb_pxb = (e != nullptr && atoi(e) > 0) ? atoi(e) : 256;
-    }
-    const int PXB = fb_pxb;  // pixels per block of the quad kernels
+    // pixels per block of the quad kernels: 256, halved (down to 64) while the grid has < ~4 blocks per CU — at the
+    // per-GPU batch of the 8-GPU run (B = 2) the 256-pixel blocks left the CUs 2 blocks each and the frame
+    // backward latency-bound (training B = 2: 66.0 -> 64.7 ms per step at 128 / 64 pixels, same box;
+    // profiles/r6/experiments/train_b2_knob_sweep.jsonl); B = 16 keeps 256
+    int PXB = 256;
+    while (PXB > 64 && (long)((npix + PXB - 1) / PXB) * a.B < 1000) PXB >>= 1;
     if (a.gn_stats) {
         NPS_CHECK_ARG(a.Cin <= 4096, "frame_pack_bwd: Cin too large");
         if (hipMemsetAsync(work, 0, sizeof(double) * 2 * a.B * a.Cin, s) != hipSuccess) {
@@ -902,12 +916,12 @@ extern "C" int nps_frame_pack_bwd_tagged(const nps_conv2d_t* ap, const float* gy
     for (int i = 0; dtag != nullptr && i < a.nsrc; ++i) t[i] = d[i] != nullptr ? dtag[i] : nullptr;
     if (quad) {
         frame_bwd_apply4_kernel<<<dim3((unsigned)((pmax + PXB - 1) / PXB), a.B, a.nsrc), 256, 0, s>>>(
-            a, gy, work, d[0], d[1], d[2], dgamma, dbeta, PXB, t[0], t[1], t[2]);
+            a, gy, work, d[0], d[1], d[2], dgamma, dbeta, PXB, t[0], t[1], t[2], gy_plain);
         NPS_CHECK_LAUNCH("frame_pack_bwd apply");
         return 0;
     }
     frame_bwd_apply_kernel<<<dim3(grid_for(nmax, 256 * 8, 2048), a.B, a.nsrc), 256, 0, s>>>(a, gy, work, d[0], d[1],
-                                                                                           d[2], dgamma, dbeta);
+                                                                                           d[2], dgamma, dbeta, gy_plain);
     NPS_CHECK_LAUNCH("frame_pack_bwd apply");
     for (int i = 0; i < a.nsrc; ++i)  // (the element-wise kernel publishes no tags: one absmax pass per source)
         if (t[i] != nullptr && nps_absmax(d[i], (long)a.B * a.src[i].H * a.src[i].W * a.src[i].C, t[i], stream) != 0)

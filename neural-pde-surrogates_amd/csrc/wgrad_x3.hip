@@ -687,15 +687,13 @@ __global__ void wgrad_fold_kernel(const float* __restrict__ w, float* __restrict
     }
 }
 
-// TEMP dev knobs: work-groups of the split-K grid (NPS_WX_WGS, default 512) and min tiles per split (NPS_WX_MINT, 8)
-const long g_wx_wgs = [] {
-    const char* e = std::getenv("NPS_WX_WGS");
-    return (e != nullptr && atol(e) > 0) ? atol(e) : 512L;
-}();
-const long g_wx_mint = [] {
-    const char* e = std::getenv("NPS_WX_MINT");
-    return (e != nullptr && atol(e) > 0) ? atol(e) : 8L;
-}();
+// Work-groups of the split-K grid: 2 per CU in turn (the first one's atomics overlap the second one's tiles), but 1
+// per CU for small pixel counts (the per-GPU batch of the 8-GPU run, B = 2 at <= 260^2): there each work-group's
+// split was only 26-90 tiles, and the per-split fixed costs (prologue, 36 K partial atomics) halved with half the
+// splits — x3w_1tap 4.57 -> 3.61 ms, x3w_9tap 12.16 -> 11.43 ms per training step at B = 2 (same box;
+// profiles/r6/experiments/train_b2_knob_sweep.jsonl; 1024 and a larger minimum split were slower)
+inline long wx_wgs(const nps_wgrad_t& p) { return (long)p.B * p.Ha * p.Wa <= 200000 ? 256 : 512; }
+constexpr long WX_MINT = 8;  // minimum pixel tiles per split
 // dev knob NPS_WX_REMAP=0: the plain (tile-fastest) work-group order
 const int g_wx_remap = [] {
     const char* e = std::getenv("NPS_WX_REMAP");
@@ -712,8 +710,8 @@ int launch_wgrad_x3(const nps_wgrad_t& p, const float* ar, const float* xr, floa
     const long base = (long)n_mt * n_nt;
     // split K (pixel tiles): at most 2 work-groups in turn per CU (the first one's atomics overlap the
     // second one's tiles; a grid just past a multiple of 256 would add a nearly empty round), >= 8 tiles each
-    long splits = g_wx_wgs / base;
-    const long max_splits = (ntiles + g_wx_mint - 1) / g_wx_mint;
+    long splits = wx_wgs(p) / base;
+    const long max_splits = (ntiles + WX_MINT - 1) / WX_MINT;
     if (splits > max_splits) splits = max_splits;
     if (splits >= 16) splits &= ~7L;  // a multiple of 8: the XCD-aware tile order (kernel comment)
     if (splits < 1) splits = 1;
@@ -752,8 +750,8 @@ int launch_wgrad1_wide(const nps_wgrad_t& p, const float* ar, const float* xr, f
     NPS_CHECK_ARG(ntiles < (1L << 30), "conv2d_wgrad_x3 (1x1): too many tiles");
     const int n_mt = (p.M + W1_ROWS - 1) / W1_ROWS, n_nt = (p.N + W1_ROWS - 1) / W1_ROWS;
     const long base = (long)n_mt * n_nt;
-    long splits = g_wx_wgs / base;  // two work-groups per CU in turn (LDS: 120 KiB each, one resident)
-    const long max_splits = (ntiles + g_wx_mint - 1) / g_wx_mint;
+    long splits = wx_wgs(p) / base;  // two work-groups per CU in turn (LDS: 120 KiB each, one resident)
+    const long max_splits = (ntiles + WX_MINT - 1) / WX_MINT;
     if (splits > max_splits) splits = max_splits;
     if (splits >= 16) splits &= ~7L;
     if (splits < 1) splits = 1;
@@ -790,8 +788,8 @@ int launch_wgrad2_wide(const nps_wgrad_t& p, const float* ar, const float* xr, f
     NPS_CHECK_ARG(ntiles < (1L << 30), "conv2d_wgrad_x3 (2x2): too many tiles");
     const int n_mt = (p.M + W2_ROWS - 1) / W2_ROWS, n_nt = (p.N + W2_ROWS - 1) / W2_ROWS;
     const long base = (long)n_mt * n_nt;
-    long splits = g_wx_wgs / base;
-    const long max_splits = (ntiles + g_wx_mint - 1) / g_wx_mint;
+    long splits = wx_wgs(p) / base;
+    const long max_splits = (ntiles + WX_MINT - 1) / WX_MINT;
     if (splits > max_splits) splits = max_splits;
     if (splits >= 16) splits &= ~7L;
     if (splits < 1) splits = 1;

@@ -383,13 +383,17 @@ class ResidualBlock(nn.Module):
         H, W = frame_hw
         n1 = self.norm1 if isinstance(self.norm1, nn.GroupNorm) else None
         n2 = self.norm2 if isinstance(self.norm2, nn.GroupNorm) else None
-        h1 = ad.conv2d(self.conv1, ad.frame(srcs, (H, W), n1, act))
         if isinstance(self.shortcut, nn.Identity):
             if len(srcs) != 1 or srcs[0].off_y or srcs[0].off_x or tuple(srcs[0].t.shape[1:3]) != (H, W):
                 raise RuntimeError("identity shortcut on a concatenated input")
-            sc = srcs[0].t
+        # conv1's frame and the shortcut's input (x itself for the identity) from one node: the backward adds the
+        # shortcut path's gradient inside the frame backward (ad.frame_pair), not as a separate accumulation
+        f1, xin = ad.frame_pair(srcs, (H, W), n1, act) if ad.FRAME_PAIR else (ad.frame(srcs, (H, W), n1, act), None)
+        h1 = ad.conv2d(self.conv1, f1)
+        if isinstance(self.shortcut, nn.Identity):
+            sc = xin if xin is not None else srcs[0].t
         else:
-            sc = ad.conv2d(self.shortcut, ad.frame(srcs, (H, W)))
+            sc = ad.conv2d(self.shortcut, xin if xin is not None else ad.frame(srcs, (H, W)))
         h2 = ad.conv2d(self.conv2, ad.frame([ops.Src(h1)], h1.shape[1:3], n2, act))
         return ad.add_at(sc, h2, crop_offsets(h2.shape[1:3], sc.shape[1:3]))
 

@@ -132,6 +132,8 @@ _SIGS = {
     "nps_frame_pack_bwd": (_i, [ctypes.POINTER(Conv2dArgs), _vp, ctypes.POINTER(ctypes.c_void_p), _vp, _vp, _vp, _vp]),
     "nps_frame_pack_bwd_tagged": (_i, [ctypes.POINTER(Conv2dArgs), _vp, ctypes.POINTER(ctypes.c_void_p),
                                        ctypes.POINTER(ctypes.c_void_p), _vp, _vp, _vp, _vp]),
+    "nps_frame_pack_bwd2": (_i, [ctypes.POINTER(Conv2dArgs), _vp, _vp, ctypes.POINTER(ctypes.c_void_p),
+                                 ctypes.POINTER(ctypes.c_void_p), _vp, _vp, _vp, _vp]),
     "nps_gelu": (_i, [_vp, _vp, _l, _vp]),
     "nps_gelu_bwd": (_i, [_vp, _vp, _vp, _l, _vp]),
     "nps_add_at": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp]),

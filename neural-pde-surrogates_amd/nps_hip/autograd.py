@@ -170,42 +170,102 @@ class FrameFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gout):
-        offsets, frame_hw, groups, eps, act = ctx.meta
-        saved = ctx.saved_tensors
-        if ctx.has_gn:
-            gamma, beta, stats = saved[:3]
-            srcs = saved[3:]
-        else:
-            gamma = beta = stats = None
-            srcs = saved
-        gout = _c(gout)
-        B = srcs[0].shape[0]
-        Cin = sum(t.shape[3] for t in srcs)
-        a = Conv2dArgs()
-        a.nsrc = len(srcs)
-        a.src = ops._c_src([Src(t, *o) for t, o in zip(srcs, offsets)])
-        a.B, a.Hin, a.Win, a.Cin = B, frame_hw[0], frame_hw[1], Cin
-        dgamma = dbeta = work = None
-        if ctx.has_gn:
-            a.gn_stats, a.gn_gamma, a.gn_beta = ptr(stats), ptr(gamma), ptr(beta)
-            a.gn_groups, a.gn_eps = groups, eps
-            dgamma = torch.empty_like(gamma)
-            dbeta = torch.empty_like(beta)
-            work = torch.empty((B, 2, Cin), dtype=torch.float64, device=gout.device)
-        a.pre_act = act
-        need = ctx.needs_input_grad[3:]
-        dsrc = [torch.empty_like(t) if need[i] else None for i, t in enumerate(srcs)]
-        arr = (ctypes.c_void_p * 3)(*[(d.data_ptr() if d is not None else None) for d in dsrc] +
-                                   [None] * (3 - len(dsrc)))
-        # each source gradient leaves with a range tag: the conv backward reading it as dy needs no absmax pass
-        tags = [None] * 3
-        if ops.USE_OUT_TAGS:
-            ops.reserve_tags(gout.device, len(dsrc))
-            tags[:len(dsrc)] = [ops.new_tag(d) if d is not None else None for d in dsrc]
-        tarr = (ctypes.c_void_p * 3)(*tags)
-        check(lib.nps_frame_pack_bwd_tagged(ctypes.byref(a), ptr(gout), arr, tarr, ptr(dgamma), ptr(dbeta),
-                                            ptr(work), stream_ptr()), "frame_pack_bwd")
-        return (None, dgamma, dbeta, *dsrc)
+        return _frame_bwd(ctx, gout, None)
+
+
+# ResidualBlock's two uses of its input in one autograd node (frame_pair; dev knob NPS_FRAME_PAIR=0: two FrameFns)
+FRAME_PAIR = os.environ.get("NPS_FRAME_PAIR", "1") != "0"
+
+
+def _frame_bwd(ctx, gout, gplain):
+    """FrameFn / FramePairFn backward: the sources' gradients (and GroupNorm affine's) in one frame-backward pass,
+    gplain (the plain concatenation's gradient, or None) added inside it (nps_frame_pack_bwd2)."""
+    offsets, frame_hw, groups, eps, act = ctx.meta
+    saved = ctx.saved_tensors
+    if ctx.has_gn:
+        gamma, beta, stats = saved[:3]
+        srcs = saved[3:]
+    else:
+        gamma = beta = stats = None
+        srcs = saved
+    gout = _c(gout)
+    B = srcs[0].shape[0]
+    Cin = sum(t.shape[3] for t in srcs)
+    a = Conv2dArgs()
+    a.nsrc = len(srcs)
+    a.src = ops._c_src([Src(t, *o) for t, o in zip(srcs, offsets)])
+    a.B, a.Hin, a.Win, a.Cin = B, frame_hw[0], frame_hw[1], Cin
+    dgamma = dbeta = work = None
+    if ctx.has_gn:
+        a.gn_stats, a.gn_gamma, a.gn_beta = ptr(stats), ptr(gamma), ptr(beta)
+        a.gn_groups, a.gn_eps = groups, eps
+        dgamma = torch.empty_like(gamma)
+        dbeta = torch.empty_like(beta)
+        work = torch.empty((B, 2, Cin), dtype=torch.float64, device=gout.device)
+    a.pre_act = act
+    need = ctx.needs_input_grad[3:]
+    dsrc = [torch.empty_like(t) if need[i] else None for i, t in enumerate(srcs)]
+    arr = (ctypes.c_void_p * 3)(*[(d.data_ptr() if d is not None else None) for d in dsrc] +
+                               [None] * (3 - len(dsrc)))
+    # each source gradient leaves with a range tag: the conv backward reading it as dy needs no absmax pass
+    tags = [None] * 3
+    if ops.USE_OUT_TAGS:
+        ops.reserve_tags(gout.device, len(dsrc))
+        tags[:len(dsrc)] = [ops.new_tag(d) if d is not None else None for d in dsrc]
+    tarr = (ctypes.c_void_p * 3)(*tags)
+    gp = _c(gplain) if gplain is not None else None
+    check(lib.nps_frame_pack_bwd2(ctypes.byref(a), ptr(gout), ptr(gp), arr, tarr, ptr(dgamma), ptr(dbeta),
+                                  ptr(work), stream_ptr()), "frame_pack_bwd")
+    return (None, dgamma, dbeta, *dsrc)
+
+
+class FramePairFn(torch.autograd.Function):
+    """(act(GroupNorm(cat(crop_Nd(src_i)))), cat(crop_Nd(src_i))) — a ResidualBlock's conv1 input and its shortcut's
+    (or identity path's) input, proc_unet_modern.py:243-250 — from one node, so the backward adds the second
+    output's gradient inside the frame backward (nps_frame_pack_bwd2) instead of autograd accumulating two
+    gradients per source with a separate pass.  A single source covering the frame is returned as the plain
+    output itself (a view: no copy)."""
+
+    @staticmethod
+    def forward(ctx, meta, gamma, beta, *srcs):
+        offsets, frame_hw, groups, eps, act = meta
+        ss = [Src(_c(t), *o) for t, o in zip(srcs, offsets)]
+        gn = None
+        if gamma is not None:
+            stats = ops.group_norm_stats(ss, frame_hw, groups)
+            gn = ops.GN(stats, gamma.detach(), beta.detach(), groups, eps)
+        out = ops.frame_pack(ss, frame_hw, gn, act)
+        ident = len(ss) == 1 and tuple(offsets[0]) == (0, 0) and tuple(srcs[0].shape[1:3]) == tuple(frame_hw)
+        plain = srcs[0] if ident else ops.frame_pack(ss, frame_hw, None, 0)
+        ctx.meta = meta
+        ctx.has_gn = gamma is not None
+        ctx.ident = ident
+        ctx.save_for_backward(*([gamma, beta, gn.stats] if gn is not None else []), *[s.t for s in ss])
+        return out, plain
+
+    @staticmethod
+    def backward(ctx, gout, gplain):
+        if gout is None:  # (only the plain output was used)
+            gout = torch.zeros((ctx.saved_tensors[-1].shape[0], *ctx.meta[1],
+                                sum(t.shape[3] for t in ctx.saved_tensors[(3 if ctx.has_gn else 0):])),
+                               dtype=torch.float32, device=gplain.device)
+        return _frame_bwd(ctx, gout, gplain)
+
+
+def frame_pair(srcs: Sequence[Src], frame_hw, norm=None, act=0):
+    """(frame(srcs, norm, act), frame(srcs)) through FramePairFn: one frame backward for both consumers."""
+    frame_hw = (int(frame_hw[0]), int(frame_hw[1]))
+    meta = (tuple((int(s.off_y), int(s.off_x)) for s in srcs), frame_hw,
+            norm.num_groups if norm is not None else 0, float(norm.eps) if norm is not None else 0.0, act)
+    gamma = norm.weight if norm is not None else None
+    beta = norm.bias if norm is not None else None
+    f, p = FramePairFn.apply(meta, gamma, beta, *[s.t for s in srcs])
+    t0 = srcs[0].t
+    if p._base is t0:  # the identity view carries the source's live range tag and moments (same version counter)
+        for attr in ("_nps_tag", "_nps_stats"):
+            if getattr(t0, attr, None) is not None:
+                setattr(p, attr, getattr(t0, attr))
+    return f, p
 
 
 def frame(srcs: Sequence[Src], frame_hw, norm=None, act=0) -> torch.Tensor:

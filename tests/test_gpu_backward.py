@@ -573,4 +573,5 @@ def test_batched_repack_equals_individual_packs():
         ref = fn(w)
         gs, rs = (g, ref) if isinstance(g, list) else ([g], [ref])
         for a, b in zip(gs, rs):
-            assert torch.equal(a.view(torch.int32), b.view(torch.int32)), kind
+            n = a.numel() - 64 + 1  # the fragment body and trailer[0] = max|w| (the rest: absmax partials / unused)
+            assert torch.equal(a[:n].view(torch.int32), b[:n].view(torch.int32)), kind
