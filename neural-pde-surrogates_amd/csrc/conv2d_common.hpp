@@ -324,9 +324,13 @@ constexpr int X3_PIXB = 80;   // LDS bytes per patch pixel of the split-fp16 ker
 // 16x8 tile collide 3-way (8-wide rows) and of an 8x16 tile 2-way (SQ_LDS_BANK_CONFLICT: 61-63 % of LDS-active
 // cycles).  Row bytes = 128 mod 256 (8-pixel tile rows) or 0 mod 256 (16-pixel rows) make every
 // group's 16 slots distinct; rows of 32+ pixels are conflict-free at any pitch.
+// A/B build flag: -DNPS_X3_ROW_PAD=0 (tools/build_variant.sh) keeps the unpadded 80-B-pixel rows.
+#ifndef NPS_X3_ROW_PAD
+#define NPS_X3_ROW_PAD 1
+#endif
 __host__ __device__ inline int x3_row_bytes(int TW, int PW) {
     int rb = PW * X3_PIXB;
-    if (TW > 16) return rb;
+    if (!NPS_X3_ROW_PAD || TW > 16) return rb;
     const int want = TW == 8 ? 128 : 0;
     while ((rb & 255) != want) rb += 16;
     return rb;
