@@ -753,6 +753,258 @@ __global__ __launch_bounds__(256) void frame_pack3d_kernel(const nps_conv3d_t a,
     }
 }
 
+// 1x1x1 Conv3d on bf16 storage (K = 1, stride 1, no frame extension): the ResidualBlock shortcut over
+// cat(h, crop_Nd(skip), crop_Nd(vb)) and the U-Net's final GroupNorm + GELU + 1x1 (proc_unet_modern.py:84, :265,
+// :429).  A pointwise GEMM has no patch to share between output positions, and conv3d_kernel's 16-channel stages
+// (one barrier, one dependent global load and 4 MFMAs each) left it latency-bound near 2 TB/s.  Here the packed
+// weight of all Cout (NCB 32-channel blocks) and the bias stay in LDS for the whole launch; each wave takes 32
+// voxels of its sample at a time, issues the loads of ALL its Cin channels (one 8-channel piece per 16-channel
+// K-step and lane, at most NCH K-steps) for the NEXT tile before it runs the K-steps and the epilogue of this one
+// (two tiles in flight per wave, no barrier).  Operand rounding, K order, prologue and epilogue are conv3d_kernel's,
+// so the results are bit-identical; only the moments' fp32 partial sums group differently.
+// (Measured alternative, not kept: the tile staged through LDS with voxel-major coalesced quad loads and 16-B
+// stores — 2x slower, its per-quad addressing cost more than the fragment-shaped accesses it replaced.)
+// Grid: work-groups per sample x B, one round of resident work-groups.
+template <int NCB, int NCH, bool PRO>
+__global__ __launch_bounds__(256) void conv3d_1x1_kernel(const nps_conv3d_t a, int nchunk) {
+    constexpr int NCO = NCB * 32;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    bf16_t* Wl = reinterpret_cast<bf16_t*>(smem);  // [nchunk][NCO][16], 8-channel halves swizzled by row bit 3
+    float* bsh = reinterpret_cast<float*>(smem + (size_t)nchunk * NCO * 32);  // [NCO] bias, zero past Cout
+    float* gscale = bsh + NCO;
+    float* gshift = gscale + nchunk * 16;
+    double* red = reinterpret_cast<double*>(gshift + nchunk * 16);  // [4 waves][2]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int b = blockIdx.y;
+    // packed rows [tile][kd = 0][chunk][tap = 0][64][16]: NCO = 64 x the packing's Cout tiles (host-checked)
+    const bf16_t* wg = reinterpret_cast<const bf16_t*>(a.wpack);
+    for (int i = tid; i < nchunk * NCO * 2; i += 256) {
+        const int half = i & 1, row = i >> 1;  // row = chunk * NCO + co
+        const int chunk = row / NCO, co = row - chunk * NCO;
+        const u32x4 v = *reinterpret_cast<const u32x4*>(wg + ((size_t)((co >> 6) * nchunk + chunk) * 64 + (co & 63)) * 16 +
+                                                        half * 8);
+        *reinterpret_cast<u32x4*>(Wl + row * 16 + ((half ^ swz(co)) * 8)) = v;
+    }
+    if (tid < NCO) bsh[tid] = (a.bias != nullptr && tid < a.Cout) ? a.bias[tid] : 0.f;
+    if constexpr (PRO) {  // as conv3d_kernel
+        for (int c = tid; c < nchunk * 16; c += 256) {
+            float sc = 1.f, sh = 0.f;
+            if (a.gn_stats != nullptr && c < a.Cin) {
+                const int g = c / (a.Cin / a.gn_groups);
+                const double n = (double)a.Dc * a.Hc * a.Wc * (a.Cin / a.gn_groups);
+                const double mean = a.gn_stats[(b * a.gn_groups + g) * 2] / n;
+                const double var = fmax(a.gn_stats[(b * a.gn_groups + g) * 2 + 1] / n - mean * mean, 0.0);
+                const float rstd = (float)(1.0 / sqrt(var + (double)a.gn_eps));
+                sc = a.gn_gamma[c] * rstd;
+                sh = a.gn_beta[c] - (float)mean * sc;
+            }
+            gscale[c] = sc;
+            gshift[c] = sh;
+        }
+    }
+    __syncthreads();
+
+    const int col = lane & 31, hl = lane >> 5;
+    const int nvox = a.Dc * a.Hc * a.Wc;  // = Dout x Hout x Wout (K = 1, no extension)
+    const int ntv = (nvox + 31) / 32;
+    bf16_t* out = reinterpret_cast<bf16_t*>(a.out);
+    const bf16_t* add = reinterpret_cast<const bf16_t*>(a.addend);
+    const bool st = a.out_stats != nullptr;
+    // sources: first channels lo1 / lo2 of sources 1 / 2 (Cin past the last one), every source C % 4 == 0 and all
+    // but the last C % 8 == 0 (host-checked), so a lane's 8-channel piece lies in one source: one 16-B load, or
+    // one 8-B half at the last source's end
+    const int ns = a.nsrc;
+    const int lo1 = ns > 1 ? a.src[0].C : a.Cin, lo2 = ns > 2 ? a.src[0].C + a.src[1].C : a.Cin;
+    auto coords = [&](int t, int& cd, int& ch, int& cw) {
+        const int v = t * 32 + col;
+        cw = v % a.Wc;
+        const int r = v / a.Wc;
+        ch = r % a.Hc;
+        cd = r / a.Hc;
+        return v < nvox;
+    };
+    // the NCH pieces of tile t, all loads in flight at once
+    auto fetch = [&](int t, Vec8<bf16_t> (&x)[NCH]) {
+        int cd, ch, cw;
+        const bool vin = coords(t, cd, ch, cw);
+        const bf16_t* sp[NPS_MAX_SRC];  // this voxel's channel 0 in each source, or null where it does not cover
+#pragma unroll
+        for (int si = 0; si < NPS_MAX_SRC; ++si) {
+            const nps_src3_t& s = a.src[si];
+            const int dd = cd - s.off_d, hh = ch - s.off_h, ww = cw - s.off_w;
+            const bool ok = vin && si < ns && dd >= 0 && dd < s.D && hh >= 0 && hh < s.H && ww >= 0 && ww < s.W;
+            sp[si] = ok ? reinterpret_cast<const bf16_t*>(s.ptr) + ((((size_t)b * s.D + dd) * s.H + hh) * s.W + ww) * s.C
+                        : nullptr;
+        }
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            x[c].zero();
+            const int c0 = c * 16 + hl * 8;
+            if (c >= nchunk || c0 >= a.Cin) continue;
+            const int si = c0 < lo1 ? 0 : (c0 < lo2 ? 1 : 2);
+            const int cl = c0 - (si == 0 ? 0 : (si == 1 ? lo1 : lo2));
+            const int sC = si == 0 ? lo1 : (si == 1 ? lo2 - lo1 : a.Cin - lo2);
+            const bf16_t* p = si == 0 ? sp[0] : (si == 1 ? sp[1] : sp[2]);
+            if (p == nullptr) continue;
+            if (cl + 8 <= sC) x[c].load(p + cl);
+            else x[c].load_half(0, p + cl);
+        }
+    };
+    float f1 = 0.f, f2 = 0.f;  // this lane's stored values (changes, under accumulate): conv3d_kernel's momd
+    const int tstride = gridDim.x * 4;
+    int t = blockIdx.x * 4 + wave;
+    Vec8<bf16_t> x[NCH];
+    if (t < ntv) fetch(t, x);
+    for (; t < ntv; t += tstride) {
+        // next tile's loads first (two tiles in flight per wave)
+        Vec8<bf16_t> xn[NCH];
+        if (t + tstride < ntv) fetch(t + tstride, xn);
+        int cd, ch, cw;
+        const bool vin = coords(t, cd, ch, cw);
+        f32x16 acc[NCB];
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) acc[cb][q] = 0.f;
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            if (c >= nchunk) break;
+            if constexpr (PRO) {  // frame values, crop zeros included, are normalised (as conv3d_kernel's commit)
+                const int c0 = c * 16 + hl * 8;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    float y = fmaf(x[c].get(e), gscale[c0 + e], gshift[c0 + e]);
+                    if (a.pre_act == 1) y = nps::gelu_fast(y);
+                    x[c].set(e, c0 + e < a.Cin ? y : 0.f);
+                }
+            }
+            const bf16x8 B = __builtin_bit_cast(bf16x8, x[c].a);
+#pragma unroll
+            for (int cb = 0; cb < NCB; ++cb) {
+                const int co = cb * 32 + col;
+                const bf16x8 A = *reinterpret_cast<const bf16x8*>(Wl + (c * NCO + co) * 16 + ((hl ^ swz(co)) * 8));
+                acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, B, acc[cb], 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) x[c] = xn[c];
+        // epilogue (conv3d_kernel's bf16 vec4 path): lane holds voxel `col`, channels cb*32 + 8j + 4hl + (0..3)
+        const int od = cd * a.out_os + a.out_off_d, oh = ch * a.out_os + a.out_off_h, ow = cw * a.out_os + a.out_off_w;
+        if (!vin || od < 0 || od >= a.out_D || oh < 0 || oh >= a.out_H || ow < 0 || ow >= a.out_W) continue;
+        const size_t vox = (((size_t)b * a.out_D + od) * a.out_H + oh) * a.out_W + ow;
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int co0 = cb * 32 + 8 * j + 4 * hl;
+                if (co0 >= a.Cout) continue;
+                const f32x4 bv = *reinterpret_cast<const f32x4*>(bsh + co0);
+                float o[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) o[e] = acc[cb][4 * j + e] + bv[e];
+                bf16_t* op = out + vox * a.out_C + co0;
+                if (add != nullptr) {
+                    const u32x2 w = *reinterpret_cast<const u32x2*>(add + vox * a.out_C + co0);
+                    o[0] += bf2f(w[0] & 0xffffu); o[1] += bf2f(w[0] >> 16);
+                    o[2] += bf2f(w[1] & 0xffffu); o[3] += bf2f(w[1] >> 16);
+                }
+                if (a.act == 1)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) o[e] = nps::gelu_erf(o[e]);
+                float old[4] = {0.f, 0.f, 0.f, 0.f};
+                if (a.accumulate) {
+                    const u32x2 w = *reinterpret_cast<const u32x2*>(op);
+                    old[0] = bf2f(w[0] & 0xffffu); old[1] = bf2f(w[0] >> 16);
+                    old[2] = bf2f(w[1] & 0xffffu); old[3] = bf2f(w[1] >> 16);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) o[e] += old[e];
+                }
+                const u32x2 rr = {f2bf(o[0]) | (f2bf(o[1]) << 16), f2bf(o[2]) | (f2bf(o[3]) << 16)};
+                *reinterpret_cast<u32x2*>(op) = rr;
+                if (st) {  // (as stored)
+                    const float s4[4] = {bf2f(rr[0] & 0xffffu), bf2f(rr[0] >> 16), bf2f(rr[1] & 0xffffu),
+                                         bf2f(rr[1] >> 16)};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        f1 += s4[e] - old[e];
+                        f2 += (s4[e] - old[e]) * (s4[e] + old[e]);
+                    }
+                }
+            }
+        }
+    }
+    if (st) {  // (uniform) one atomic pair per work-group, as conv3d_kernel
+        const double s1 = nps::wave_sum((double)f1);
+        const double s2 = nps::wave_sum((double)f2);
+        if (lane == 0) {
+            red[2 * wave] = s1;
+            red[2 * wave + 1] = s2;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double* q = a.out_stats + ((size_t)b * NPS_STATS_SUB + blockIdx.x % NPS_STATS_SUB) * 2;
+            atomicAdd(q, (red[0] + red[2]) + (red[4] + red[6]));
+            atomicAdd(q + 1, (red[1] + red[3]) + (red[5] + red[7]));
+        }
+    }
+}
+
+// dev knob NPS_C3D_1X1=0: 1x1x1 bf16 convs on conv3d_kernel (A/B)
+bool c3d_1x1_on() {
+    static const int g = [] {
+        const char* e = std::getenv("NPS_C3D_1X1");
+        return (e != nullptr && e[0] == '0') ? 0 : 1;
+    }();
+    return g != 0;
+}
+
+bool c3d_1x1_eligible(const nps_conv3d_t& a) {
+    if (!a.bf16 || a.K != 1 || a.stride != 1 || a.transposed || a.circ != 0 || a.zpad != 0) return false;
+    if (a.Cout > 128 || a.Cin > 256 || (a.Cout & 3) != 0 || (a.out_C & 3) != 0) return false;
+    for (int i = 0; i < a.nsrc; ++i)
+        if ((a.src[i].C & 3) != 0 || (i < a.nsrc - 1 && (a.src[i].C & 7) != 0)) return false;
+    // (three-source frames, the up-path cat(h, skip, vb): measured slower than conv3d_kernel, 437 vs 360 us at
+    // 132 -> 64 over 16 x 128^2, B = 8 — the per-piece source selection; two sources and GN-prologue frames gain)
+    if (a.nsrc > 2) return false;
+    return c3d_1x1_on();
+}
+
+template <int NCB, int NCH, bool PRO>
+int launch_1x1(const nps_conv3d_t& a, int nchunk, hipStream_t s) {
+    const size_t lds = (size_t)nchunk * NCB * 32 * 32 + NCB * 32 * sizeof(float) + 2 * (size_t)nchunk * 16 * sizeof(float) +
+                       8 * sizeof(double);
+    NPS_CHECK_ARG(lds <= 160 * 1024, "conv3d (1x1x1): %zu B of LDS", lds);
+    const long nvox = (long)a.Dc * a.Hc * a.Wc;
+    NPS_CHECK_ARG(nvox < (1L << 31) - 32, "conv3d (1x1x1): volume too large");
+    const long ntv = (nvox + 31) / 32;
+    // one round of resident work-groups (occupancy x CUs) over the whole grid, split over the samples; at most
+    // one tile per wave
+    static int resident = 0;  // (per instantiation: sized for the first launch's LDS)
+    if (resident == 0) {
+        int dev = 0, ncu = 0, occ = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+            ncu = 256;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, conv3d_1x1_kernel<NCB, NCH, PRO>, 256, lds) !=
+                hipSuccess || occ <= 0)
+            occ = 2;
+        resident = ncu * occ;
+    }
+    long per = (resident + a.B - 1) / a.B;
+    if (per > (ntv + 3) / 4) per = (ntv + 3) / 4;
+    conv3d_1x1_kernel<NCB, NCH, PRO><<<dim3((unsigned)per, (unsigned)a.B), 256, lds, s>>>(a, nchunk);
+    NPS_CHECK_LAUNCH("conv3d (1x1x1)");
+    return 0;
+}
+
+template <bool PRO>
+int dispatch_1x1(const nps_conv3d_t& a, int nchunk, hipStream_t s) {
+    const bool w4 = a.Cout > 64;
+    if (nchunk <= 5) return w4 ? launch_1x1<4, 5, PRO>(a, nchunk, s) : launch_1x1<2, 5, PRO>(a, nchunk, s);
+    if (nchunk <= 9) return w4 ? launch_1x1<4, 9, PRO>(a, nchunk, s) : launch_1x1<2, 9, PRO>(a, nchunk, s);
+    return w4 ? launch_1x1<4, 16, PRO>(a, nchunk, s) : launch_1x1<2, 16, PRO>(a, nchunk, s);
+}
+
 template <typename T, int K, int S, int TH, bool SIMPLE>
 int launch(const nps_conv3d_t& a, int nchunk, int ntile, hipStream_t s) {
     using G = Geo<K, S, TH>;
@@ -852,6 +1104,9 @@ extern "C" int nps_conv3d_fwd(const nps_conv3d_t* ap, void* stream) {
     // of a transposed conv write disjoint elements)
     const int nchunk = (a.Cin + 15) / 16, ntile = (a.Cout + 63) / 64;
     hipStream_t s = (hipStream_t)stream;
+    if (c3d_1x1_eligible(a))
+        return (a.gn_stats != nullptr || a.pre_act != 0) ? dispatch_1x1<true>(a, nchunk, s)
+                                                         : dispatch_1x1<false>(a, nchunk, s);
     return a.bf16 ? dispatch<bf16_t>(a, nchunk, ntile, s) : dispatch<float>(a, nchunk, ntile, s);
 }
 

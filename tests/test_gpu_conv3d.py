@@ -249,3 +249,65 @@ def test_conv3d_out_stats_with_accumulate_addend_act_and_phases(dt):
     u = ops.conv3d([ops.Src3(x)], dhw, ops.pack_conv3d_weight(wt.to(DEV), transposed=True, bf16=bf), None, 32, 2,
                    transposed=True, circ=1, zpad=1, out_stats=st)
     torch.testing.assert_close(carried(st), passes(u), rtol=1e-5, atol=1e-2)
+
+
+@pytest.mark.parametrize("cout", [64, 96, 128])
+@pytest.mark.parametrize("chans,offs", [((64, 4), ((0, 0, 0), (0, 0, 0))),
+                                        ((64, 64, 4), ((0, 0, 0), (-1, 1, 0), (1, 0, 0))),
+                                        ((192, 8), ((0, 0, 0), (0, -2, 1)))])
+def test_conv3d_1x1x1_bf16_streaming(cout, chans, offs):
+    """The bf16 1x1x1 kernel (conv3d_1x1_kernel: weights resident in LDS, every K-step's load of a 32-voxel tile in
+    flight at once): the ResidualBlock shortcut over cat(h, crop_Nd(skip), crop_Nd(vb)) at Cin 68 / 132 / 200 (5, 9
+    and 16 K-step register sets), Cout 64 / 96 / 128 (2 and 4 channel blocks), a volume that is not a multiple of
+    32 voxels; bias, out_stats; against fp64 on the bf16-rounded operands, and the moments against a gn_stats3d pass."""
+    from nps_hip import ops
+    torch.manual_seed(13)
+    B, dhw = 2, (5, 9, 37)
+    xs = []
+    for k, (c, o) in enumerate(zip(chans, offs)):
+        shp = tuple(n - 2 * oo for n, oo in zip(dhw, o))  # crop (< 0): larger; zero-pad (> 0): smaller
+        xs.append(torch.randn(B, c, *shp) * (1 + 0.5 * k))
+    dt = torch.bfloat16
+    cin = sum(chans)
+    w, b = torch.randn(cout, cin, 1, 1, 1) / cin ** 0.5, torch.randn(cout) * 0.1
+    fr = _frame([(_rt(x, dt), o) for x, o in zip(xs, offs)], B, dhw)
+    ref = F.conv3d(fr, _rt(w, dt), b.double())
+    srcs = [ops.Src3(_ndhwc(x, dt), *o) for x, o in zip(xs, offs)]
+    st = ops.new_stats(B, srcs[0].t)
+    y = ops.conv3d(srcs, dhw, ops.pack_conv3d_weight(w.to(DEV), bf16=True), b.to(DEV), cout, 1, out_stats=st)
+    assert rel_l2(_ncdhw(y), ref) < 1e-2
+    got = ops._stats_sum([st], B, ops.new_stats(B, y, 1)).cpu()[:, 0]
+    torch.testing.assert_close(got, ops.gn_stats3d([ops.Src3(y)], dhw, 1).cpu()[:, 0], rtol=1e-5, atol=1e-2)
+
+
+def test_conv3d_1x1x1_bf16_streaming_prologue_epilogue():
+    """The same kernel with the GroupNorm(2) + GELU prologue on a cropped two-source frame, written at a crop offset
+    with addend + GELU, and accumulating (the change's moments into a buffer seeded with the old output's)."""
+    from nps_hip import ops
+    torch.manual_seed(14)
+    dt = torch.bfloat16
+    B, dhw = 2, (6, 10, 35)
+    h, v = torch.randn(B, 64, *dhw) + 0.3, torch.rand(B, 4, 6, 8, 35)
+    offs = [(0, 0, 0), (0, 1, 0)]
+    gamma, beta = 1 + 0.2 * torch.randn(68), 0.1 * torch.randn(68)
+    fr = _frame([(_rt(h, dt), offs[0]), (_rt(v, dt), offs[1])], B, dhw)
+    n = _rt(F.gelu(F.group_norm(fr, 2, gamma.double(), beta.double(), eps=1e-5)), dt)
+    w, b = torch.randn(64, 68, 1, 1, 1) / 68 ** 0.5, torch.randn(64) * 0.1
+    srcs = [ops.Src3(_ndhwc(t, dt), *o) for t, o in zip((h, v), offs)]
+    gn = ops.GN(ops.gn_stats3d(srcs, dhw, 2), gamma.to(DEV), beta.to(DEV), 2, 1e-5)
+    wp = ops.pack_conv3d_weight(w.to(DEV), bf16=True)
+    # crop to (4, 8, 33) at offset -1 with addend + GELU
+    addend = torch.randn(B, 64, 4, 8, 33)
+    want = F.gelu(F.conv3d(n, _rt(w, dt), b.double())[:, :, 1:5, 1:9, 1:34] + _rt(addend, dt))
+    o2 = torch.empty(B, 4, 8, 33, 64, dtype=dt, device=DEV)
+    ops.conv3d(srcs, dhw, wp, b.to(DEV), 64, 1, gn=gn, pre_act=1, out=o2, out_off=(-1, -1, -1),
+               addend=_ndhwc(addend, dt), act=1)
+    assert rel_l2(_ncdhw(o2), want) < 1e-2
+    # accumulate into a seeded output
+    base = torch.randn(B, 64, *dhw)
+    out = _ndhwc(base, dt)
+    st = ops.copy_stats(ops.gn_stats3d([ops.Src3(out)], dhw, 1))
+    ops.conv3d(srcs, dhw, wp, b.to(DEV), 64, 1, gn=gn, pre_act=1, out=out, accumulate=True, out_stats=st)
+    assert rel_l2(_ncdhw(out), F.conv3d(n, _rt(w, dt), b.double()) + _rt(base, dt)) < 1e-2
+    got = ops._stats_sum([st], B, ops.new_stats(B, out, 1)).cpu()[:, 0]
+    torch.testing.assert_close(got, ops.gn_stats3d([ops.Src3(out)], dhw, 1).cpu()[:, 0], rtol=1e-5, atol=1e-2)
