@@ -367,6 +367,10 @@ typedef struct {
     int Hx, Wx, N;
     int KH, KW, dil, pad_y, pad_x, circ;
     float* g;                       /* [M][N][KH*KW], accumulated with += */
+    /* [M] or NULL: the split-fp16 entry points (nps_conv2d_wgrad_x3 / _set) also give db[m] = sum_{b,py,px}
+     * a[b][py][px][m] — the conv's bias gradient when a = dy — with g's semantics (+= / =), from the values the
+     * kernel stages anyway (no nps_channel_sums pass over dy).  Must be NULL for nps_conv2d_wgrad. */
+    float* db;
 } nps_wgrad_t;
 size_t nps_wgrad_lds_bytes(int KH, int KW);
 int nps_conv2d_wgrad(const nps_wgrad_t* p, void* stream);
@@ -376,7 +380,7 @@ int nps_conv2d_wgrad(const nps_wgrad_t* p, void* stream);
  * a_range / x_range (NPS_TAG_FLOATS floats, e.g. from nps_absmax) before the split.  ws: a device
  * workspace of nps_wgrad_x3_ws_floats(M, N, KH, KW) floats (the split-K partials accumulate there
  * tap-major, then fold into g).  Same geometry and += semantics as nps_conv2d_wgrad. */
-size_t nps_wgrad_x3_ws_floats(int M, int N, int KH, int KW);
+size_t nps_wgrad_x3_ws_floats(int M, int N, int KH, int KW);  /* KH*KW*M*N partials + M (the bias row) */
 int nps_conv2d_wgrad_x3(const nps_wgrad_t* p, const float* a_range, const float* x_range, float* ws, void* stream);
 /* The same, storing G = the weight gradient (g need not be zeroed beforehand) instead of adding to it. */
 int nps_conv2d_wgrad_x3_set(const nps_wgrad_t* p, const float* a_range, const float* x_range, float* ws,

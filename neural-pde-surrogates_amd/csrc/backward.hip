@@ -748,6 +748,7 @@ extern "C" int nps_conv2d_wgrad(const nps_wgrad_t* pp, void* stream) {
                   "conv2d_wgrad: bad shape");
     NPS_CHECK_ARG(p.KH >= 1 && p.KH <= 5 && p.KW >= 1 && p.KW <= 5 && p.dil >= 1 && p.circ >= 0,
                   "conv2d_wgrad: kernel %dx%d dil %d unsupported", p.KH, p.KW, p.dil);
+    NPS_CHECK_ARG(p.db == nullptr, "conv2d_wgrad: the bias gradient (db) is computed by the split-fp16 entry points only");
     const int T = p.dil;
     const int ny = (p.Ha + T - 1) / T, nx = (p.Wa + T - 1) / T;
     const long tiles_y = (long)T * ((ny + WG_TH - 1) / WG_TH), tiles_x = (long)T * ((nx + WG_TW - 1) / WG_TW);

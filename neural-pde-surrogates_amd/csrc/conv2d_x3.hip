@@ -848,8 +848,13 @@ __global__ __launch_bounds__(512) void conv1x1_x3_kernel(const nps_conv2d_t a) {
 // proc_unet_modern.py:191-196) applied to each loaded input element before the split, instead of a frame_pack
 // pass: per-channel affine (scale, shift) of this work-group's sample in an LDS table built at kernel start from the
 // fp64 moments, then GELU; frame pixels no source covers get act(GN(0)), the conv's own zero padding stays 0.
+// Cout > NCB * 32 (the input-gradient convs 192 -> 388 / 196 of the shortcut and FNO 1x1s): channel groups of
+// NCB * 32, group g = work-group index / 8 % ng, pixel tile = the rest (nps_launch_conv2d_x3: the ng groups of one
+// tile are 8 work-groups apart, so they run on one XCD and the later ones read the tile's input from its L2);
+// a group's blocks past Cout skip their MFMAs (the 4-channel tail group of 388 costs 1 block of 6).
 template <int NCB, int D, bool PRO = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void conv1x1_wl_kernel(const nps_conv2d_t a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void conv1x1_wl_kernel(const nps_conv2d_t a,
+                                                                                                  int ng) {
     constexpr int WSTAGE = 2 * NCB * 2048;       // bytes of one stage's weight fragments
     constexpr int WPT = WSTAGE / (256 * 16);     // 16-B pieces per thread per stage
     static_assert(WSTAGE % (256 * 16) == 0, "weight stage split");
@@ -858,7 +863,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     const int b = blockIdx.y;
     const int h = lane >> 5;
     const int npx = a.Hout * a.Wout;
-    const int P = blockIdx.x * 128 + wv * 32 + (lane & 31);
+    int tile = (int)blockIdx.x, grp = 0;
+    if (ng > 1) {
+        const int r = (int)blockIdx.x >> 3;
+        grp = r % ng;
+        tile = (r / ng) * 8 + ((int)blockIdx.x & 7);
+        if (tile * 128 >= npx) return;  // (the tile count is padded to a multiple of 8)
+    }
+    const int cob = grp * NCB * 32;                       // this group's first output channel
+    const int nact = min(NCB, (a.Cout - cob + 31) / 32);  // its blocks that hold output channels
+    const int P = tile * 128 + wv * 32 + (lane & 31);
     const float xs = PRO ? gn_prologue_scale(a) : in_scale_of(a);
     const bool scaled = PRO || has_in_scale(a);
     int fy, fx;
@@ -914,7 +928,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     };
     // weight stage st: chunks 2st, 2st + 1, blocks [0, NCB) of each (the packed chunk holds packed_ncb blocks)
     const size_t gstride = (size_t)packed_ncb(a.Cout) * 2048;
-    const char* wg = reinterpret_cast<const char*>(a.wpack);
+    const char* wg = reinterpret_cast<const char*>(a.wpack) + (size_t)grp * NCB * 2048;
     f32x4 wr[WPT];
     auto wfetch = [&](int st) {
 #pragma unroll
@@ -931,7 +945,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     };
     if ((int)threadIdx.x < NCB * 32)  // the epilogue's bias table (zero past Cout), behind the first barrier
         reinterpret_cast<float*>(wl + 2 * WSTAGE)[threadIdx.x] =
-            (a.bias != nullptr && (int)threadIdx.x < a.Cout) ? a.bias[threadIdx.x] : 0.f;
+            (a.bias != nullptr && cob + (int)threadIdx.x < a.Cout) ? a.bias[cob + threadIdx.x] : 0.f;
     // PRO: per-channel GroupNorm affine of sample b, y = x * gs[c] + gb[c] (gs = rstd * gamma, gb = beta - mean * gs, the
     // producers' form in conv2d_x3_kernel), zero past Cin (GELU(0) = 0 against zero weights)
     float* gtab = reinterpret_cast<float*>(wl + 2 * WSTAGE + NCB * 32 * 4);  // [2][nstages * 32]
@@ -1016,6 +1030,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
                 const f16x8 Bl = f16x8{l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
 #pragma unroll
                 for (int cb = 0; cb < NCB; ++cb) {
+                    if (cb >= nact) break;  // (uniform: a tail group's empty blocks)
                     const f16x8 Ah = *reinterpret_cast<const f16x8*>(wb + (k * NCB + cb) * 2048);
                     const f16x8 Al = *reinterpret_cast<const f16x8*>(wb + (k * NCB + cb) * 2048 + 1024);
                     acc[cb] = X3_MFMA(Ah, Bh, acc[cb], 0, 0, 0);
@@ -1036,7 +1051,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
             // work-group's 128 pixels lie in one row (Wout % 128 == 0, host-checked): Z' of that row and the
             // pixels' twiddles are staged in the (free) weight buffers, behind the exchange slot at their start.
             const int m2 = a.spec_m2, K2 = 2 * m2;
-            const int t0 = (int)blockIdx.x * 128, y0 = t0 / a.Wout, x0 = t0 - y0 * a.Wout;
+            const int t0 = tile * 128, y0 = t0 / a.Wout, x0 = t0 - y0 * a.Wout;  // (Cout <= NCB * 32: one group)
             float* zs = reinterpret_cast<float*>(wl + 256);                 // [K2][NCB * 32]
             float* ts = zs + K2 * NCB * 32;                                   // [128][K2]
             const float fac = a.spec_scale / inv;
@@ -1090,7 +1105,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
             auto load = [&](int cb) {
 #pragma unroll
                 for (int m = 0; m < 4; ++m) {
-                    const int co0 = cb * 32 + 8 * m + 4 * h;
+                    const int co0 = cob + cb * 32 + 8 * m + 4 * h;
                     const bool ok = pout && co0 < a.Cout;
                     a0[m] = *reinterpret_cast<const f32x4*>(ok ? a.addend0 + base + co0 : x3_zero16);
                 }
@@ -1102,7 +1117,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
 #pragma unroll
                 for (int m = 0; m < 4; ++m) {
                     const int co0 = cb * 32 + 8 * m + 4 * h;
-                    const bool ok = pout && co0 < a.Cout;
+                    const bool ok = pout && cob + co0 < a.Cout;
                     const f32x4 bi = *reinterpret_cast<const f32x4*>(btab + co0);
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
@@ -1129,7 +1144,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int m = 0; m < 4; ++m) {
-                    const int co0 = cb * 32 + 8 * m + 4 * h;
+                    const int co0 = cob + cb * 32 + 8 * m + 4 * h;
                     const bool ok = pout && co0 < a.Cout;
                     const f32x4 r = {acc[cb][4 * m], acc[cb][4 * m + 1], acc[cb][4 * m + 2], acc[cb][4 * m + 3]};
                     *reinterpret_cast<f32x4*>(ok ? a.out + base + co0 : x3_sink + 4 * lane) = r;
@@ -1149,11 +1164,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     if (pout) {
 #pragma unroll
         for (int cb = 0; cb < NCB; ++cb) {
-            if (cb * 32 >= a.Cout) continue;
+            if (cob + cb * 32 >= a.Cout) continue;
             f32x16 v = acc[cb];
 #pragma unroll
             for (int r = 0; r < 16; ++r) v[r] *= inv;
-            store_tile(a, b, cb * 32, h, v, dy, dx, amax);
+            store_tile(a, b, cob + cb * 32, h, v, dy, dx, amax);
         }
     }
     nps::tag_publish(a.out_tag, amax, nps::wave_salt());
@@ -1165,11 +1180,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
         if (pout) {
 #pragma unroll
             for (int cb = 0; cb < NCB; ++cb) {
-                if (cb * 32 >= a.Cout) continue;
+                if (cob + cb * 32 >= a.Cout) continue;
                 float f1 = 0.f, f2 = 0.f;
 #pragma unroll
                 for (int m = 0; m < 4; ++m) {
-                    const int co0 = cb * 32 + 8 * m + 4 * h;
+                    const int co0 = cob + cb * 32 + 8 * m + 4 * h;
                     if (co0 >= a.Cout) continue;
                     const f32x4 z = {0.f, 0.f, 0.f, 0.f};
                     const f32x4 bi = a.bias ? *reinterpret_cast<const f32x4*>(a.bias + co0) : z;
@@ -1203,6 +1218,13 @@ void launch_x3_one(const nps_conv2d_t& a, unsigned nwg, int lds, hipStream_t s) 
 
 }  // namespace
 
+
+// dev knob NPS_X1_GROUPS=0: 1x1 convs with Cout > 192 on the co-block kernel (conv1x1_x3_kernel) instead of the
+// LDS-weight kernel's channel groups
+static const int g_x1_groups = [] {
+    const char* e = getenv("NPS_X1_GROUPS");
+    return (e != nullptr && e[0] == '0') ? 0 : 1;
+}();
 
 // test hook (nps_x3_set_grid): persistent-grid size override (> 0)
 static long g_x3_grid_override = 0;
@@ -1263,16 +1285,20 @@ int nps_launch_conv2d_x3(const nps_conv2d_t& a, int lds, hipStream_t s) {
             const long nb = ((long)a.Hout * a.Wout + 127) / 128;
             NPS_CHECK_ARG(nb < (1L << 31) && a.B < 65536, "conv2d_fwd: grid too large");
             const int ncp = ((a.Cin + 31) / 32) * 32;
-            conv1x1_wl_kernel<6, 2, true><<<dim3((unsigned)nb, a.B), 256, 2 * 2 * 6 * 2048 + 6 * 32 * 4 + 2 * ncp * 4, s>>>(a);
+            conv1x1_wl_kernel<6, 2, true><<<dim3((unsigned)nb, a.B), 256, 2 * 2 * 6 * 2048 + 6 * 32 * 4 + 2 * ncp * 4, s>>>(a, 1);
             NPS_CHECK_LAUNCH("conv2d_fwd (split-fp16 1x1, LDS weights, GroupNorm prologue)");
             return 0;
         }
         if (nps_launch_conv1x1_res(a, res_on, s)) return 0;  // resident weights (conv1x1_res.hip)
-        if (a.Cout <= 192) {  // (Cout 193..256 measured slower with 8 blocks per wave: co-block waves)
-            const long nb = ((long)a.Hout * a.Wout + 127) / 128;
+        if (a.Cout <= 192 || g_x1_groups) {
+            // Cout > 192: channel groups of 192 (the input-gradient convs 192 -> 388 / 196), the ng groups of a pixel
+            // tile 8 work-groups apart (one XCD: the later groups read the tile from L2), tiles padded to 8
+            const int ng = (a.Cout + 191) / 192;
+            long nb = ((long)a.Hout * a.Wout + 127) / 128;
+            if (ng > 1) nb = (nb + 7) / 8 * 8 * ng;
             NPS_CHECK_ARG(nb < (1L << 31) && a.B < 65536, "conv2d_fwd: grid too large");
             // B-ring depth 2: measured fastest on every rollout shape (profiles/r1_conv_shapes_1x1_wl_depth.log)
-            conv1x1_wl_kernel<6, 2><<<dim3((unsigned)nb, a.B), 256, 2 * 2 * 6 * 2048 + 6 * 32 * 4, s>>>(a);
+            conv1x1_wl_kernel<6, 2><<<dim3((unsigned)nb, a.B), 256, 2 * 2 * 6 * 2048 + 6 * 32 * 4, s>>>(a, ng);
             NPS_CHECK_LAUNCH("conv2d_fwd (split-fp16 1x1, LDS weights)");
             return 0;
         }
@@ -1333,9 +1359,10 @@ extern "C" long nps_conv2d_x3_weight_span(const nps_conv2d_t* ap) {
         if (!pro && nps_conv1x1_res_plan(a, all, &rncb, &rng, &rnres)) {
             // conv1x1_res_kernel: chunks [0, nres), blocks [0, ng * NCB) (group grp at grp * NCB)
             top((rnres - 1) * gstride + (long)rng * rncb * 2048);
-        } else if (a.Cout <= 192) {
-            // conv1x1_wl_kernel<6, *>: wfetch(min(st + 2, last)) -> chunks 2 last + 1, 6 blocks of the chunk
-            top((2 * nst - 1) * gstride + 6 * 2048);
+        } else if (a.Cout <= 192 || g_x1_groups) {
+            // conv1x1_wl_kernel<6, *>: wfetch(min(st + 2, last)) -> chunks 2 last + 1, 6 blocks of the chunk at
+            // its group's offset (ng groups of 6 blocks)
+            top((2 * nst - 1) * gstride + (long)((a.Cout + 191) / 192) * 6 * 2048);
         } else {
             // conv1x1_x3_kernel: wave block min(cob, ncb / 2 - 1) x 2 blocks, chunks 2 st + k
             top((2 * nst - 1) * gstride + ncb * 2048);

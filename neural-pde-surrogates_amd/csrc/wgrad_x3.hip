@@ -61,6 +61,22 @@ __device__ __forceinline__ f16x8 shifted_run(const unsigned (&d)[6]) {
 // makes them drain the newest loads too)
 __device__ __attribute__((aligned(16))) float wx_zero4[4];
 
+// Bias gradient beside the weight gradient (nps_wgrad_t.db, a = dy): the A staging threads of the work-groups of
+// n-tile 0 (each A element is staged once per n-tile) sum the raw values they stage, per channel quad, over their
+// split; the 16 lanes of a quarter-wave that stage one quad combine their sums, and one lane adds each channel into
+// the workspace's bias row wsb[M] (zeroed with the partials, stored into db by the fold) — the separate
+// nps_channel_sums pass over dy and its zero-fill are gone.
+__device__ __forceinline__ void db_flush(float* wsb, int m, int M, f32x4 s) {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) s[e] += __shfl_xor(s[e], o);
+    if ((threadIdx.x & 15) == 0)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            if (m + e < M) atomicAdd(wsb + m + e, s[e]);
+}
+
 // Work-group (8 waves, 512 threads, one per CU) = 64 m x 64 n x KH*KW taps over a range of pixel tiles
 // (split K).  Wave w owns 32 m x 32 n (wm = w & 1, wn = (w >> 1) & 1) and half the taps: waves 0-3 taps
 // [0, NT0), waves 4-7 taps [NT0, NT) — one 32x32 accumulator per tap; waves w and w + 4 share a SIMD, so
@@ -78,7 +94,8 @@ __device__ __attribute__((aligned(16))) float wx_zero4[4];
 template <int KH, int KW>
 __global__ __launch_bounds__(512) void wgrad_x3_kernel(const nps_wgrad_t p, const float* a_range,
                                                        const float* x_range, float* __restrict__ ws, int ntiles,
-                                                       int tiles_per_split, int n_nt, int base, int xcd_remap) {
+                                                       int tiles_per_split, int n_nt, int base, int xcd_remap,
+                                                       float* wsb) {
     constexpr int NT = KH * KW;
     constexpr bool ROWSPLIT = NT == 1;
     constexpr int NT0 = ROWSPLIT ? 1 : (NT + 1) / 2;       // taps of waves 0-3
@@ -191,6 +208,10 @@ __global__ __launch_bounds__(512) void wgrad_x3_kernel(const nps_wgrad_t p, cons
             *reinterpret_cast<h2f*>(L + base + e * pitch) = h2f{l0[e], l1[e]};
         }
     };
+    const bool dbo = wsb != nullptr && nt == 0;  // bias-gradient partials (db_flush)
+    f32x4 dbs[NA];
+#pragma unroll
+    for (int k = 0; k < NA; ++k) dbs[k] = f32x4{0.f, 0.f, 0.f, 0.f};
     auto commit = [&](int i, const f32x4 (&ra)[NA][2], const f32x4 (&rb)[NB][2]) {
         _Float16* Ah = wsm + (i & 1) * BUF;
         _Float16* Al = Ah + 64 * WX_APITCH;
@@ -198,7 +219,10 @@ __global__ __launch_bounds__(512) void wgrad_x3_kernel(const nps_wgrad_t p, cons
         _Float16* Bl = Bh + 64 * BP;
 #pragma unroll
         for (int k = 0; k < NA; ++k)
-            if (a_lds[k] >= 0) put(Ah, Al, a_lds[k], WX_APITCH, ra[k][0], ra[k][1], sa);
+            if (a_lds[k] >= 0) {
+                put(Ah, Al, a_lds[k], WX_APITCH, ra[k][0], ra[k][1], sa);
+                if (dbo) dbs[k] += ra[k][0] + ra[k][1];
+            }
 #pragma unroll
         for (int k = 0; k < NB; ++k)
             if (b_lds[k] >= 0) put(Bh, Bl, b_lds[k], BP, rb[k][0], rb[k][1], sx);
@@ -302,6 +326,11 @@ __global__ __launch_bounds__(512) void wgrad_x3_kernel(const nps_wgrad_t p, cons
         __syncthreads();
     }
 
+    if (dbo) {
+#pragma unroll
+        for (int k = 0; k < NA; ++k)
+            if (a_lds[k] >= 0) db_flush(wsb, a_m[k], p.M, dbs[k]);  // (a_lds: uniform per 16-lane group)
+    }
     // this split's partial into the tap-major workspace W[tap][m][n]: lane holds rows (r/4)*8 + h*4 + r%4,
     // column lane%32, so one atomic wave-instruction covers two 128-B runs (the full-rate shape; the
     // [m][n][tap] order of G would scatter the 64 lanes 36 B apart)
@@ -343,7 +372,7 @@ constexpr size_t W1_LDS = (size_t)2 * W1_BUF * 2;   // two buffers, bytes
 __global__ __launch_bounds__(512) void wgrad1_wide_kernel(const nps_wgrad_t p, const float* a_range,
                                                           const float* x_range, float* __restrict__ ws,
                                                           long npix, int ntiles, int tiles_per_split, int n_nt,
-                                                          int base, int xcd_remap) {
+                                                          int base, int xcd_remap, float* wsb) {
     extern __shared__ __attribute__((aligned(16))) _Float16 w1sm[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     int tile, split;
@@ -390,11 +419,14 @@ __global__ __launch_bounds__(512) void wgrad1_wide_kernel(const nps_wgrad_t p, c
                 r[k][j] = *reinterpret_cast<const f32x4*>(q);
             }
     };
+    const bool dbo = wsb != nullptr && nt == 0 && !isx;  // bias-gradient partials of the A stagers (db_flush)
+    f32x4 dbs[3] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
     auto commit = [&](int i, const f32x4 (&r)[3][2]) {
         _Float16* H = w1sm + (i & 1) * W1_BUF + (isx ? 2 * W1_ROWS * W1_PITCH : 0);
         _Float16* L = H + W1_ROWS * W1_PITCH;
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
+            if (dbo) dbs[k] += r[k][0] + r[k][1];
             f16x4 h0, l0, h1, l1;
             split4(r[k][0] * scale, h0, l0);
             split4(r[k][1] * scale, h1, l1);
@@ -456,6 +488,10 @@ __global__ __launch_bounds__(512) void wgrad1_wide_kernel(const nps_wgrad_t p, c
         __syncthreads();
     }
 
+    if (dbo) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) db_flush(wsb, m0 + it_c[k], p.M, dbs[k]);
+    }
     // ---- partial into W[m][n]: lane holds rows (rr/4)*8 + h*4 + rr%4 of each block, column lane%32
     const float inv = 1.f / (sa * sx);
 #pragma unroll
@@ -489,7 +525,8 @@ constexpr size_t W2_LDS = (size_t)2 * W2_BUF * 2;
 
 __global__ __launch_bounds__(512) void wgrad2_wide_kernel(const nps_wgrad_t p, const float* a_range,
                                                           const float* x_range, float* __restrict__ ws, int ntiles,
-                                                          int tiles_per_split, int n_nt, int base, int xcd_remap) {
+                                                          int tiles_per_split, int n_nt, int base, int xcd_remap,
+                                                          float* wsb) {
     constexpr int PC = W2_TW + 1, PPR = (PC + 1) / 2;  // useful patch columns, pixel pairs per patch row (9)
     constexpr int NPB = W2_PR * PPR;                    // patch pixel pairs (27)
     extern __shared__ __attribute__((aligned(16))) _Float16 w2sm[];
@@ -578,12 +615,15 @@ __global__ __launch_bounds__(512) void wgrad2_wide_kernel(const nps_wgrad_t p, c
             *reinterpret_cast<h2f*>(L + base_o + e * pitch) = h2f{l0[e], l1[e]};
         }
     };
+    const bool dbo = wsb != nullptr && nt == 0;  // bias-gradient partials (db_flush)
+    f32x4 dbs = {0.f, 0.f, 0.f, 0.f};
     auto commit = [&](int i, const f32x4 (&ra)[2], const f32x4 (&rb)[2][2]) {
         _Float16* Ah = w2sm + (i & 1) * W2_BUF;
         _Float16* Al = Ah + W2_ROWS * W2_APITCH;
         _Float16* Bh = Al + W2_ROWS * W2_APITCH;
         _Float16* Bl = Bh + W2_ROWS * W2_BPITCH;
         put(Ah, Al, a_lds, W2_APITCH, ra[0], ra[1], sa);
+        if (dbo) dbs += ra[0] + ra[1];
 #pragma unroll
         for (int k = 0; k < 2; ++k)
             if (b_lds[k] >= 0) put(Bh, Bl, b_lds[k], W2_BPITCH, rb[k][0], rb[k][1], sx);
@@ -658,6 +698,7 @@ __global__ __launch_bounds__(512) void wgrad2_wide_kernel(const nps_wgrad_t p, c
         __syncthreads();
     }
 
+    if (dbo) db_flush(wsb, a_m, p.M, dbs);
     const float inv = 1.f / (sa * sx);
 #pragma unroll
     for (int kx = 0; kx < 2; ++kx) {
@@ -676,8 +717,10 @@ __global__ __launch_bounds__(512) void wgrad2_wide_kernel(const nps_wgrad_t p, c
     }
 }
 
-// G[m][n][tap] += W[tap][m][n] (acc), or = (nps_conv2d_wgrad_x3_set: G need not be zeroed first)
-__global__ void wgrad_fold_kernel(const float* __restrict__ w, float* __restrict__ g, int MN, int nt, int acc) {
+// G[m][n][tap] += W[tap][m][n] (acc), or = (nps_conv2d_wgrad_x3_set: G need not be zeroed first); the same for
+// the bias row (db += / = wsb) when the launch computed one
+__global__ void wgrad_fold_kernel(const float* __restrict__ w, float* __restrict__ g, int MN, int nt, int acc,
+                                  const float* __restrict__ wsb, float* __restrict__ db, int M) {
     const long total = (long)MN * nt;
     for (long o = (long)blockIdx.x * blockDim.x + threadIdx.x; o < total; o += (long)gridDim.x * blockDim.x) {
         const long mn = o / nt;
@@ -685,6 +728,9 @@ __global__ void wgrad_fold_kernel(const float* __restrict__ w, float* __restrict
         const float v = w[(size_t)t * MN + mn];
         g[o] = acc ? g[o] + v : v;
     }
+    if (db != nullptr)
+        for (int m = blockIdx.x * blockDim.x + threadIdx.x; m < M; m += gridDim.x * blockDim.x)
+            db[m] = acc ? db[m] + wsb[m] : wsb[m];
 }
 
 // Work-groups of the split-K grid: 2 per CU in turn (the first one's atomics overlap the second one's tiles), but 1
@@ -728,16 +774,17 @@ int launch_wgrad_x3(const nps_wgrad_t& p, const float* ar, const float* xr, floa
         attr_set = true;
     }
     const size_t MN = (size_t)p.M * p.N;
-    if (hipMemsetAsync(ws, 0, sizeof(float) * MN * KH * KW, s) != hipSuccess) {
+    float* wsb = p.db != nullptr ? ws + MN * KH * KW : nullptr;  // bias row behind the partials (db_flush)
+    if (hipMemsetAsync(ws, 0, sizeof(float) * (MN * KH * KW + (wsb ? p.M : 0)), s) != hipSuccess) {
         nps::set_error("conv2d_wgrad_x3: workspace memset failed");
         return -2;
     }
     wgrad_x3_kernel<KH, KW><<<(unsigned)(base * splits), 512, lds, s>>>(p, ar, xr, ws, (int)ntiles, per, n_nt,
-                                                                         (int)base, remap);
+                                                                         (int)base, remap, wsb);
     NPS_CHECK_LAUNCH("conv2d_wgrad_x3");
     const long total = (long)MN * KH * KW;
     const long nb = (total + 255) / 256;
-    wgrad_fold_kernel<<<(unsigned)(nb < 2048 ? nb : 2048), 256, 0, s>>>(ws, p.g, (int)MN, KH * KW, acc);
+    wgrad_fold_kernel<<<(unsigned)(nb < 2048 ? nb : 2048), 256, 0, s>>>(ws, p.g, (int)MN, KH * KW, acc, wsb, p.db, p.M);
     NPS_CHECK_LAUNCH("conv2d_wgrad_x3 (fold)");
     return 0;
 }
@@ -767,15 +814,16 @@ int launch_wgrad1_wide(const nps_wgrad_t& p, const float* ar, const float* xr, f
         attr_set = true;
     }
     const size_t MN = (size_t)p.M * p.N;
-    if (hipMemsetAsync(ws, 0, sizeof(float) * MN, s) != hipSuccess) {
+    float* wsb = p.db != nullptr ? ws + MN : nullptr;
+    if (hipMemsetAsync(ws, 0, sizeof(float) * (MN + (wsb ? p.M : 0)), s) != hipSuccess) {
         nps::set_error("conv2d_wgrad_x3: workspace memset failed");
         return -2;
     }
     wgrad1_wide_kernel<<<(unsigned)(base * splits), 512, W1_LDS, s>>>(p, ar, xr, ws, npix, (int)ntiles, per, n_nt,
-                                                                       (int)base, remap);
+                                                                       (int)base, remap, wsb);
     NPS_CHECK_LAUNCH("conv2d_wgrad_x3 (1x1 wide)");
     const long nb = ((long)MN + 255) / 256;
-    wgrad_fold_kernel<<<(unsigned)(nb < 2048 ? nb : 2048), 256, 0, s>>>(ws, p.g, (int)MN, 1, acc);
+    wgrad_fold_kernel<<<(unsigned)(nb < 2048 ? nb : 2048), 256, 0, s>>>(ws, p.g, (int)MN, 1, acc, wsb, p.db, p.M);
     NPS_CHECK_LAUNCH("conv2d_wgrad_x3 (fold)");
     return 0;
 }
@@ -805,15 +853,16 @@ int launch_wgrad2_wide(const nps_wgrad_t& p, const float* ar, const float* xr, f
         attr_set = true;
     }
     const size_t MN = (size_t)p.M * p.N;
-    if (hipMemsetAsync(ws, 0, sizeof(float) * MN * 4, s) != hipSuccess) {
+    float* wsb = p.db != nullptr ? ws + MN * 4 : nullptr;
+    if (hipMemsetAsync(ws, 0, sizeof(float) * (MN * 4 + (wsb ? p.M : 0)), s) != hipSuccess) {
         nps::set_error("conv2d_wgrad_x3: workspace memset failed");
         return -2;
     }
     wgrad2_wide_kernel<<<(unsigned)(base * splits), 512, W2_LDS, s>>>(p, ar, xr, ws, (int)ntiles, per, n_nt, (int)base,
-                                                                       remap);
+                                                                       remap, wsb);
     NPS_CHECK_LAUNCH("conv2d_wgrad_x3 (2x2 wide)");
     const long nb = ((long)MN * 4 + 255) / 256;
-    wgrad_fold_kernel<<<(unsigned)(nb < 2048 ? nb : 2048), 256, 0, s>>>(ws, p.g, (int)MN, 4, acc);
+    wgrad_fold_kernel<<<(unsigned)(nb < 2048 ? nb : 2048), 256, 0, s>>>(ws, p.g, (int)MN, 4, acc, wsb, p.db, p.M);
     NPS_CHECK_LAUNCH("conv2d_wgrad_x3 (fold)");
     return 0;
 }
@@ -831,7 +880,8 @@ const int g_wx_wide2 = [] {
 
 }  // namespace
 
-extern "C" size_t nps_wgrad_x3_ws_floats(int M, int N, int KH, int KW) { return (size_t)M * N * KH * KW; }
+// partials [KH*KW][M][N] + the bias row [M] (nps_wgrad_t.db)
+extern "C" size_t nps_wgrad_x3_ws_floats(int M, int N, int KH, int KW) { return (size_t)M * N * KH * KW + M; }
 
 namespace {
 int wgrad_x3_dispatch(const nps_wgrad_t* pp, const float* a_range, const float* x_range, float* ws, void* stream,

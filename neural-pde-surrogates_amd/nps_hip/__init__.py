@@ -58,7 +58,7 @@ class WgradArgs(ctypes.Structure):
         ("a", ctypes.c_void_p), ("B", ctypes.c_int), ("Ha", ctypes.c_int), ("Wa", ctypes.c_int), ("M", ctypes.c_int),
         ("x", ctypes.c_void_p), ("Hx", ctypes.c_int), ("Wx", ctypes.c_int), ("N", ctypes.c_int),
         ("KH", ctypes.c_int), ("KW", ctypes.c_int), ("dil", ctypes.c_int), ("pad_y", ctypes.c_int),
-        ("pad_x", ctypes.c_int), ("circ", ctypes.c_int), ("g", ctypes.c_void_p),
+        ("pad_x", ctypes.c_int), ("circ", ctypes.c_int), ("g", ctypes.c_void_p), ("db", ctypes.c_void_p),
     ]
 
 

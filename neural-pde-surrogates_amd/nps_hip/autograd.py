@@ -30,19 +30,24 @@ def _c(t):
 
 # ------------------------------------------------------------------------- weight gradient
 def wgrad(a: torch.Tensor, x: torch.Tensor, KH: int, KW: int, dil=1, pad=(0, 0), circ=0,
-          g: Optional[torch.Tensor] = None, a_range: Optional[int] = None, x_range: Optional[int] = None
-          ) -> torch.Tensor:
+          g: Optional[torch.Tensor] = None, a_range: Optional[int] = None, x_range: Optional[int] = None,
+          db: Optional[torch.Tensor] = None) -> torch.Tensor:
     """G[m][n][KH*KW] (+)= sum_pix a[pix][m] * Xext[pix + tap*dil - pad][n].
 
     Split-fp16 MFMA (nps_conv2d_wgrad_x3) under ops.CONV_PRECISION == PREC_X3F16 for undilated square
     kernels up to 3x3 over channel counts that are multiples of 4 — a and x range-scaled from their
     max |.| (a_range / x_range: a's / x's range-tag pointers when the caller already has them) — else exact fp32 MFMA
-    (nps_conv2d_wgrad)."""
+    (nps_conv2d_wgrad).  db ([M], with g is None): also db[m] = sum_pix a[pix][m] (the conv's bias gradient when
+    a = dy) — from the split-fp16 kernels' own staging of a (nps_wgrad_t.db), else an nps_channel_sums pass."""
     a, x = _c(a), _c(x)
     B, Ha, Wa, M = a.shape
     _, Hx, Wx, N = x.shape
     x3 = ops.CONV_PRECISION == ops.PREC_X3F16 and KH == KW and KH <= 3 and dil == 1
     store = g is None and x3 and M % 4 == 0 and N % 4 == 0  # the split-fp16 fold stores g: no zero-fill
+    if db is not None and not (store and FUSE_DB):
+        db.zero_()
+        check(lib.nps_channel_sums(ptr(a), a.numel() // M, M, ptr(db), stream_ptr()), "channel_sums")
+        db = None
     if g is None:
         g = (torch.empty if store else torch.zeros)((M, N, KH, KW), dtype=torch.float32, device=a.device)
     if (ops.CONV_PRECISION == ops.PREC_X3F16 and KH == KW and KH <= 3 and dil == 1 and (M % 4 or N % 4)):
@@ -70,6 +75,7 @@ def wgrad(a: torch.Tensor, x: torch.Tensor, KH: int, KW: int, dil=1, pad=(0, 0),
         ar = a_range if a_range is not None else _range_ptr(a)
         xr = x_range if x_range is not None else _range_ptr(x)
         ws = torch.empty(lib.nps_wgrad_x3_ws_floats(M, N, KH, KW), dtype=torch.float32, device=a.device)
+        p.db = ptr(db)  # (None -> NULL)
         arith = "x3w"
 
         fn = lib.nps_conv2d_wgrad_x3_set if store else lib.nps_conv2d_wgrad_x3
@@ -114,6 +120,11 @@ def _keep(t):
     _KEEP.append(t)
     del _KEEP[:-8]
     return t
+
+
+# the bias gradient of a conv from its weight-gradient launch (wgrad(db=...)) instead of a channel_sums pass over dy
+# (dev knob NPS_FUSE_DB=0: off)
+FUSE_DB = os.environ.get("NPS_FUSE_DB", "1") != "0"
 
 
 def channel_sums(x: torch.Tensor) -> torch.Tensor:
@@ -382,17 +393,20 @@ class Conv2dFn(torch.autograd.Function):
                                    in_scale=rng)
         if ctx.needs_input_grad[2]:
             with fork:
+                # the bias gradient from the weight-gradient launch's staging of gy (wgrad(db=...))
+                db = (torch.empty(Cout, dtype=torch.float32, device=gy.device)
+                      if ctx.has_bias and ctx.needs_input_grad[3] else None)
                 if s == 1:
-                    dw = wgrad(gy, xs, KH, KW, dil=d, pad=lo, circ=circ, a_range=rng)
+                    dw = wgrad(gy, xs, KH, KW, dil=d, pad=lo, circ=circ, a_range=rng, db=db)
                     if dw.shape[1] != Cin:      # input carried zero padding channels (packed encoder input)
                         dw = dw[:, :Cin].contiguous()
                 else:
                     C = Cin
-                    G = wgrad(gy, xs, 2, 2, a_range=rng)                       # [Cout][4C][2][2]
+                    G = wgrad(gy, xs, 2, 2, a_range=rng, db=db)                # [Cout][4C][2][2]
                     G = G.view(Cout, 2, 2, C, 2, 2).permute(0, 3, 4, 1, 5, 2).reshape(Cout, C, 4, 4)
                     dw = G[:, :, :3, :3].contiguous()
-            fork.join(dw)
-        if ctx.has_bias and ctx.needs_input_grad[3]:
+            fork.join(dw, *([db] if db is not None else []))
+        if ctx.has_bias and ctx.needs_input_grad[3] and db is None:
             db = channel_sums(gy)
         return None, dx, dw, db
 

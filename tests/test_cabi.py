@@ -28,7 +28,8 @@ import pytest
 
 @pytest.mark.parametrize("cstruct,pyname,srcname,pysrc", [("nps_conv2d_t", "Conv2dArgs", "nps_src_t", "Src"),
                                                          ("nps_conv3d_t", "Conv3dArgs", "nps_src3_t", "Src3"),
-                                                         ("nps_pack_job_t", "PackJob", "nps_src_t", "Src")])
+                                                         ("nps_pack_job_t", "PackJob", "nps_src_t", "Src"),
+                                                         ("nps_wgrad_t", "WgradArgs", "nps_src_t", "Src")])
 def test_struct_layout_matches_header(cstruct, pyname, srcname, pysrc):
     """ctypes mirror vs a C compile of the header (offsetof / sizeof)."""
     import subprocess

@@ -575,3 +575,44 @@ def test_batched_repack_equals_individual_packs():
         for a, b in zip(gs, rs):
             n = a.numel() - 64 + 1  # the fragment body and trailer[0] = max|w| (the rest: absmax partials / unused)
             assert torch.equal(a[:n].view(torch.int32), b[:n].view(torch.int32)), kind
+
+
+@pytest.mark.parametrize("case", [c for c in WGRAD_X3_CASES if c[1] % 4 == 0 and c[2] % 4 == 0])
+def test_wgrad_x3_bias_gradient_from_staging(case):
+    """nps_wgrad_t.db: the split-fp16 weight-gradient launch also stores sum_pix a[pix][m] (the conv's bias gradient,
+    a = dy) from its own staging of a — on wgrad_x3_kernel (1x1 / 2x2 / 3x3 64 x 64 tiles), wgrad1_wide_kernel and
+    wgrad2_wide_kernel, with m-tails past one tile and several n-tiles (only n-tile 0 adds) — against the fp64 sums;
+    the weight gradient itself is unchanged by it."""
+    from nps_hip import autograd as ad
+    B, M, N, k, pad, circ, Ha, Wa, sa, sx = case
+    Hx, Wx = Ha + k - 1 - 2 * pad - 2 * circ, Wa + k - 1 - 2 * pad - 2 * circ
+    torch.manual_seed(2)
+    a = torch.randn(B, M, Ha, Wa, dtype=torch.float64) * sa + 0.1 * sa
+    x = torch.randn(B, N, Hx, Wx, dtype=torch.float64) * sx
+    ad_a = a.float().permute(0, 2, 3, 1).contiguous().to(DEV)
+    ad_x = x.float().permute(0, 2, 3, 1).contiguous().to(DEV)
+    db = torch.full((M,), float("nan"), device=DEV)
+    g1 = ad.wgrad(ad_a, ad_x, k, k, pad=(pad, pad), circ=circ, db=db)
+    g0 = ad.wgrad(ad_a, ad_x, k, k, pad=(pad, pad), circ=circ)
+    assert rel_l2(g1, g0) < 1e-6  # (split-K fp32 atomics: equal up to the order of the partial sums)
+    ref = a.sum((0, 2, 3))
+    assert rel_l2(db.cpu().double(), ref) < 1e-6, rel_l2(db.cpu().double(), ref)
+
+
+@pytest.mark.parametrize("cout", [388, 196, 256])
+def test_conv1x1_channel_groups_vs_fp64(cout):
+    """1x1 convs with Cout > 192 (the input-gradient convs 192 -> 388 / 196 of the shortcut and FNO 1x1s) on the
+    LDS-weight kernel's channel groups of 192: the groups of one pixel tile, the tail group's empty blocks skipped,
+    bias and an addend at an output channel stride, against fp64."""
+    from nps_hip import ops
+    torch.manual_seed(6)
+    B, H, W, cin = 2, 23, 37, 192
+    x = torch.randn(B, H, W, cin, dtype=torch.float64)
+    w = torch.randn(cout, cin, dtype=torch.float64) / cin ** 0.5
+    b = torch.randn(cout, dtype=torch.float64) * 0.1
+    add = torch.randn(B, H, W, cout, dtype=torch.float64)
+    ref = x @ w.T + b + add
+    wp = ops.pack_conv_weight(w.float().view(cout, cin, 1, 1).to(DEV))
+    y = ops.conv2d([ops.Src(x.float().to(DEV))], (H, W), wp, b.float().to(DEV), cout, 1, 1,
+                   addends=(add.float().to(DEV),))
+    assert rel_l2(y.cpu().double(), ref) < TOL
