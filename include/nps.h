@@ -198,6 +198,9 @@ int nps_conv2d_x3_sources_ok(const nps_src_t* src, int nsrc);
 /* Range tag `tag` (NPS_TAG_FLOATS floats) := max |x[i]| (zeroed, then raised) — the input range a
  * split-fp16 conv scales by (nps_conv2d_t.in_scale / in_tag*). */
 int nps_absmax(const float* x, long n, float* tag, void* stream);
+/* The same without the zeroing: raises `tag` (already zero, e.g. fresh from a zero-filled arena, or a valid lower
+ * bound) to >= max |x[i]| — no memset launch. */
+int nps_absmax_into(const float* x, long n, float* tag, void* stream);
 /* Stride-2 3x3 convs (U-Net Downsample, proc_unet_modern.py:445-455) run as 2x2 stride-1 convs
  * over a space-to-depth copy: out[B][Hq][Wq][4C], channel (dy*2+dx)*C + c = x[2y+dy-pad][2x+dx-pad][c]
  * (zero outside); pack the weight with transposed_phase = -2 (Cin = 4C). */
@@ -400,7 +403,9 @@ int nps_frame_pack_bwd_tagged(const nps_conv2d_t* a, const float* gy, float* con
                               float* dgamma, float* dbeta, double* work, void* stream);
 /* The same with gy_plain (or NULL): the gradient of the plain concatenation of the same sources (the frame without
  * prologue, shaped like gy) from a second consumer — the ResidualBlock's shortcut conv or identity path
- * (proc_unet_modern.py:243-250) — added into dsrc in the same pass instead of by a separate accumulation. */
+ * (proc_unet_modern.py:243-250) — added into dsrc in the same pass instead of by a separate accumulation.
+ * Unlike the two above, `work` must hold zeros on entry (e.g. a slice of a zero-filled buffer used once): no
+ * memset launch per frame. */
 int nps_frame_pack_bwd2(const nps_conv2d_t* a, const float* gy, const float* gy_plain, float* const* dsrc,
                         float* const* dtag, float* dgamma, float* dbeta, double* work, void* stream);
 

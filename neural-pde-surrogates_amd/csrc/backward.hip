@@ -859,14 +859,25 @@ extern "C" int nps_frame_pack_bwd(const nps_conv2d_t* ap, const float* gy, float
     return nps_frame_pack_bwd_tagged(ap, gy, dsrc, nullptr, dgamma, dbeta, work, stream);
 }
 
+namespace {
+int frame_pack_bwd_impl(const nps_conv2d_t* ap, const float* gy, const float* gy_plain, float* const* dsrc,
+                        float* const* dtag, float* dgamma, float* dbeta, double* work, bool work_zeroed, void* stream);
+}  // namespace
+
 extern "C" int nps_frame_pack_bwd_tagged(const nps_conv2d_t* ap, const float* gy, float* const* dsrc,
                                          float* const* dtag, float* dgamma, float* dbeta, double* work,
                                          void* stream) {
-    return nps_frame_pack_bwd2(ap, gy, nullptr, dsrc, dtag, dgamma, dbeta, work, stream);
+    return frame_pack_bwd_impl(ap, gy, nullptr, dsrc, dtag, dgamma, dbeta, work, false, stream);
 }
 
 extern "C" int nps_frame_pack_bwd2(const nps_conv2d_t* ap, const float* gy, const float* gy_plain, float* const* dsrc,
                                    float* const* dtag, float* dgamma, float* dbeta, double* work, void* stream) {
+    return frame_pack_bwd_impl(ap, gy, gy_plain, dsrc, dtag, dgamma, dbeta, work, true, stream);
+}
+
+namespace {
+int frame_pack_bwd_impl(const nps_conv2d_t* ap, const float* gy, const float* gy_plain, float* const* dsrc,
+                        float* const* dtag, float* dgamma, float* dbeta, double* work, bool work_zeroed, void* stream) {
     NPS_CHECK_ARG(ap && gy && dsrc, "frame_pack_bwd: null");
     const nps_conv2d_t& a = *ap;
     NPS_CHECK_ARG(a.nsrc >= 1 && a.nsrc <= NPS_MAX_SRC && a.B > 0 && a.Hin > 0 && a.Win > 0 && a.Cin > 0,
@@ -894,7 +905,7 @@ extern "C" int nps_frame_pack_bwd2(const nps_conv2d_t* ap, const float* gy, cons
     while (PXB > 64 && (long)((npix + PXB - 1) / PXB) * a.B < 1000) PXB >>= 1;
     if (a.gn_stats) {
         NPS_CHECK_ARG(a.Cin <= 4096, "frame_pack_bwd: Cin too large");
-        if (hipMemsetAsync(work, 0, sizeof(double) * 2 * a.B * a.Cin, s) != hipSuccess) {
+        if (!work_zeroed && hipMemsetAsync(work, 0, sizeof(double) * 2 * a.B * a.Cin, s) != hipSuccess) {
             nps::set_error("frame_pack_bwd: memset failed");
             return -2;
         }
@@ -929,3 +940,4 @@ extern "C" int nps_frame_pack_bwd2(const nps_conv2d_t* ap, const float* gy, cons
             return -2;
     return 0;
 }
+}  // namespace

@@ -1317,6 +1317,12 @@ extern "C" int nps_absmax(const float* x, long n, float* out, void* stream) {
         nps::set_error("absmax: memset failed");
         return -2;
     }
+    return nps_absmax_into(x, n, out, stream);
+}
+
+extern "C" int nps_absmax_into(const float* x, long n, float* out, void* stream) {
+    NPS_CHECK_ARG(x && out && n > 0, "absmax: bad args");
+    hipStream_t s = (hipStream_t)stream;
     long nb = (n + 256 * 16 - 1) / (256 * 16);
     nb = nb < 1 ? 1 : (nb > 1024 ? 1024 : nb);
     absmax_kernel<<<(unsigned)nb, 256, 0, s>>>(x, n, out);

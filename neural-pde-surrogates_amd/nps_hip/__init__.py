@@ -99,6 +99,7 @@ _SIGS = {
     "nps_conv2d_x3_sources_ok": (_i, [ctypes.POINTER(Src), _i]),
     "nps_conv2d_x3_prologue_ok": (_i, [_i, _i, _i, _i, _i]),
     "nps_absmax": (_i, [_vp, _l, _vp, _vp]),
+    "nps_absmax_into": (_i, [_vp, _l, _vp, _vp]),
     "nps_conv2d_plan": (_i, [ctypes.POINTER(Conv2dArgs)]),
     "nps_conv2d_x3_weight_span": (_l, [ctypes.POINTER(Conv2dArgs)]),
     "nps_conv2d_fwd": (_i, [ctypes.POINTER(Conv2dArgs), _vp]),

@@ -212,7 +212,7 @@ def _frame_bwd(ctx, gout, gplain):
         a.gn_groups, a.gn_eps = groups, eps
         dgamma = torch.empty_like(gamma)
         dbeta = torch.empty_like(beta)
-        work = torch.empty((B, 2, Cin), dtype=torch.float64, device=gout.device)
+        work = ops.new_stats(B, gout, Cin)  # zero on entry (nps_frame_pack_bwd2): a slice of a zeroed chunk
     a.pre_act = act
     need = ctx.needs_input_grad[3:]
     dsrc = [torch.empty_like(t) if need[i] else None for i, t in enumerate(srcs)]

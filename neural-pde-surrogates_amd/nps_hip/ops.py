@@ -284,7 +284,7 @@ def out_tag(t: torch.Tensor, accumulate: bool) -> int:
         return tag.ptr
     p = new_tag(t)
     if accumulate:
-        check(lib.nps_absmax(ptr(t), t.numel(), p, stream_ptr()), "absmax (tag seed)")
+        check(lib.nps_absmax_into(ptr(t), t.numel(), p, stream_ptr()), "absmax (tag seed)")  # (fresh: zero)
     return p
 
 
@@ -307,7 +307,7 @@ def input_tag(t: torch.Tensor) -> int:
     if tag is not None:
         return tag.ptr
     p = _arena(t.device).alloc().ptr if _side_depth > 0 else new_tag(t)
-    check(lib.nps_absmax(ptr(t), t.numel(), p, stream_ptr()), "absmax (input tag)")
+    check(lib.nps_absmax_into(ptr(t), t.numel(), p, stream_ptr()), "absmax (input tag)")  # (fresh arena tag: zero)
     return p
 
 
