@@ -765,7 +765,7 @@ __global__ __launch_bounds__(256) void frame_pack3d_kernel(const nps_conv3d_t a,
 // (Measured alternative, not kept: the tile staged through LDS with voxel-major coalesced quad loads and 16-B
 // stores — 2x slower, its per-quad addressing cost more than the fragment-shaped accesses it replaced.)
 // Grid: work-groups per sample x B, one round of resident work-groups.
-template <int NCB, int NCH, bool PRO, bool DB>
+template <int NCB, int NCH, bool PRO>
 __global__ __launch_bounds__(256) void conv3d_1x1_kernel(const nps_conv3d_t a, int nchunk) {
     constexpr int NCO = NCB * 32;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -854,16 +854,11 @@ __global__ __launch_bounds__(256) void conv3d_1x1_kernel(const nps_conv3d_t a, i
     const int tstride = gridDim.x * 4;
     int t = blockIdx.x * 4 + wave;
     Vec8<bf16_t> x[NCH];
-    if (DB && t < ntv) fetch(t, x);
+    if (t < ntv) fetch(t, x);
     for (; t < ntv; t += tstride) {
-        // DB: the next tile's loads first (two tiles in flight per wave); else this tile's only (more resident
-        // waves instead: the three-source frames, dev knob NPS_C3D_1X1_3SRC)
+        // next tile's loads first (two tiles in flight per wave)
         Vec8<bf16_t> xn[NCH];
-        if constexpr (DB) {
-            if (t + tstride < ntv) fetch(t + tstride, xn);
-        } else {
-            fetch(t, x);
-        }
+        if (t + tstride < ntv) fetch(t + tstride, xn);
         int cd, ch, cw;
         const bool vin = coords(t, cd, ch, cw);
         f32x16 acc[NCB];
@@ -892,8 +887,7 @@ __global__ __launch_bounds__(256) void conv3d_1x1_kernel(const nps_conv3d_t a, i
             }
         }
 #pragma unroll
-        for (int c = 0; c < NCH; ++c)
-            if constexpr (DB) x[c] = xn[c];
+        for (int c = 0; c < NCH; ++c) x[c] = xn[c];
         // epilogue (conv3d_kernel's bf16 vec4 path): lane holds voxel `col`, channels cb*32 + 8j + 4hl + (0..3)
         const int od = cd * a.out_os + a.out_off_d, oh = ch * a.out_os + a.out_off_h, ow = cw * a.out_os + a.out_off_w;
         if (!vin || od < 0 || od >= a.out_D || oh < 0 || oh >= a.out_H || ow < 0 || ow >= a.out_W) continue;
@@ -955,15 +949,6 @@ __global__ __launch_bounds__(256) void conv3d_1x1_kernel(const nps_conv3d_t a, i
     }
 }
 
-// dev knob NPS_C3D_1X1_3SRC=1: three-source frames on conv3d_1x1_kernel too (A/B)
-bool c3d_1x1_3src() {
-    static const int g = [] {
-        const char* e = std::getenv("NPS_C3D_1X1_3SRC");
-        return (e != nullptr && e[0] == '1') ? 1 : 0;
-    }();
-    return g != 0;
-}
-
 // dev knob NPS_C3D_1X1=0: 1x1x1 bf16 convs on conv3d_kernel (A/B)
 bool c3d_1x1_on() {
     static const int g = [] {
@@ -978,13 +963,14 @@ bool c3d_1x1_eligible(const nps_conv3d_t& a) {
     if (a.Cout > 128 || a.Cin > 256 || (a.Cout & 3) != 0 || (a.out_C & 3) != 0) return false;
     for (int i = 0; i < a.nsrc; ++i)
         if ((a.src[i].C & 3) != 0 || (i < a.nsrc - 1 && (a.src[i].C & 7) != 0)) return false;
-    // (three-source frames, the up-path cat(h, skip, vb): measured slower than conv3d_kernel, 437 vs 360 us at
-    // 132 -> 64 over 16 x 128^2, B = 8 — the per-piece source selection; two sources and GN-prologue frames gain)
-    if (a.nsrc > 2 && !c3d_1x1_3src()) return false;
+    // (three-source frames, the up-path cat(h, skip, vb): measured slower than conv3d_kernel — 437 vs 360 us at
+    // 132 -> 64 over 16 x 128^2, B = 8, double-buffered; 538 vs 363 single-buffered at 4 waves per SIMD; C5 -2 %,
+    // profiles/r6/experiments/c5_1x1x1_three_source_ab.txt; two sources and GN-prologue frames gain)
+    if (a.nsrc > 2) return false;
     return c3d_1x1_on();
 }
 
-template <int NCB, int NCH, bool PRO, bool DB>
+template <int NCB, int NCH, bool PRO>
 int launch_1x1(const nps_conv3d_t& a, int nchunk, hipStream_t s) {
     const size_t lds = (size_t)nchunk * NCB * 32 * 32 + NCB * 32 * sizeof(float) + 2 * (size_t)nchunk * 16 * sizeof(float) +
                        8 * sizeof(double);
@@ -1000,28 +986,24 @@ int launch_1x1(const nps_conv3d_t& a, int nchunk, hipStream_t s) {
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
             ncu = 256;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, conv3d_1x1_kernel<NCB, NCH, PRO, DB>, 256, lds) !=
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, conv3d_1x1_kernel<NCB, NCH, PRO>, 256, lds) !=
                 hipSuccess || occ <= 0)
             occ = 2;
         resident = ncu * occ;
     }
     long per = (resident + a.B - 1) / a.B;
     if (per > (ntv + 3) / 4) per = (ntv + 3) / 4;
-    conv3d_1x1_kernel<NCB, NCH, PRO, DB><<<dim3((unsigned)per, (unsigned)a.B), 256, lds, s>>>(a, nchunk);
+    conv3d_1x1_kernel<NCB, NCH, PRO><<<dim3((unsigned)per, (unsigned)a.B), 256, lds, s>>>(a, nchunk);
     NPS_CHECK_LAUNCH("conv3d (1x1x1)");
     return 0;
 }
 
-template <bool PRO, bool DB>
-int dispatch_1x1_db(const nps_conv3d_t& a, int nchunk, hipStream_t s) {
-    const bool w4 = a.Cout > 64;
-    if (nchunk <= 5) return w4 ? launch_1x1<4, 5, PRO, DB>(a, nchunk, s) : launch_1x1<2, 5, PRO, DB>(a, nchunk, s);
-    if (nchunk <= 9) return w4 ? launch_1x1<4, 9, PRO, DB>(a, nchunk, s) : launch_1x1<2, 9, PRO, DB>(a, nchunk, s);
-    return w4 ? launch_1x1<4, 16, PRO, DB>(a, nchunk, s) : launch_1x1<2, 16, PRO, DB>(a, nchunk, s);
-}
 template <bool PRO>
 int dispatch_1x1(const nps_conv3d_t& a, int nchunk, hipStream_t s) {
-    return a.nsrc > 2 ? dispatch_1x1_db<PRO, false>(a, nchunk, s) : dispatch_1x1_db<PRO, true>(a, nchunk, s);
+    const bool w4 = a.Cout > 64;
+    if (nchunk <= 5) return w4 ? launch_1x1<4, 5, PRO>(a, nchunk, s) : launch_1x1<2, 5, PRO>(a, nchunk, s);
+    if (nchunk <= 9) return w4 ? launch_1x1<4, 9, PRO>(a, nchunk, s) : launch_1x1<2, 9, PRO>(a, nchunk, s);
+    return w4 ? launch_1x1<4, 16, PRO>(a, nchunk, s) : launch_1x1<2, 16, PRO>(a, nchunk, s);
 }
 
 template <typename T, int K, int S, int TH, bool SIMPLE>

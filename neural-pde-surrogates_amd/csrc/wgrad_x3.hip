@@ -740,13 +740,6 @@ __global__ void wgrad_fold_kernel(const float* __restrict__ w, float* __restrict
 // profiles/r6/experiments/train_b2_knob_sweep.jsonl; 1024 and a larger minimum split were slower)
 inline long wx_wgs(const nps_wgrad_t& p) { return (long)p.B * p.Ha * p.Wa <= 200000 ? 256 : 512; }
 constexpr long WX_MINT = 8;  // minimum pixel tiles per split
-// dev knob NPS_WX_SPLIT8=1: 8..15 splits rounded down to 8, so the XCD-aware order (splits % 8 == 0) applies to the
-// small grids too (B = 2: 12 splits of the 21 (m, n) tiles of a 192 x 388 weight, whose work-groups otherwise spread
-// each split's pixels over every XCD's L2)
-const int g_wx_split8 = [] {
-    const char* e = std::getenv("NPS_WX_SPLIT8");
-    return (e != nullptr && e[0] == '1') ? 1 : 0;
-}();
 // dev knob NPS_WX_REMAP=0: the plain (tile-fastest) work-group order
 const int g_wx_remap = [] {
     const char* e = std::getenv("NPS_WX_REMAP");
@@ -766,7 +759,7 @@ int launch_wgrad_x3(const nps_wgrad_t& p, const float* ar, const float* xr, floa
     long splits = wx_wgs(p) / base;
     const long max_splits = (ntiles + WX_MINT - 1) / WX_MINT;
     if (splits > max_splits) splits = max_splits;
-    if (splits >= 16 || (g_wx_split8 && splits >= 8)) splits &= ~7L;  // a multiple of 8: the XCD-aware tile order (kernel comment)
+    if (splits >= 16) splits &= ~7L;  // a multiple of 8: the XCD-aware tile order (kernel comment)
     if (splits < 1) splits = 1;
     const int per = (int)((ntiles + splits - 1) / splits);
     const long used = (ntiles + per - 1) / per;  // splits that own tiles (the rest exit at once)
@@ -807,7 +800,7 @@ int launch_wgrad1_wide(const nps_wgrad_t& p, const float* ar, const float* xr, f
     long splits = wx_wgs(p) / base;  // two work-groups per CU in turn (LDS: 120 KiB each, one resident)
     const long max_splits = (ntiles + WX_MINT - 1) / WX_MINT;
     if (splits > max_splits) splits = max_splits;
-    if (splits >= 16 || (g_wx_split8 && splits >= 8)) splits &= ~7L;
+    if (splits >= 16) splits &= ~7L;
     if (splits < 1) splits = 1;
     const int per = (int)((ntiles + splits - 1) / splits);
     const long used = (ntiles + per - 1) / per;
@@ -846,7 +839,7 @@ int launch_wgrad2_wide(const nps_wgrad_t& p, const float* ar, const float* xr, f
     long splits = wx_wgs(p) / base;
     const long max_splits = (ntiles + WX_MINT - 1) / WX_MINT;
     if (splits > max_splits) splits = max_splits;
-    if (splits >= 16 || (g_wx_split8 && splits >= 8)) splits &= ~7L;
+    if (splits >= 16) splits &= ~7L;
     if (splits < 1) splits = 1;
     const int per = (int)((ntiles + splits - 1) / splits);
     const long used = (ntiles + per - 1) / per;
