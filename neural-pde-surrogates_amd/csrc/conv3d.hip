@@ -980,17 +980,19 @@ int launch_1x1(const nps_conv3d_t& a, int nchunk, hipStream_t s) {
     const long ntv = (nvox + 31) / 32;
     // one round of resident work-groups (occupancy x CUs) over the whole grid, split over the samples; at most
     // one tile per wave
-    static int resident = 0;  // (per instantiation: sized for the first launch's LDS)
-    if (resident == 0) {
-        int dev = 0, ncu = 0, occ = 0;
+    static int ncu = 0;
+    static int occ_by_chunks[NCH + 1] = {};  // resident work-groups per CU, per K-step count (the LDS it takes)
+    if (ncu == 0) {
+        int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
             ncu = 256;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, conv3d_1x1_kernel<NCB, NCH, PRO>, 256, lds) !=
-                hipSuccess || occ <= 0)
-            occ = 2;
-        resident = ncu * occ;
     }
+    int& occ = occ_by_chunks[nchunk];
+    if (occ == 0 && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, conv3d_1x1_kernel<NCB, NCH, PRO>, 256, lds) !=
+                         hipSuccess || occ <= 0))
+        occ = 2;
+    const long resident = (long)ncu * occ;
     long per = (resident + a.B - 1) / a.B;
     if (per > (ntv + 3) / 4) per = (ntv + 3) / 4;
     conv3d_1x1_kernel<NCB, NCH, PRO><<<dim3((unsigned)per, (unsigned)a.B), 256, lds, s>>>(a, nchunk);
