@@ -154,3 +154,25 @@ def test_fused_synthesis_arguments_are_checked_on_the_host():
     assert ops.spectral_fusable(256, 10, 192) == (ops.FUSE_IDFT and ops.CONV_PRECISION == ops.PREC_X3F16)
     assert not ops.spectral_fusable(200, 10, 192) and not ops.spectral_fusable(256, 17, 192)
     assert not ops.spectral_fusable(256, 10, 225)
+
+
+def test_wgrad_workspace_holds_the_bias_row():
+    """nps_wgrad_x3_ws_floats: the split-K partials [KH*KW][M][N] plus the bias-gradient row [M] (nps_wgrad_t.db)."""
+    import nps_hip
+    lib = nps_hip.lib
+    for M, N, k in [(192, 388, 3), (196, 192, 1), (40, 768, 2)]:
+        assert lib.nps_wgrad_x3_ws_floats(M, N, k, k) == M * N * k * k + M
+
+
+def test_fp32_wgrad_refuses_the_bias_row():
+    """The exact-fp32 weight gradient computes no bias gradient: a non-NULL db is an error, not a silent skip."""
+    import ctypes
+    import nps_hip
+    p = nps_hip.WgradArgs()
+    p.a, p.B, p.Ha, p.Wa, p.M = 0x1000, 1, 4, 4, 8
+    p.x, p.Hx, p.Wx, p.N = 0x2000, 4, 4, 8
+    p.KH = p.KW = 3
+    p.dil, p.pad_y, p.pad_x, p.circ, p.g = 2, 1, 1, 0, 0x3000
+    p.db = 0x4000
+    assert nps_hip.lib.nps_conv2d_wgrad(ctypes.byref(p), None) < 0
+    assert b"bias gradient" in nps_hip.lib.nps_last_error()

@@ -117,6 +117,12 @@ WGRAD_X3_CASES = [
     (2, 192, 768, 2, 0, 0, 33, 31, 1.0, 1.0),
     (1, 100, 136, 2, 1, 0, 19, 21, 1e-4, 1e3),
     (2, 132, 80, 2, 0, 1, 20, 24, 1.0, 1.0),
+    # N tails of <= 8 channels past the 64-channel tiles on wgrad_tail_kernel (the 388 / 196-channel U-Net frames):
+    # padding, circular extension, 2x2 with an 8-channel tail, range
+    (2, 192, 388, 3, 1, 0, 29, 31, 1.0, 1.0),
+    (2, 64, 68, 3, 0, 1, 22, 26, 1e-4, 1e3),
+    (1, 48, 136, 2, 1, 0, 18, 21, 1.0, 1.0),
+    (2, 40, 72, 3, 1, 0, 16, 19, 1.5e5, 1e-3),
 ]
 
 
@@ -616,3 +622,30 @@ def test_conv1x1_channel_groups_vs_fp64(cout):
     y = ops.conv2d([ops.Src(x.float().to(DEV))], (H, W), wp, b.float().to(DEV), cout, 1, 1,
                    addends=(add.float().to(DEV),))
     assert rel_l2(y.cpu().double(), ref) < TOL
+
+
+def test_wgrad_x3_bias_row_accumulates_like_g():
+    """nps_conv2d_wgrad_x3 (+= mode) through ctypes: db follows g's semantics — a second launch adds into it."""
+    import ctypes
+    from nps_hip import WgradArgs, lib, ops
+    from nps_hip import autograd as ad
+    torch.manual_seed(23)
+    B, H, W, M, N = 2, 17, 21, 64, 36
+    a = torch.randn(B, H, W, M, device=DEV)
+    x = torch.randn(B, H, W, N, device=DEV)
+    g = torch.zeros(M, N, 3, 3, device=DEV)
+    db = torch.zeros(M, device=DEV)
+    p = WgradArgs()
+    p.a, p.B, p.Ha, p.Wa, p.M = a.data_ptr(), B, H, W, M
+    p.x, p.Hx, p.Wx, p.N = x.data_ptr(), H, W, N
+    p.KH = p.KW = 3
+    p.dil, p.pad_y, p.pad_x, p.circ, p.g, p.db = 1, 1, 1, 0, g.data_ptr(), db.data_ptr()
+    ops.reserve_tags(a.device, 2)
+    ar, xr = ad._range_ptr(a), ad._range_ptr(x)
+    ws = torch.empty(lib.nps_wgrad_x3_ws_floats(M, N, 3, 3), device=DEV)
+    for _ in range(2):
+        assert lib.nps_conv2d_wgrad_x3(ctypes.byref(p), ar, xr, ws.data_ptr(), ops.stream_ptr()) == 0
+    ref = 2 * a.double().sum((0, 1, 2))
+    assert rel_l2(db.cpu().double(), ref.cpu()) < 1e-6
+    gref = 2 * ad.wgrad(a, x, 3, 3, pad=(1, 1))
+    assert rel_l2(g.cpu(), gref.cpu()) < 1e-6
