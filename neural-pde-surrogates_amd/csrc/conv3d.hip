@@ -143,13 +143,19 @@ struct Geo {
 };
 
 __device__ __forceinline__ int swz(int row) { return (row >> 3) & 1; }
+// 64 zero bytes: the LDS-DMA source of patch slots outside the frame
+__device__ __attribute__((aligned(64))) unsigned int c3d_zero16[16];
 
 // SIMPLE: one source covering the core frame at offset 0, channels a multiple of 16, no prologue (the
 // frame_pack3d output): a patch slot's address is fixed per tile (only the depth slice moves per stage), so
 // staging is one add + one 16-B load and one ds_write per slot
-template <typename T, int K, int S, int TH, bool SIMPLE>
-__global__ __launch_bounds__(256) void conv3d_kernel(const nps_conv3d_t a, int nchunk, int ntile) {
+// GLT (bf16 SIMPLE frames): the stage is copied global -> LDS by LDS-DMA (global_load_lds_dwordx4) instead of
+// through registers; the lane-linear LDS image keeps the half-swap swizzle by swapping the SOURCE halves, and
+// slots outside the frame read a zero line — no staging registers, no commit pass
+template <typename T, int K, int S, int TH, bool SIMPLE, bool GLT = false>
+__device__ __forceinline__ void conv3d_body(const nps_conv3d_t& a, int nchunk, int ntile) {
     using G = Geo<K, S, TH>;
+    constexpr bool GL = GLT && SIMPLE && sizeof(T) == 2;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     T* ring = reinterpret_cast<T*>(smem);
     float* gscale = reinterpret_cast<float*>(smem + 2 * G::BUF * sizeof(T));  // [nchunk*16] GN affine per channel
@@ -190,7 +196,7 @@ __global__ __launch_bounds__(256) void conv3d_kernel(const nps_conv3d_t a, int n
     const T* wbase = reinterpret_cast<const T*>(a.wpack) + (size_t)(z * ntile + tile) * K * nchunk * G::WTS;
     const int nstage = K * nchunk;
 
-    Vec8<T> pr[G::PPT], wr[G::WPT];
+    Vec8<T> pr[GL ? 1 : G::PPT], wr[GL ? 1 : G::WPT];
     // SIMPLE: per-slot element offset within a depth slice (-1: zero padding / past the patch)
     int soff[G::PPT];
     const T* sbase = reinterpret_cast<const T*>(a.src[0].ptr) + (size_t)b * a.Dc * a.Hc * a.Wc * a.Cin;
@@ -206,7 +212,8 @@ __global__ __launch_bounds__(256) void conv3d_kernel(const nps_conv3d_t a, int n
                 const int fh = h0 * S + prr, fw = w0 * S + pcc;
                 const int ch = fh < Hext ? ext_to_core(fh, a.Hc, a.circ, a.zpad) : -1;
                 const int cw = fw < Wext ? ext_to_core(fw, a.Wc, a.circ, a.zpad) : -1;
-                if (ch >= 0 && cw >= 0) soff[i] = (ch * a.Wc + cw) * a.Cin + half * 8;
+                // (GL: the slot's LDS half holds channel half half ^ swz(pix), as commit's swizzled store)
+                if (ch >= 0 && cw >= 0) soff[i] = (ch * a.Wc + cw) * a.Cin + (GL ? (half ^ swz(pix)) : half) * 8;
             }
         }
     }
@@ -281,6 +288,37 @@ __global__ __launch_bounds__(256) void conv3d_kernel(const nps_conv3d_t a, int n
         }
     };
 
+    // GL: stage st -> ring buffer buf by LDS-DMA; wave w's instruction i fills slots [256 i + 64 w, + 64)
+    auto fetch_gl = [&](int st, int buf) {
+        if constexpr (GL) {
+            const int kd = st / nchunk, chunk = st - kd * nchunk;
+            const int cd = ext_to_core(md * S + kd, a.Dc, a.circ, a.zpad);
+            const T* sp = sbase + (size_t)(cd < 0 ? 0 : cd) * slice + chunk * 16;
+            T* P = ring + buf * G::BUF;
+#pragma unroll
+            for (int i = 0; i < G::PPT; ++i) {
+                const int idx = tid + 256 * i;
+                if (256 * i + 64 * wave < G::NPP && idx < G::NPP) {
+                    const void* src = (cd >= 0 && soff[i] >= 0) ? (const void*)(sp + soff[i]) : (const void*)c3d_zero16;
+                    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(P + (256 * i + 64 * wave) * 8),
+                                                     16, 0, 0);
+                }
+            }
+            const T* wsrc = wbase + (size_t)st * G::WTS;
+            T* Wl = P + G::PATCH;
+#pragma unroll
+            for (int i = 0; i < G::WPT; ++i) {
+                const int idx = tid + 256 * i;
+                if (256 * i + 64 * wave < G::NWP && idx < G::NWP) {
+                    const int half = idx & 1, row = idx >> 1;
+                    __builtin_amdgcn_global_load_lds((const void*)(wsrc + row * 16 + ((half ^ swz(row & 63)) * 8)),
+                                                     (__attribute__((address_space(3))) void*)(Wl + (256 * i + 64 * wave) * 8),
+                                                     16, 0, 0);
+                }
+            }
+        }
+    };
+
     f32x16 acc[2][G::RW];
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb)
@@ -289,13 +327,22 @@ __global__ __launch_bounds__(256) void conv3d_kernel(const nps_conv3d_t a, int n
 #pragma unroll
             for (int q = 0; q < 16; ++q) acc[cb][r][q] = 0.f;
 
-    fetch(0);
-    commit(0, 0);
+    if constexpr (GL) {
+        fetch_gl(0, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+        fetch(0);
+        commit(0, 0);
+    }
     __syncthreads();
     const int col = lane & 31, hl = lane >> 5;
     for (int st = 0; st < nstage; ++st) {
         const int buf = st & 1;
-        if (st + 1 < nstage) fetch(st + 1);
+        if constexpr (GL) {
+            if (st + 1 < nstage) fetch_gl(st + 1, buf ^ 1);
+        } else {
+            if (st + 1 < nstage) fetch(st + 1);
+        }
         const T* P = ring + buf * G::BUF;
         const T* Wl = P + G::PATCH;
 #pragma unroll
@@ -344,7 +391,11 @@ __global__ __launch_bounds__(256) void conv3d_kernel(const nps_conv3d_t a, int n
                 }
             }
         }
-        if (st + 1 < nstage) commit(st + 1, buf ^ 1);
+        if constexpr (GL) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of stage st + 1 has landed
+        } else {
+            if (st + 1 < nstage) commit(st + 1, buf ^ 1);
+        }
         __syncthreads();
     }
 
@@ -471,6 +522,17 @@ __global__ __launch_bounds__(256) void conv3d_kernel(const nps_conv3d_t a, int n
             atomicAdd(q + 1, (red[1] + red[3]) + (red[5] + red[7]));
         }
     }
+}
+
+template <typename T, int K, int S, int TH, bool SIMPLE, bool GLT = false>
+__global__ __launch_bounds__(256) void conv3d_kernel(const nps_conv3d_t a, int nchunk, int ntile) {
+    conv3d_body<T, K, S, TH, SIMPLE, GLT>(a, nchunk, ntile);
+}
+// (dev variant: the same body held to two waves per SIMD, for register-heavy tile shapes)
+template <typename T, int K, int S, int TH, bool SIMPLE, bool GLT = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void conv3d_kernel_o2(const nps_conv3d_t a,
+                                                                                             int nchunk, int ntile) {
+    conv3d_body<T, K, S, TH, SIMPLE, GLT>(a, nchunk, ntile);
 }
 
 // wpack[(((((z*ntile + tile)*K + kd)*nchunk + chunk)*K*K + tap)*64 + col)*16 + k]
@@ -1008,21 +1070,23 @@ int dispatch_1x1(const nps_conv3d_t& a, int nchunk, hipStream_t s) {
     return w4 ? launch_1x1<4, 16, PRO>(a, nchunk, s) : launch_1x1<2, 16, PRO>(a, nchunk, s);
 }
 
-template <typename T, int K, int S, int TH, bool SIMPLE>
+template <typename T, int K, int S, int TH, bool SIMPLE, bool O2 = false, bool GLT = false>
 int launch(const nps_conv3d_t& a, int nchunk, int ntile, hipStream_t s) {
+    auto kern = conv3d_kernel<T, K, S, TH, SIMPLE, GLT>;
+    if constexpr (O2) kern = conv3d_kernel_o2<T, K, S, TH, SIMPLE, GLT>;
     using G = Geo<K, S, TH>;
     const size_t lds = 2 * (size_t)G::BUF * sizeof(T) + 2 * (size_t)nchunk * 16 * sizeof(float);
     NPS_CHECK_ARG(lds <= 160 * 1024, "conv3d: %zu B of LDS (Cin too large for the GroupNorm table)", lds);
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)conv3d_kernel<T, K, S, TH, SIMPLE>,
+        (void)hipFuncSetAttribute((const void*)kern,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = true;
     }
     const long ntiles = (long)a.B * a.Dout * ((a.Hout + TH - 1) / TH) * ((a.Wout + 31) / 32);
     NPS_CHECK_ARG(ntiles < (1L << 31), "conv3d: grid too large");
     const dim3 grid((unsigned)ntiles, (unsigned)ntile, a.transposed ? 8u : 1u);
-    conv3d_kernel<T, K, S, TH, SIMPLE><<<grid, 256, lds, s>>>(a, nchunk, ntile);
+    kern<<<grid, 256, lds, s>>>(a, nchunk, ntile);
     NPS_CHECK_LAUNCH("conv3d");
     return 0;
 }
@@ -1036,6 +1100,25 @@ bool simple_frame(const nps_conv3d_t& a) {
 template <typename T>
 int dispatch(const nps_conv3d_t& a, int nchunk, int ntile, hipStream_t s) {
     const bool sim = simple_frame(a);
+    // dev knob NPS_C3D_TH16=1 / 2 / 3 / 5: 16-row tiles (2: two waves per SIMD; 3: LDS-DMA staging; 5: both) —
+    // measured slower or no faster than the 8-row LDS-DMA default (profiles/r6/experiments/c5_conv3d_glds_ab.txt)
+    static int th16 = -1;
+    // NPS_C3D_GLDS=0: register-staged 8-row tiles instead of the LDS-DMA default (bf16 3x3x3 stride-1 fast path)
+    static int glds = -1;
+    if (th16 < 0) {
+        const char* e = std::getenv("NPS_C3D_TH16");
+        th16 = (e != nullptr && e[0] >= '1' && e[0] <= '5' && e[0] != '4') ? e[0] - '0' : 0;
+        const char* g = std::getenv("NPS_C3D_GLDS");
+        glds = (g != nullptr && g[0] == '0') ? 0 : 1;
+    }
+    if constexpr (sizeof(T) == 2)
+        if (a.K == 3 && a.stride == 1 && sim) {
+            if (th16 == 1) return launch<T, 3, 1, 16, true>(a, nchunk, ntile, s);
+            if (th16 == 2) return launch<T, 3, 1, 16, true, true>(a, nchunk, ntile, s);
+            if (th16 == 3) return launch<T, 3, 1, 16, true, false, true>(a, nchunk, ntile, s);
+            if (th16 == 5) return launch<T, 3, 1, 16, true, true, true>(a, nchunk, ntile, s);
+            if (glds) return launch<T, 3, 1, 8, true, false, true>(a, nchunk, ntile, s);
+        }
     if (a.K == 3 && a.stride == 1)
         return sim ? launch<T, 3, 1, 8, true>(a, nchunk, ntile, s) : launch<T, 3, 1, 8, false>(a, nchunk, ntile, s);
     if (a.K == 3 && a.stride == 2)

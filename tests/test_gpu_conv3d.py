@@ -311,3 +311,53 @@ def test_conv3d_1x1x1_bf16_streaming_prologue_epilogue():
     assert rel_l2(_ncdhw(out), F.conv3d(n, _rt(w, dt), b.double()) + _rt(base, dt)) < 1e-2
     got = ops._stats_sum([st], B, ops.new_stats(B, out, 1)).cpu()[:, 0]
     torch.testing.assert_close(got, ops.gn_stats3d([ops.Src3(out)], dhw, 1).cpu()[:, 0], rtol=1e-5, atol=1e-2)
+
+
+# the bf16 3x3x3 stride-1 fast path (one 16-channel-aligned source, no prologue): stage copies by LDS-DMA with the
+# half-swap swizzle on the source address and a zero line for the padding (conv3d.hip GLT); 1 / 3 / 5 channel
+# chunks, one or two 64-channel co tiles, zero / circular / both paddings, odd extents (row and column tails)
+FAST_CASES = [(16, 40, 0, 1, (2, 5, 9, 37)), (48, 64, 1, 0, (1, 6, 17, 33)), (80, 96, 1, 1, (2, 4, 8, 70)),
+              (64, 64, 0, 0, (1, 3, 12, 64))]
+
+
+def _fast_case(cin, cout, circ, zpad, shape):
+    from nps_hip import ops
+    torch.manual_seed(0)
+    B, D, H, W = shape
+    x = torch.randn(B, cin, D, H, W)
+    w = torch.randn(cout, cin, 3, 3, 3) * 0.05
+    b = torch.randn(cout) * 0.1
+    y = ops.conv3d([ops.Src3(_ndhwc(x, torch.bfloat16))], (D, H, W), ops.pack_conv3d_weight(w.to(DEV), bf16=True),
+                   b.to(DEV), cout, 3, circ=circ, zpad=zpad)
+    return x, w, b, y
+
+
+@pytest.mark.parametrize("cin,cout,circ,zpad,shape", FAST_CASES)
+def test_conv3d_bf16_fast_path_lds_dma(cin, cout, circ, zpad, shape):
+    x, w, b, y = _fast_case(cin, cout, circ, zpad, shape)
+    xr = _rt(x, torch.bfloat16)
+    if circ:
+        xr = F.pad(xr, (circ,) * 6, mode="circular")
+    if zpad:
+        xr = F.pad(xr, (zpad,) * 6)
+    ref = F.conv3d(xr, _rt(w, torch.bfloat16), b.double())
+    assert rel_l2(_ncdhw(y), ref) < TOL[torch.bfloat16]
+
+
+def test_conv3d_bf16_fast_path_lds_dma_matches_register_staging(tmp_path):
+    """The LDS-DMA staging changes only how a stage reaches LDS: the same image, the same MFMA order — the output
+    is bit-identical to the register-staged kernel (NPS_C3D_GLDS=0, read once per process: a child process)."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    f = tmp_path / "staged.pt"
+    code = (f"import sys, torch; sys.path[:0] = [{here!r}, {os.path.dirname(here)!r}, "
+            f"{os.path.join(os.path.dirname(here), 'neural-pde-surrogates_amd')!r}]\n"
+            "import test_gpu_conv3d as t\n"
+            f"torch.save([t._fast_case(*c)[3].cpu() for c in t.FAST_CASES], {str(f)!r})\n")
+    env = dict(os.environ, NPS_C3D_GLDS="0")
+    subprocess.run([sys.executable, "-c", code], env=env, check=True, timeout=240)
+    staged = torch.load(f, weights_only=True)
+    for c, ys in zip(FAST_CASES, staged):
+        assert torch.equal(_fast_case(*c)[3].cpu(), ys), c
