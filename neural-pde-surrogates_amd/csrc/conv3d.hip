@@ -152,13 +152,17 @@ __device__ __attribute__((aligned(64))) unsigned int c3d_zero16[16];
 // GLT (bf16 SIMPLE frames): the stage is copied global -> LDS by LDS-DMA (global_load_lds_dwordx4) instead of
 // through registers; the lane-linear LDS image keeps the half-swap swizzle by swapping the SOURCE halves, and
 // slots outside the frame read a zero line — no staging registers, no commit pass
-template <typename T, int K, int S, int TH, bool SIMPLE, bool GLT = false>
+// SB (with GLT): ONE stage buffer — load, barrier, compute, barrier — so a work-group needs half the LDS and three
+// fit a CU: each exposes its own load latency, the other two keep the MFMA pipe fed
+template <typename T, int K, int S, int TH, bool SIMPLE, bool GLT = false, bool SB = false>
 __device__ __forceinline__ void conv3d_body(const nps_conv3d_t& a, int nchunk, int ntile) {
     using G = Geo<K, S, TH>;
     constexpr bool GL = GLT && SIMPLE && sizeof(T) == 2;
+    static_assert(!SB || GLT, "single stage buffer: LDS-DMA staging only");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     T* ring = reinterpret_cast<T*>(smem);
-    float* gscale = reinterpret_cast<float*>(smem + 2 * G::BUF * sizeof(T));  // [nchunk*16] GN affine per channel
+    // [nchunk*16] GN affine per channel
+    float* gscale = reinterpret_cast<float*>(smem + (SB ? 1 : 2) * G::BUF * sizeof(T));
     float* gshift = gscale + nchunk * 16;
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -337,8 +341,9 @@ __device__ __forceinline__ void conv3d_body(const nps_conv3d_t& a, int nchunk, i
     __syncthreads();
     const int col = lane & 31, hl = lane >> 5;
     for (int st = 0; st < nstage; ++st) {
-        const int buf = st & 1;
-        if constexpr (GL) {
+        const int buf = SB ? 0 : (st & 1);
+        if constexpr (SB) {
+        } else if constexpr (GL) {
             if (st + 1 < nstage) fetch_gl(st + 1, buf ^ 1);
         } else {
             if (st + 1 < nstage) fetch(st + 1);
@@ -391,7 +396,13 @@ __device__ __forceinline__ void conv3d_body(const nps_conv3d_t& a, int nchunk, i
                 }
             }
         }
-        if constexpr (GL) {
+        if constexpr (SB) {
+            if (st + 1 < nstage) {
+                __syncthreads();  // every read of the buffer is done
+                fetch_gl(st + 1, 0);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+        } else if constexpr (GL) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of stage st + 1 has landed
         } else {
             if (st + 1 < nstage) commit(st + 1, buf ^ 1);
@@ -524,15 +535,21 @@ __device__ __forceinline__ void conv3d_body(const nps_conv3d_t& a, int nchunk, i
     }
 }
 
-template <typename T, int K, int S, int TH, bool SIMPLE, bool GLT = false>
+template <typename T, int K, int S, int TH, bool SIMPLE, bool GLT = false, bool SB = false>
 __global__ __launch_bounds__(256) void conv3d_kernel(const nps_conv3d_t a, int nchunk, int ntile) {
-    conv3d_body<T, K, S, TH, SIMPLE, GLT>(a, nchunk, ntile);
+    conv3d_body<T, K, S, TH, SIMPLE, GLT, SB>(a, nchunk, ntile);
 }
 // (dev variant: the same body held to two waves per SIMD, for register-heavy tile shapes)
 template <typename T, int K, int S, int TH, bool SIMPLE, bool GLT = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void conv3d_kernel_o2(const nps_conv3d_t a,
                                                                                              int nchunk, int ntile) {
     conv3d_body<T, K, S, TH, SIMPLE, GLT>(a, nchunk, ntile);
+}
+// (dev variant: one stage buffer held to four waves per SIMD — four work-groups per CU)
+template <typename T, int K, int S, int TH, bool SIMPLE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void conv3d_kernel_o4(const nps_conv3d_t a,
+                                                                                             int nchunk, int ntile) {
+    conv3d_body<T, K, S, TH, SIMPLE, true, true>(a, nchunk, ntile);
 }
 
 // wpack[(((((z*ntile + tile)*K + kd)*nchunk + chunk)*K*K + tap)*64 + col)*16 + k]
@@ -1070,12 +1087,13 @@ int dispatch_1x1(const nps_conv3d_t& a, int nchunk, hipStream_t s) {
     return w4 ? launch_1x1<4, 16, PRO>(a, nchunk, s) : launch_1x1<2, 16, PRO>(a, nchunk, s);
 }
 
-template <typename T, int K, int S, int TH, bool SIMPLE, bool O2 = false, bool GLT = false>
+template <typename T, int K, int S, int TH, bool SIMPLE, bool O2 = false, bool GLT = false, bool SB = false>
 int launch(const nps_conv3d_t& a, int nchunk, int ntile, hipStream_t s) {
-    auto kern = conv3d_kernel<T, K, S, TH, SIMPLE, GLT>;
-    if constexpr (O2) kern = conv3d_kernel_o2<T, K, S, TH, SIMPLE, GLT>;
+    auto kern = conv3d_kernel<T, K, S, TH, SIMPLE, GLT, SB>;
+    if constexpr (O2 && SB) kern = conv3d_kernel_o4<T, K, S, TH, SIMPLE>;
+    if constexpr (O2 && !SB) kern = conv3d_kernel_o2<T, K, S, TH, SIMPLE, GLT>;
     using G = Geo<K, S, TH>;
-    const size_t lds = 2 * (size_t)G::BUF * sizeof(T) + 2 * (size_t)nchunk * 16 * sizeof(float);
+    const size_t lds = (SB ? 1 : 2) * (size_t)G::BUF * sizeof(T) + 2 * (size_t)nchunk * 16 * sizeof(float);
     NPS_CHECK_ARG(lds <= 160 * 1024, "conv3d: %zu B of LDS (Cin too large for the GroupNorm table)", lds);
     static bool attr = false;
     if (!attr) {
@@ -1100,24 +1118,31 @@ bool simple_frame(const nps_conv3d_t& a) {
 template <typename T>
 int dispatch(const nps_conv3d_t& a, int nchunk, int ntile, hipStream_t s) {
     const bool sim = simple_frame(a);
-    // dev knob NPS_C3D_TH16=1 / 2 / 3 / 5: 16-row tiles (2: two waves per SIMD; 3: LDS-DMA staging; 5: both) —
-    // measured slower or no faster than the 8-row LDS-DMA default (profiles/r6/experiments/c5_conv3d_glds_ab.txt)
-    static int th16 = -1;
-    // NPS_C3D_GLDS=0: register-staged 8-row tiles instead of the LDS-DMA default (bf16 3x3x3 stride-1 fast path)
-    static int glds = -1;
+    // bf16 fast-path frames: stage copies by LDS-DMA into ONE stage buffer (SB) — three work-groups per CU (3x3x3),
+    // four for the register-light 2x2x2 phases (held to 4 waves per SIMD); NPS_C3D_GLDS=0: the register-staged
+    // double-buffered kernels.  Dev knob NPS_C3D_TH16 (3x3x3 stride 1, measured no faster, records in
+    // profiles/r6/experiments/c5_conv3d_glds_ab.txt): 1 / 2 / 3 / 5 16-row tiles (2: two waves per SIMD, 3: LDS-DMA,
+    // 5: both), 4 8-row LDS-DMA with two stage buffers, 7 the one-buffer kernel held to 4 waves per SIMD
+    static int th16 = -1, glds = 1;
     if (th16 < 0) {
         const char* e = std::getenv("NPS_C3D_TH16");
-        th16 = (e != nullptr && e[0] >= '1' && e[0] <= '5' && e[0] != '4') ? e[0] - '0' : 0;
+        th16 = (e != nullptr && e[0] >= '1' && e[0] <= '7' && e[0] != '6') ? e[0] - '0' : 0;
         const char* g = std::getenv("NPS_C3D_GLDS");
         glds = (g != nullptr && g[0] == '0') ? 0 : 1;
     }
     if constexpr (sizeof(T) == 2)
-        if (a.K == 3 && a.stride == 1 && sim) {
-            if (th16 == 1) return launch<T, 3, 1, 16, true>(a, nchunk, ntile, s);
-            if (th16 == 2) return launch<T, 3, 1, 16, true, true>(a, nchunk, ntile, s);
-            if (th16 == 3) return launch<T, 3, 1, 16, true, false, true>(a, nchunk, ntile, s);
-            if (th16 == 5) return launch<T, 3, 1, 16, true, true, true>(a, nchunk, ntile, s);
-            if (glds) return launch<T, 3, 1, 8, true, false, true>(a, nchunk, ntile, s);
+        if (sim && glds) {
+            if (a.K == 3 && a.stride == 1) {
+                if (th16 == 1) return launch<T, 3, 1, 16, true>(a, nchunk, ntile, s);
+                if (th16 == 2) return launch<T, 3, 1, 16, true, true>(a, nchunk, ntile, s);
+                if (th16 == 3) return launch<T, 3, 1, 16, true, false, true>(a, nchunk, ntile, s);
+                if (th16 == 4) return launch<T, 3, 1, 8, true, false, true>(a, nchunk, ntile, s);
+                if (th16 == 5) return launch<T, 3, 1, 16, true, true, true>(a, nchunk, ntile, s);
+                if (th16 == 7) return launch<T, 3, 1, 8, true, true, true, true>(a, nchunk, ntile, s);
+                return launch<T, 3, 1, 8, true, false, true, true>(a, nchunk, ntile, s);
+            }
+            if (a.K == 3 && a.stride == 2) return launch<T, 3, 2, 4, true, false, true, true>(a, nchunk, ntile, s);
+            if (a.K == 2 && a.stride == 1) return launch<T, 2, 1, 8, true, true, true, true>(a, nchunk, ntile, s);
         }
     if (a.K == 3 && a.stride == 1)
         return sim ? launch<T, 3, 1, 8, true>(a, nchunk, ntile, s) : launch<T, 3, 1, 8, false>(a, nchunk, ntile, s);

@@ -313,40 +313,48 @@ def test_conv3d_1x1x1_bf16_streaming_prologue_epilogue():
     torch.testing.assert_close(got, ops.gn_stats3d([ops.Src3(out)], dhw, 1).cpu()[:, 0], rtol=1e-5, atol=1e-2)
 
 
-# the bf16 3x3x3 stride-1 fast path (one 16-channel-aligned source, no prologue): stage copies by LDS-DMA with the
-# half-swap swizzle on the source address and a zero line for the padding (conv3d.hip GLT); 1 / 3 / 5 channel
-# chunks, one or two 64-channel co tiles, zero / circular / both paddings, odd extents (row and column tails)
-FAST_CASES = [(16, 40, 0, 1, (2, 5, 9, 37)), (48, 64, 1, 0, (1, 6, 17, 33)), (80, 96, 1, 1, (2, 4, 8, 70)),
-              (64, 64, 0, 0, (1, 3, 12, 64))]
+# the bf16 fast paths (one 16-channel-aligned source, no prologue): stage copies by LDS-DMA into one stage buffer
+# with the half-swap swizzle on the source address and a zero line for the padding (conv3d.hip GLT / SB): 3x3x3
+# stride 1 on 1 / 3 / 5 channel chunks, one or two 64-channel co tiles, zero / circular / both paddings, odd extents
+# (row and column tails); 3x3x3 stride 2; the 8 phases of the 3-D Upsample (2x2x2, circular + zero pad)
+FAST_CASES = [(16, 40, 0, 1, (2, 5, 9, 37), 3, 1, False), (48, 64, 1, 0, (1, 6, 17, 33), 3, 1, False),
+              (80, 96, 1, 1, (2, 4, 8, 70), 3, 1, False), (64, 64, 0, 0, (1, 3, 12, 64), 3, 1, False),
+              (64, 64, 0, 1, (1, 9, 19, 37), 3, 2, False), (48, 40, 1, 1, (2, 5, 7, 20), 2, 1, True)]
 
 
-def _fast_case(cin, cout, circ, zpad, shape):
+def _fast_case(cin, cout, circ, zpad, shape, k, stride, transposed):
     from nps_hip import ops
     torch.manual_seed(0)
     B, D, H, W = shape
     x = torch.randn(B, cin, D, H, W)
-    w = torch.randn(cout, cin, 3, 3, 3) * 0.05
+    w = torch.randn(*((cin, cout) if transposed else (cout, cin)), *(4 if transposed else k,) * 3) * 0.05
     b = torch.randn(cout) * 0.1
-    y = ops.conv3d([ops.Src3(_ndhwc(x, torch.bfloat16))], (D, H, W), ops.pack_conv3d_weight(w.to(DEV), bf16=True),
-                   b.to(DEV), cout, 3, circ=circ, zpad=zpad)
+    wp = ops.pack_conv3d_weight(w.to(DEV), transposed=transposed, bf16=True)
+    y = ops.conv3d([ops.Src3(_ndhwc(x, torch.bfloat16))], (D, H, W), wp, b.to(DEV), cout, k, stride=stride,
+                   transposed=transposed, circ=circ, zpad=zpad)
     return x, w, b, y
 
 
-@pytest.mark.parametrize("cin,cout,circ,zpad,shape", FAST_CASES)
-def test_conv3d_bf16_fast_path_lds_dma(cin, cout, circ, zpad, shape):
-    x, w, b, y = _fast_case(cin, cout, circ, zpad, shape)
+@pytest.mark.parametrize("cin,cout,circ,zpad,shape,k,stride,transposed", FAST_CASES)
+def test_conv3d_bf16_fast_path_lds_dma(cin, cout, circ, zpad, shape, k, stride, transposed):
+    x, w, b, y = _fast_case(cin, cout, circ, zpad, shape, k, stride, transposed)
     xr = _rt(x, torch.bfloat16)
     if circ:
         xr = F.pad(xr, (circ,) * 6, mode="circular")
-    if zpad:
-        xr = F.pad(xr, (zpad,) * 6)
-    ref = F.conv3d(xr, _rt(w, torch.bfloat16), b.double())
+    if transposed:  # the 3-D Upsample: circular pad, then ConvTranspose3d(k=4, s=2) (zpad 1 = its full extent)
+        ref = F.conv_transpose3d(xr, _rt(w, torch.bfloat16), b.double(), stride=2)
+    else:
+        if zpad:
+            xr = F.pad(xr, (zpad,) * 6)
+        ref = F.conv3d(xr, _rt(w, torch.bfloat16), b.double(), stride=stride)
+    assert y.shape[1:4] == ref.shape[2:]
     assert rel_l2(_ncdhw(y), ref) < TOL[torch.bfloat16]
 
 
 def test_conv3d_bf16_fast_path_lds_dma_matches_register_staging(tmp_path):
-    """The LDS-DMA staging changes only how a stage reaches LDS: the same image, the same MFMA order — the output
-    is bit-identical to the register-staged kernel (NPS_C3D_GLDS=0, read once per process: a child process)."""
+    """The LDS-DMA staging changes only how a stage reaches LDS (and how many work-groups share a CU): the same
+    image, the same MFMA order — the output is bit-identical to the register-staged double-buffered kernels
+    (NPS_C3D_GLDS=0, read once per process: a child process)."""
     import os
     import subprocess
     import sys

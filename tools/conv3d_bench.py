@@ -1,6 +1,6 @@
 """Micro-benchmark of one nps_conv3d launch shape (dev tool, not part of the product).
 
-python tools/conv3d_bench.py [--srcs 64,4 --cout 64 --k 1 --dhw 16,128,128 --b 8 --gn 0 --iters 20] [--save F]
+python tools/conv3d_bench.py [--srcs 64,4 --cout 64 --k 1 --stride 1 --dhw 16,128,128 --b 8 --gn 0 --iters 20] [--save F]
 Prints HIP-event time, algorithmic TB/s (sources + weights + output, bf16) and TFLOP/s.  --save writes the output
 tensor (torch.save) so two processes with different dev knobs (e.g. NPS_C3D_1X1=0) can be compared bit for bit
 with --compare F.
@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--dhw", default="16,128,128")
     ap.add_argument("--b", type=int, default=8)
     ap.add_argument("--gn", type=int, default=0)
+    ap.add_argument("--stride", type=int, default=1)
     ap.add_argument("--stats", type=int, default=1)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--save", default=None)
@@ -44,7 +45,8 @@ def main():
     st = ops.new_stats(a.b, srcs[0].t) if a.stats else None
 
     def run():
-        return ops.conv3d(srcs, dhw, wp, bias, a.cout, a.k, gn=gn, pre_act=1 if a.gn else 0, out_stats=st)
+        return ops.conv3d(srcs, dhw, wp, bias, a.cout, a.k, stride=a.stride, gn=gn, pre_act=1 if a.gn else 0,
+                          out_stats=st)
 
     y = run()
     torch.cuda.synchronize()
@@ -55,7 +57,7 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / a.iters
-    nv = a.b * (dhw[0] - a.k + 1) * (dhw[1] - a.k + 1) * (dhw[2] - a.k + 1)
+    nv = a.b * ((dhw[0] - a.k) // a.stride + 1) * ((dhw[1] - a.k) // a.stride + 1) * ((dhw[2] - a.k) // a.stride + 1)
     nbytes = 2 * (sum(s.t.numel() for s in srcs) + w.numel() + nv * a.cout)
     fl = 2.0 * nv * a.cout * cin * a.k ** 3
     knob = os.environ.get("NPS_C3D_1X1", "1")
