@@ -545,7 +545,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
                                                                                              int nchunk, int ntile) {
     conv3d_body<T, K, S, TH, SIMPLE, GLT>(a, nchunk, ntile);
 }
-// (dev variant: one stage buffer held to four waves per SIMD — four work-groups per CU)
+// (register-staged, held to four waves per SIMD: the 1x1x1 over several sources, a streaming kernel)
+template <typename T, int K, int S, int TH, bool SIMPLE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void conv3d_kernel_o4r(const nps_conv3d_t a,
+                                                                                              int nchunk, int ntile) {
+    conv3d_body<T, K, S, TH, SIMPLE>(a, nchunk, ntile);
+}
+// (one stage buffer held to four waves per SIMD — four work-groups per CU)
 template <typename T, int K, int S, int TH, bool SIMPLE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void conv3d_kernel_o4(const nps_conv3d_t a,
                                                                                              int nchunk, int ntile) {
@@ -749,7 +755,8 @@ __global__ __launch_bounds__(256) void gn_stats3d_kernel(const nps_conv3d_t a, i
 // and halo); the conv then reads a single 16-channel-aligned source (conv3d_kernel SIMPLE).  One item = 8
 // channels of one voxel (16-B loads / stores for bf16).
 template <typename T>
-__global__ __launch_bounds__(256) void frame_pack3d_kernel(const nps_conv3d_t a, T* __restrict__ out, int Cpad) {
+__global__ __launch_bounds__(256) void frame_pack3d_kernel(const nps_conv3d_t a, T* __restrict__ out, int Cpad,
+                                                           bool mflat_disabled) {
     __shared__ __attribute__((aligned(16))) float scl[512], sft[512];
     const int b = blockIdx.y;
     const bool gn = a.gn_stats != nullptr;
@@ -775,7 +782,23 @@ __global__ __launch_bounds__(256) void frame_pack3d_kernel(const nps_conv3d_t a,
     const nps_src3_t& s0 = a.src[0];
     const bool flat = a.nsrc == 1 && s0.off_d == 0 && s0.off_h == 0 && s0.off_w == 0 && s0.D == a.Dc &&
                       s0.H == a.Hc && s0.W == a.Wc && (s0.C & 3) == 0;
+    const bool mflat_off = mflat_disabled;
     const T* fb = reinterpret_cast<const T*>(s0.ptr) + (size_t)b * a.Dc * a.Hc * a.Wc * s0.C;
+    // several sources, each covering the frame exactly (no crop offset), C % 4 == 0: a 4-channel half of a piece
+    // lies in one source at the frame's voxel index — no coordinate decode, no per-source bounds checks
+    bool mflat = !flat && a.nsrc >= 2 && !mflat_off;
+    int mlo[NPS_MAX_SRC + 1];
+    const T* mb[NPS_MAX_SRC];
+    mlo[0] = 0;
+#pragma unroll
+    for (int si = 0; si < NPS_MAX_SRC; ++si) {
+        const nps_src3_t& q = a.src[si];
+        const bool in = si < a.nsrc;
+        mflat = mflat && (!in || (q.off_d == 0 && q.off_h == 0 && q.off_w == 0 && q.D == a.Dc && q.H == a.Hc &&
+                                  q.W == a.Wc && (q.C & 3) == 0));
+        mlo[si + 1] = mlo[si] + (in ? q.C : 0);
+        mb[si] = in ? reinterpret_cast<const T*>(q.ptr) + (size_t)b * a.Dc * a.Hc * a.Wc * q.C : nullptr;
+    }
     auto fetch = [&](Vec8<T>& v, int it) {
         const int vox = it / npc;
         const int pc = it - vox * npc;
@@ -784,6 +807,20 @@ __global__ __launch_bounds__(256) void frame_pack3d_kernel(const nps_conv3d_t a,
             const T* p = fb + (size_t)vox * s0.C + pc * 8;
             if (pc * 8 + 4 <= s0.C) v.load_half(0, p);
             if (pc * 8 + 8 <= s0.C) v.load_half(1, p + 4);
+            return;
+        }
+        if (mflat) {
+            v.zero();
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int c = pc * 8 + 4 * h;
+                if (c >= a.Cin) break;
+                const int si = c < mlo[1] ? 0 : (c < mlo[2] ? 1 : 2);
+                const int lo = si == 0 ? 0 : (si == 1 ? mlo[1] : mlo[2]);
+                const int sC = (si == 0 ? mlo[1] : (si == 1 ? mlo[2] : mlo[3])) - lo;
+                const T* p = (si == 0 ? mb[0] : (si == 1 ? mb[1] : mb[2])) + (size_t)vox * sC + (c - lo);
+                v.load_half(h, p);
+            }
             return;
         }
         const int cw = vox % a.Wc, r = vox / a.Wc;
@@ -1087,9 +1124,11 @@ int dispatch_1x1(const nps_conv3d_t& a, int nchunk, hipStream_t s) {
     return w4 ? launch_1x1<4, 16, PRO>(a, nchunk, s) : launch_1x1<2, 16, PRO>(a, nchunk, s);
 }
 
-template <typename T, int K, int S, int TH, bool SIMPLE, bool O2 = false, bool GLT = false, bool SB = false>
+template <typename T, int K, int S, int TH, bool SIMPLE, bool O2 = false, bool GLT = false, bool SB = false,
+          bool O4R = false>
 int launch(const nps_conv3d_t& a, int nchunk, int ntile, hipStream_t s) {
     auto kern = conv3d_kernel<T, K, S, TH, SIMPLE, GLT, SB>;
+    if constexpr (O4R) kern = conv3d_kernel_o4r<T, K, S, TH, SIMPLE>;
     if constexpr (O2 && SB) kern = conv3d_kernel_o4<T, K, S, TH, SIMPLE>;
     if constexpr (O2 && !SB) kern = conv3d_kernel_o2<T, K, S, TH, SIMPLE, GLT>;
     using G = Geo<K, S, TH>;
@@ -1150,8 +1189,19 @@ int dispatch(const nps_conv3d_t& a, int nchunk, int ntile, hipStream_t s) {
         return sim ? launch<T, 3, 2, 4, true>(a, nchunk, ntile, s) : launch<T, 3, 2, 4, false>(a, nchunk, ntile, s);
     if (a.K == 2 && a.stride == 1)
         return sim ? launch<T, 2, 1, 8, true>(a, nchunk, ntile, s) : launch<T, 2, 1, 8, false>(a, nchunk, ntile, s);
-    if (a.K == 1 && a.stride == 1)
+    if (a.K == 1 && a.stride == 1) {
+        // bf16 multi-source 1x1x1 (the C5 shortcuts over cat(h, skip, vb)): a streaming kernel, held to four waves
+        // per SIMD (four work-groups per CU, 128 VGPRs): (64, 64, 4) -> 64 at 16x128^2 471 -> 385 us, bit-identical
+        // (profiles/r6/experiments/c5_conv3d_glds_ab.txt); NPS_C3D_K1O4=0: three work-groups
+        static int k1 = -1;
+        if (k1 < 0) {
+            const char* e = std::getenv("NPS_C3D_K1O4");
+            k1 = (e != nullptr && e[0] == '0') ? 0 : 1;
+        }
+        if constexpr (sizeof(T) == 2)
+            if (!sim && k1) return launch<T, 1, 1, 8, false, false, false, false, true>(a, nchunk, ntile, s);
         return sim ? launch<T, 1, 1, 8, true>(a, nchunk, ntile, s) : launch<T, 1, 1, 8, false>(a, nchunk, ntile, s);
+    }
     NPS_CHECK_ARG(false, "conv3d: K=%d stride=%d not supported (K in {1,2,3}, stride 2 only for K=3)", a.K, a.stride);
 }
 
@@ -1233,10 +1283,15 @@ extern "C" int nps_frame_pack3d(const nps_conv3d_t* ap, void* out, int Cpad, voi
     const long nb = (nitem + 2047) / 2048 < 1024 ? (nitem + 2047) / 2048 : 1024;
     hipStream_t s = (hipStream_t)stream;
     const dim3 grid((unsigned)(nb > 0 ? nb : 1), (unsigned)a.B);
+    static int mflat_off = -1;  // dev knob NPS_PACK3D_MFLAT=0: multi-source frames through the general decode
+    if (mflat_off < 0) {
+        const char* e = std::getenv("NPS_PACK3D_MFLAT");
+        mflat_off = (e != nullptr && e[0] == '0') ? 1 : 0;
+    }
     if (a.bf16)
-        frame_pack3d_kernel<bf16_t><<<grid, 256, 0, s>>>(a, reinterpret_cast<bf16_t*>(out), Cpad);
+        frame_pack3d_kernel<bf16_t><<<grid, 256, 0, s>>>(a, reinterpret_cast<bf16_t*>(out), Cpad, mflat_off != 0);
     else
-        frame_pack3d_kernel<float><<<grid, 256, 0, s>>>(a, reinterpret_cast<float*>(out), Cpad);
+        frame_pack3d_kernel<float><<<grid, 256, 0, s>>>(a, reinterpret_cast<float*>(out), Cpad, mflat_off != 0);
     NPS_CHECK_LAUNCH("frame_pack3d");
     return 0;
 }

@@ -351,10 +351,47 @@ def test_conv3d_bf16_fast_path_lds_dma(cin, cout, circ, zpad, shape, k, stride, 
     assert rel_l2(_ncdhw(y), ref) < TOL[torch.bfloat16]
 
 
+# multi-source frames: the bf16 1x1x1 over three sources (generic kernel at four waves per SIMD) and the GroupNorm +
+# GELU frame pack — flat (every source covers the frame at offset 0: no coordinate decode) and cropped
+MULTI_CASES = [((64, 64, 4), ((0, 0, 0), (0, 0, 0), (0, 0, 0)), 64, (2, 5, 9, 37)),
+               ((64, 64, 4), ((0, 0, 0), (-1, 1, 0), (1, 0, 0)), 96, (1, 6, 17, 33)),
+               ((64, 4), ((0, 0, 0), (0, 0, 0)), 64, (2, 4, 8, 70)), ((4, 48, 12), ((0, 0, 0),) * 3, 40, (1, 3, 12, 64))]
+
+
+def _multi_case(chans, offs, cout, shape):
+    from nps_hip import ops
+    torch.manual_seed(1)
+    B, D, H, W = shape
+    dt = torch.bfloat16
+    xs = [torch.randn(B, c, *(n - 2 * oo for n, oo in zip((D, H, W), o))) * (1 + 0.5 * k)
+          for k, (c, o) in enumerate(zip(chans, offs))]
+    srcs = [ops.Src3(_ndhwc(x, dt), *o) for x, o in zip(xs, offs)]
+    cin = sum(chans)
+    w, b = torch.randn(cout, cin, 1, 1, 1) / cin ** 0.5, torch.randn(cout) * 0.1
+    y = ops.conv3d(srcs, (D, H, W), ops.pack_conv3d_weight(w.to(DEV), bf16=True), b.to(DEV), cout, 1)
+    gamma, beta = 1 + 0.2 * torch.randn(cin), 0.1 * torch.randn(cin)
+    gn = ops.GN(ops.gn_stats3d(srcs, (D, H, W), 2), gamma.to(DEV), beta.to(DEV), 2, 1e-5)
+    packed = ops.frame_pack3d(srcs, (D, H, W), gn, 1)
+    return xs, gamma, beta, y, packed
+
+
+@pytest.mark.parametrize("chans,offs,cout,shape", MULTI_CASES)
+def test_frame_pack3d_multi_source_vs_fp64(chans, offs, cout, shape):
+    xs, gamma, beta, _, packed = _multi_case(chans, offs, cout, shape)
+    B, D, H, W = shape
+    dt = torch.bfloat16
+    fr = _frame([(_rt(x, dt), o) for x, o in zip(xs, offs)], B, (D, H, W))
+    want = F.gelu(F.group_norm(fr, 2, gamma.double(), beta.double(), eps=1e-5))
+    cin = sum(chans)
+    assert packed.shape[-1] % 16 == 0 and bool((packed[..., cin:] == 0).all())
+    assert rel_l2(_ncdhw(packed[..., :cin]), want) < 1e-2
+
+
 def test_conv3d_bf16_fast_path_lds_dma_matches_register_staging(tmp_path):
     """The LDS-DMA staging changes only how a stage reaches LDS (and how many work-groups share a CU): the same
     image, the same MFMA order — the output is bit-identical to the register-staged double-buffered kernels
-    (NPS_C3D_GLDS=0, read once per process: a child process)."""
+    (NPS_C3D_GLDS=0, read once per process: a child process).  Likewise the four-waves-per-SIMD 1x1x1 and the flat
+    multi-source frame pack against their previous forms."""
     import os
     import subprocess
     import sys
@@ -363,9 +400,15 @@ def test_conv3d_bf16_fast_path_lds_dma_matches_register_staging(tmp_path):
     code = (f"import sys, torch; sys.path[:0] = [{here!r}, {os.path.dirname(here)!r}, "
             f"{os.path.join(os.path.dirname(here), 'neural-pde-surrogates_amd')!r}]\n"
             "import test_gpu_conv3d as t\n"
-            f"torch.save([t._fast_case(*c)[3].cpu() for c in t.FAST_CASES], {str(f)!r})\n")
-    env = dict(os.environ, NPS_C3D_GLDS="0")
+            f"torch.save([[t._fast_case(*c)[3].cpu() for c in t.FAST_CASES], "
+            f"[[r.cpu() for r in t._multi_case(*c)[3:]] for c in t.MULTI_CASES]], {str(f)!r})\n")
+    # (and the multi-source defaults: the 1x1x1 at three waves per SIMD, the frame pack through the general decode)
+    env = dict(os.environ, NPS_C3D_GLDS="0", NPS_C3D_K1O4="0", NPS_PACK3D_MFLAT="0")
     subprocess.run([sys.executable, "-c", code], env=env, check=True, timeout=240)
-    staged = torch.load(f, weights_only=True)
+    staged, multi = torch.load(f, weights_only=True)
     for c, ys in zip(FAST_CASES, staged):
         assert torch.equal(_fast_case(*c)[3].cpu(), ys), c
+    for c, (ys, ps) in zip(MULTI_CASES, multi):
+        _, _, _, y, p = _multi_case(*c)
+        assert torch.equal(y.cpu(), ys), c
+        assert torch.equal(p.cpu(), ps), c

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--b", type=int, default=8)
     ap.add_argument("--gn", type=int, default=0)
     ap.add_argument("--stride", type=int, default=1)
+    ap.add_argument("--pack-only", type=int, default=0, help="time nps_frame_pack3d of the frame alone")
     ap.add_argument("--stats", type=int, default=1)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--save", default=None)
@@ -45,6 +46,8 @@ def main():
     st = ops.new_stats(a.b, srcs[0].t) if a.stats else None
 
     def run():
+        if a.pack_only:
+            return ops.frame_pack3d(srcs, dhw, gn, 1 if a.gn else 0)
         return ops.conv3d(srcs, dhw, wp, bias, a.cout, a.k, stride=a.stride, gn=gn, pre_act=1 if a.gn else 0,
                           out_stats=st)
 
@@ -59,8 +62,14 @@ def main():
     ms = e0.elapsed_time(e1) / a.iters
     nv = a.b * ((dhw[0] - a.k) // a.stride + 1) * ((dhw[1] - a.k) // a.stride + 1) * ((dhw[2] - a.k) // a.stride + 1)
     nbytes = 2 * (sum(s.t.numel() for s in srcs) + w.numel() + nv * a.cout)
+    if a.pack_only:  # frame in, padded frame out
+        nbytes = 2 * (sum(s.t.numel() for s in srcs) + y.numel())
     fl = 2.0 * nv * a.cout * cin * a.k ** 3
     knob = os.environ.get("NPS_C3D_1X1", "1")
+    if a.pack_only:
+        print(f"frame_pack3d[bf16] srcs={a.srcs} dhw={a.dhw} B={a.b} gn={a.gn}: {ms * 1e3:.1f} us "
+              f"{nbytes / ms / 1e9:.2f} TB/s", flush=True)
+        fl = 0.0
     print(f"conv3d[bf16] srcs={a.srcs} cout={a.cout} k={a.k} dhw={a.dhw} B={a.b} gn={a.gn} knob={knob}: {ms * 1e3:.1f} us "
           f"{nbytes / ms / 1e9:.2f} TB/s {fl / ms / 1e9:.1f} TFLOP/s", flush=True)
     if a.save:
