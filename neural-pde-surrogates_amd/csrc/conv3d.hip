@@ -869,6 +869,103 @@ __global__ __launch_bounds__(256) void frame_pack3d_kernel(const nps_conv3d_t a,
     }
 }
 
+// frame_pack3d for frames whose sources all cover the frame at offset 0 (C % 4 == 0): thread = (voxel lane, piece
+// pc) with pc fixed for the thread's life, so the piece's source pointers, channel offsets and GroupNorm affine
+// (computed as frame_pack3d_kernel does) stay in registers and a voxel costs one multiply-add per half, the
+// loads, the affine + GELU and one coalesced 16-B store — no division per item, no LDS table.  Blocks of
+// npc x (256 / npc) threads (npc = Cpad / 8 <= 64).  Bit-identical to frame_pack3d_kernel.
+template <typename T>
+__global__ __launch_bounds__(256) void frame_pack3d_flat_kernel(const nps_conv3d_t a, T* __restrict__ out, int Cpad) {
+    const int npc = Cpad / 8, vpb = 256 / npc;
+    const int tid = threadIdx.x;
+    if (tid >= npc * vpb) return;  // (no barrier in this kernel)
+    const int pc = tid % npc, vl = tid / npc;
+    const int b = blockIdx.y;
+    const int nvox = a.Dc * a.Hc * a.Wc;
+    const bool gn = a.gn_stats != nullptr, tr = gn || a.pre_act != 0;
+    float sc[8], sh[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const int c = pc * 8 + e;
+        sc[e] = 1.f;
+        sh[e] = 0.f;
+        if (gn && c < a.Cin) {  // (frame_pack3d_kernel's table entry for channel c)
+            const int g = c / (a.Cin / a.gn_groups);
+            const double n = (double)a.Dc * a.Hc * a.Wc * (a.Cin / a.gn_groups);
+            const double mean = a.gn_stats[(b * a.gn_groups + g) * 2] / n;
+            const double var = fmax(a.gn_stats[(b * a.gn_groups + g) * 2 + 1] / n - mean * mean, 0.0);
+            const float rstd = (float)(1.0 / sqrt(var + (double)a.gn_eps));
+            sc[e] = a.gn_gamma[c] * rstd;
+            sh[e] = a.gn_beta[c] - (float)mean * sc[e];
+        }
+    }
+    // the piece's two 4-channel halves: this sample's source pointer at the half's first channel (null past Cin)
+    // and the source's channels per voxel; a whole 8-aligned piece of one source loads as one 16-B access
+    const T* hp[2] = {nullptr, nullptr};
+    int hC[2] = {0, 0};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int c = pc * 8 + 4 * h;
+        int lo = 0;
+#pragma unroll
+        for (int si = 0; si < NPS_MAX_SRC; ++si) {
+            if (si < a.nsrc) {
+                const nps_src3_t& q = a.src[si];
+                if (c < a.Cin && c >= lo && c < lo + q.C) {
+                    hp[h] = reinterpret_cast<const T*>(q.ptr) + (size_t)b * nvox * q.C + (c - lo);
+                    hC[h] = q.C;
+                }
+                lo += q.C;
+            }
+        }
+    }
+    const bool whole = hp[0] != nullptr && hp[1] == hp[0] + 4 && (hC[0] & 7) == 0 &&
+                       ((reinterpret_cast<size_t>(hp[0]) & 15) == 0);
+    T* ob = out + (size_t)b * nvox * Cpad + pc * 8;
+    auto fetch = [&](Vec8<T>& v, int vx) {
+        if (whole) {
+            v.load(hp[0] + (size_t)vx * hC[0]);
+            return;
+        }
+        v.zero();
+        if (hp[0] != nullptr) v.load_half(0, hp[0] + (size_t)vx * hC[0]);
+        if (hp[1] != nullptr) v.load_half(1, hp[1] + (size_t)vx * hC[1]);
+    };
+    auto put = [&](Vec8<T>& v, int vx) {
+        if (tr) {
+            float y[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) y[e] = fmaf(v.get(e), sc[e], sh[e]);
+            if (a.pre_act == 1) {
+#pragma unroll
+                for (int e = 0; e < 8; e += 2) {
+                    const nps::f32x2 g = nps::gelu_fast2(nps::f32x2{y[e], y[e + 1]});
+                    y[e] = g[0];
+                    y[e + 1] = g[1];
+                }
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v.set(e, pc * 8 + e < a.Cin ? y[e] : 0.f);
+        }
+        v.store(ob + (size_t)vx * Cpad);
+    };
+    constexpr int U = 4;
+    const int stride = gridDim.x * vpb;
+    int vx = blockIdx.x * vpb + vl;
+    for (; vx + (U - 1) * stride < nvox; vx += U * stride) {
+        Vec8<T> v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) fetch(v[u], vx + u * stride);
+#pragma unroll
+        for (int u = 0; u < U; ++u) put(v[u], vx + u * stride);
+    }
+    for (; vx < nvox; vx += stride) {
+        Vec8<T> v;
+        fetch(v, vx);
+        put(v, vx);
+    }
+}
+
 // 1x1x1 Conv3d on bf16 storage (K = 1, stride 1, no frame extension): the ResidualBlock shortcut over
 // cat(h, crop_Nd(skip), crop_Nd(vb)) and the U-Net's final GroupNorm + GELU + 1x1 (proc_unet_modern.py:84, :265,
 // :429).  A pointwise GEMM has no patch to share between output positions, and conv3d_kernel's 16-channel stages
@@ -1284,9 +1381,29 @@ extern "C" int nps_frame_pack3d(const nps_conv3d_t* ap, void* out, int Cpad, voi
     hipStream_t s = (hipStream_t)stream;
     const dim3 grid((unsigned)(nb > 0 ? nb : 1), (unsigned)a.B);
     static int mflat_off = -1;  // dev knob NPS_PACK3D_MFLAT=0: multi-source frames through the general decode
+    static int flat_on = 1;     // NPS_PACK3D_FLAT=0: offset-0 frames on frame_pack3d_kernel instead of the flat kernel
     if (mflat_off < 0) {
         const char* e = std::getenv("NPS_PACK3D_MFLAT");
         mflat_off = (e != nullptr && e[0] == '0') ? 1 : 0;
+        const char* f = std::getenv("NPS_PACK3D_FLAT");
+        flat_on = (f != nullptr && f[0] == '0') ? 0 : 1;
+    }
+    bool flat = flat_on && mflat_off == 0;
+    for (int i = 0; i < a.nsrc; ++i) {
+        const nps_src3_t& q = a.src[i];
+        flat = flat && q.off_d == 0 && q.off_h == 0 && q.off_w == 0 && q.D == a.Dc && q.H == a.Hc && q.W == a.Wc &&
+               (q.C & 3) == 0;
+    }
+    if (flat && Cpad / 8 <= 64) {
+        const long nvox = (long)a.Dc * a.Hc * a.Wc, vpb = 256 / (Cpad / 8);
+        const long nbv = (nvox + vpb * 8 - 1) / (vpb * 8) < 1024 ? (nvox + vpb * 8 - 1) / (vpb * 8) : 1024;
+        const dim3 fgrid((unsigned)(nbv > 0 ? nbv : 1), (unsigned)a.B);
+        if (a.bf16)
+            frame_pack3d_flat_kernel<bf16_t><<<fgrid, 256, 0, s>>>(a, reinterpret_cast<bf16_t*>(out), Cpad);
+        else
+            frame_pack3d_flat_kernel<float><<<fgrid, 256, 0, s>>>(a, reinterpret_cast<float*>(out), Cpad);
+        NPS_CHECK_LAUNCH("frame_pack3d");
+        return 0;
     }
     if (a.bf16)
         frame_pack3d_kernel<bf16_t><<<grid, 256, 0, s>>>(a, reinterpret_cast<bf16_t*>(out), Cpad, mflat_off != 0);
