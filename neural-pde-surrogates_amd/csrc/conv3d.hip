@@ -966,122 +966,6 @@ __global__ __launch_bounds__(256) void frame_pack3d_flat_kernel(const nps_conv3d
     }
 }
 
-// frame_pack3d for frames with crop offsets (sources C % 4 == 0, e.g. cat(h, crop_Nd(skip), crop_Nd(vb))): the
-// piece fixed per thread as in the flat kernel, and a block takes whole frame rows (d, h): each half's source row
-// (or none, where the row lies outside that source) is found once per row, a voxel costs one bounds check per half
-// and its loads.  Voxels outside a source read 0 and are normalised like the frame's other values (as
-// frame_pack3d_kernel).  Bit-identical to frame_pack3d_kernel.
-template <typename T>
-__global__ __launch_bounds__(256) void frame_pack3d_rows_kernel(const nps_conv3d_t a, T* __restrict__ out, int Cpad) {
-    const int npc = Cpad / 8, vpb = 256 / npc;
-    const int tid = threadIdx.x;
-    if (tid >= npc * vpb) return;  // (no barrier in this kernel)
-    const int pc = tid % npc, vl = tid / npc;
-    const int b = blockIdx.y;
-    const bool gn = a.gn_stats != nullptr, tr = gn || a.pre_act != 0;
-    float sc[8], sh[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        const int c = pc * 8 + e;
-        sc[e] = 1.f;
-        sh[e] = 0.f;
-        if (gn && c < a.Cin) {  // (frame_pack3d_kernel's table entry for channel c)
-            const int g = c / (a.Cin / a.gn_groups);
-            const double n = (double)a.Dc * a.Hc * a.Wc * (a.Cin / a.gn_groups);
-            const double mean = a.gn_stats[(b * a.gn_groups + g) * 2] / n;
-            const double var = fmax(a.gn_stats[(b * a.gn_groups + g) * 2 + 1] / n - mean * mean, 0.0);
-            const float rstd = (float)(1.0 / sqrt(var + (double)a.gn_eps));
-            sc[e] = a.gn_gamma[c] * rstd;
-            sh[e] = a.gn_beta[c] - (float)mean * sc[e];
-        }
-    }
-    // each half's source (-1: past Cin) and channel within it
-    int hs[2] = {-1, -1}, hc[2] = {0, 0};
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const int c = pc * 8 + 4 * h;
-        int lo = 0;
-#pragma unroll
-        for (int si = 0; si < NPS_MAX_SRC; ++si) {
-            if (si < a.nsrc) {
-                if (c < a.Cin && c >= lo && c < lo + a.src[si].C) {
-                    hs[h] = si;
-                    hc[h] = c - lo;
-                }
-                lo += a.src[si].C;
-            }
-        }
-    }
-    auto src_of = [&](int si) -> const nps_src3_t& { return si == 0 ? a.src[0] : (si == 1 ? a.src[1] : a.src[2]); };
-    const bool whole = hs[0] >= 0 && hs[1] == hs[0] && hc[1] == hc[0] + 4 && (hc[0] & 7) == 0 &&
-                       (src_of(hs[0]).C & 7) == 0;
-    const int nrow = a.Dc * a.Hc;
-    for (int r = blockIdx.x; r < nrow; r += gridDim.x) {
-        const int cd = r / a.Hc, ch = r - (r / a.Hc) * a.Hc;
-        // this row in each half's source: element offset of voxel w = 0 of the source row, its w range, channels
-        const T* rp[2] = {nullptr, nullptr};
-        int wlo[2] = {0, 0}, whi[2] = {0, 0}, sCh[2] = {0, 0};
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            if (hs[h] < 0) continue;
-            const nps_src3_t& S = src_of(hs[h]);
-            const int dd = cd - S.off_d, hh = ch - S.off_h;
-            if (dd < 0 || dd >= S.D || hh < 0 || hh >= S.H) continue;
-            rp[h] = reinterpret_cast<const T*>(S.ptr) + (((size_t)b * S.D + dd) * S.H + hh) * S.W * S.C + hc[h];
-            wlo[h] = S.off_w;
-            whi[h] = S.off_w + S.W;
-            sCh[h] = S.C;
-        }
-        T* orow = out + (((size_t)b * a.Dc + cd) * a.Hc + ch) * a.Wc * Cpad + pc * 8;
-        auto fetch = [&](Vec8<T>& v, int cw) {
-            if (whole) {
-                if (rp[0] != nullptr && cw >= wlo[0] && cw < whi[0]) {
-                    v.load(rp[0] + (size_t)(cw - wlo[0]) * sCh[0]);
-                    return;
-                }
-                v.zero();
-                return;
-            }
-            v.zero();
-#pragma unroll
-            for (int h = 0; h < 2; ++h)
-                if (rp[h] != nullptr && cw >= wlo[h] && cw < whi[h]) v.load_half(h, rp[h] + (size_t)(cw - wlo[h]) * sCh[h]);
-        };
-        auto put = [&](Vec8<T>& v, int cw) {
-            if (tr) {
-                float y[8];
-#pragma unroll
-                for (int e = 0; e < 8; ++e) y[e] = fmaf(v.get(e), sc[e], sh[e]);
-                if (a.pre_act == 1) {
-#pragma unroll
-                    for (int e = 0; e < 8; e += 2) {
-                        const nps::f32x2 g = nps::gelu_fast2(nps::f32x2{y[e], y[e + 1]});
-                        y[e] = g[0];
-                        y[e + 1] = g[1];
-                    }
-                }
-#pragma unroll
-                for (int e = 0; e < 8; ++e) v.set(e, pc * 8 + e < a.Cin ? y[e] : 0.f);
-            }
-            v.store(orow + (size_t)cw * Cpad);
-        };
-        constexpr int U = 4;
-        int cw = vl;
-        for (; cw + (U - 1) * vpb < a.Wc; cw += U * vpb) {
-            Vec8<T> v[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) fetch(v[u], cw + u * vpb);
-#pragma unroll
-            for (int u = 0; u < U; ++u) put(v[u], cw + u * vpb);
-        }
-        for (; cw < a.Wc; cw += vpb) {
-            Vec8<T> v;
-            fetch(v, cw);
-            put(v, cw);
-        }
-    }
-}
-
 // 1x1x1 Conv3d on bf16 storage (K = 1, stride 1, no frame extension): the ResidualBlock shortcut over
 // cat(h, crop_Nd(skip), crop_Nd(vb)) and the U-Net's final GroupNorm + GELU + 1x1 (proc_unet_modern.py:84, :265,
 // :429).  A pointwise GEMM has no patch to share between output positions, and conv3d_kernel's 16-channel stages
@@ -1509,23 +1393,6 @@ extern "C" int nps_frame_pack3d(const nps_conv3d_t* ap, void* out, int Cpad, voi
         const nps_src3_t& q = a.src[i];
         flat = flat && q.off_d == 0 && q.off_h == 0 && q.off_w == 0 && q.D == a.Dc && q.H == a.Hc && q.W == a.Wc &&
                (q.C & 3) == 0;
-    }
-    static int rows_on = -1;  // NPS_PACK3D_ROWS=0: frames with crop offsets on frame_pack3d_kernel's general path
-    if (rows_on < 0) {
-        const char* e = std::getenv("NPS_PACK3D_ROWS");
-        rows_on = (e != nullptr && e[0] == '0') ? 0 : 1;
-    }
-    bool c4 = true;
-    for (int i = 0; i < a.nsrc; ++i) c4 = c4 && (a.src[i].C & 3) == 0;
-    if (!flat && rows_on && mflat_off == 0 && c4 && Cpad / 8 <= 64) {
-        const long nrow = (long)a.Dc * a.Hc;
-        const dim3 rgrid((unsigned)(nrow < 4096 ? nrow : 4096), (unsigned)a.B);
-        if (a.bf16)
-            frame_pack3d_rows_kernel<bf16_t><<<rgrid, 256, 0, s>>>(a, reinterpret_cast<bf16_t*>(out), Cpad);
-        else
-            frame_pack3d_rows_kernel<float><<<rgrid, 256, 0, s>>>(a, reinterpret_cast<float*>(out), Cpad);
-        NPS_CHECK_LAUNCH("frame_pack3d");
-        return 0;
     }
     if (flat && Cpad / 8 <= 64) {
         const long nvox = (long)a.Dc * a.Hc * a.Wc, vpb = 256 / (Cpad / 8);

@@ -353,7 +353,7 @@ def test_conv3d_bf16_fast_path_lds_dma(cin, cout, circ, zpad, shape, k, stride, 
 
 # multi-source frames: the bf16 1x1x1 over three sources (generic kernel at four waves per SIMD) and the GroupNorm +
 # GELU frame pack — flat (every source covers the frame at offset 0: no coordinate decode) and cropped / zero-padded
-# sources (the row kernel: crop offsets of either sign on every axis)
+# sources (crop offsets of either sign on every axis: the general decode)
 MULTI_CASES = [((64, 64, 4), ((0, 0, 0), (0, 0, 0), (0, 0, 0)), 64, (2, 5, 9, 37)),
                ((64, 64, 4), ((0, 0, 0), (-1, 1, 0), (1, 0, 0)), 96, (1, 6, 17, 33)),
                ((64, 4), ((0, 0, 0), (0, 0, 0)), 64, (2, 4, 8, 70)), ((4, 48, 12), ((0, 0, 0),) * 3, 40, (1, 3, 12, 64)),
@@ -405,7 +405,7 @@ def test_conv3d_bf16_fast_path_lds_dma_matches_register_staging(tmp_path):
             f"torch.save([[t._fast_case(*c)[3].cpu() for c in t.FAST_CASES], "
             f"[[r.cpu() for r in t._multi_case(*c)[3:]] for c in t.MULTI_CASES]], {str(f)!r})\n")
     # (and the multi-source defaults: the 1x1x1 at three waves per SIMD, the frame pack through the general decode —
-    # NPS_PACK3D_MFLAT=0 also turns off the flat and row pack kernels)
+    # NPS_PACK3D_MFLAT=0 also turns off the flat pack kernel)
     env = dict(os.environ, NPS_C3D_GLDS="0", NPS_C3D_K1O4="0", NPS_PACK3D_MFLAT="0")
     subprocess.run([sys.executable, "-c", code], env=env, check=True, timeout=240)
     staged, multi = torch.load(f, weights_only=True)
