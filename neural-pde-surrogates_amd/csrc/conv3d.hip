@@ -143,6 +143,9 @@ struct Geo {
 };
 
 __device__ __forceinline__ int swz(int row) { return (row >> 3) & 1; }
+#ifndef NPS_PACK3D_U
+#define NPS_PACK3D_U 4  // pieces per thread in flight in the frame packs (dev builds: tools/build_variant.sh)
+#endif
 // 64 zero bytes: the LDS-DMA source of patch slots outside the frame
 __device__ __attribute__((aligned(64))) unsigned int c3d_zero16[16];
 
@@ -852,7 +855,7 @@ __global__ __launch_bounds__(256) void frame_pack3d_kernel(const nps_conv3d_t a,
         v.store(ob + (size_t)vox * Cpad + pc * 8);
     };
     // U pieces per thread: all loads issued before the first store (vmcnt retires loads and stores in order)
-    constexpr int U = 4;
+    constexpr int U = NPS_PACK3D_U;
     const int stride = gridDim.x * 256;
     int it = blockIdx.x * 256 + threadIdx.x;
     for (; it + (U - 1) * stride < nitem; it += U * stride) {
@@ -949,7 +952,7 @@ __global__ __launch_bounds__(256) void frame_pack3d_flat_kernel(const nps_conv3d
         }
         v.store(ob + (size_t)vx * Cpad);
     };
-    constexpr int U = 4;
+    constexpr int U = NPS_PACK3D_U;
     const int stride = gridDim.x * vpb;
     int vx = blockIdx.x * vpb + vl;
     for (; vx + (U - 1) * stride < nvox; vx += U * stride) {
