@@ -143,6 +143,12 @@ struct Geo {
 };
 
 __device__ __forceinline__ int swz(int row) { return (row >> 3) & 1; }
+#ifndef NPS_C3D_XCD
+// 3-D convs: work-group i (on XCD i % 8) takes tile (i % 8) * (n / 8) + i / 8, so each XCD's L2 sees a contiguous
+// run of tiles (whole slices, consecutive depths) instead of every 8th; a bijection, outputs unchanged.  C5 +1.1 %
+// with the A/B arms in both orders (profiles/r6/experiments/c5_conv3d_glds_ab.txt Pass 10); 0 in a dev build: off
+#define NPS_C3D_XCD 1
+#endif
 #ifndef NPS_PACK3D_U
 #define NPS_PACK3D_U 4  // pieces per thread in flight in the frame packs (dev builds: tools/build_variant.sh)
 #endif
@@ -171,6 +177,10 @@ __device__ __forceinline__ void conv3d_body(const nps_conv3d_t& a, int nchunk, i
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int ntw = (a.Wout + 31) / 32, nth = (a.Hout + TH - 1) / TH;
     int t = blockIdx.x;
+    if (NPS_C3D_XCD) {  // work-group i runs on XCD i % 8: give each XCD a contiguous run of tiles (L2 locality)
+        const int n = (int)gridDim.x, full = n & ~7;
+        if (t < full) t = (t & 7) * (full >> 3) + (t >> 3);
+    }
     const int tw = t % ntw; t /= ntw;
     const int th = t % nth; t /= nth;
     const int md = t % a.Dout;
